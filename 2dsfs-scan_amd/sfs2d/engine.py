@@ -1,0 +1,199 @@
+"""Host-side runtime over the C ABI: contexts, resident data sets, scan plans.
+
+One ``Engine`` per GPU (one process per GPU for multi-GPU runs).  A ``DeviceData`` is a packed
+SNP set resident in HBM; a ``Plan`` holds everything that depends on (data, scan parameters)
+and replays the kernels.  See include/sfs2d.h for the contract.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import _lib as L
+from .pack import PackedSNPs
+
+
+@dataclass
+class ScanConfig:
+    n1p: int
+    n2p: int
+    fold: bool = True
+    window_mode: int = L.WINDOW_BP
+    window: int = 20000
+    bg_mode: int = L.BG_PER_CHROM
+    ann_want: int = -1
+    start_position: Optional[int] = None
+    end_position: Optional[int] = None
+    prev_extra: bool = False
+
+    def params(self) -> L.Params:
+        p = L.Params()
+        p.n1p, p.n2p, p.fold = int(self.n1p), int(self.n2p), 1 if self.fold else 0
+        p.window_mode, p.window, p.bg_mode = int(self.window_mode), int(self.window), int(self.bg_mode)
+        p.ann_want = int(self.ann_want)
+        # Python ints of any size: clamp into the int64 range the kernel compares against
+        clamp = lambda v: max(-(1 << 62), min(1 << 62, int(v)))
+        p.has_start = 0 if self.start_position is None else 1
+        p.start_pos = 0 if self.start_position is None else clamp(self.start_position)
+        p.has_end = 0 if self.end_position is None else 1
+        p.end_pos = 0 if self.end_position is None else clamp(self.end_position)
+        p.flags = L.F_PREV_EXTRA if self.prev_extra else 0
+        return p
+
+
+class Engine:
+    _cache = {}
+
+    def __init__(self, device: int = 0):
+        self.lib = L.lib()
+        self.device = device
+        h = C.c_void_p()
+        rc = self.lib.sfs2d_ctx_create(device, C.byref(h))
+        if rc != 0:
+            raise L.Sfs2dError(rc, f"cannot create a HIP context on device {device} (no MI355X visible?)")
+        self.h = h
+
+    @classmethod
+    def get(cls, device: int = 0) -> "Engine":
+        e = cls._cache.get(device)
+        if e is None:
+            e = cls(device)
+            cls._cache[device] = e
+        return e
+
+    def check(self, rc):
+        if rc != 0:
+            msg = self.lib.sfs2d_last_error(self.h).decode()
+            if rc == L.E_KEY:
+                raise KeyError(msg)
+            raise L.Sfs2dError(rc, msg)
+
+    def set_stream(self, stream_handle: Optional[int]):
+        self.check(self.lib.sfs2d_ctx_set_stream(self.h, C.c_void_p(stream_handle) if stream_handle else None))
+
+    def upload(self, p: PackedSNPs) -> "DeviceData":
+        return DeviceData(self, p)
+
+    def wrap_device(self, d_counts: int, d_pos: int, d_ann: Optional[int], n: int, chrom_off: np.ndarray,
+                    chrom_last_pos: np.ndarray) -> "DeviceData":
+        return DeviceData(self, None, (d_counts, d_pos, d_ann, n, chrom_off, chrom_last_pos))
+
+    def bg_hist(self, data: "DeviceData", cfg: ScanConfig, chrom: int = -1):
+        n1, n2 = 2 * cfg.n1p, 2 * cfg.n2p
+        h2 = np.zeros((n1 + 1) * (n2 + 1), np.int64)
+        h1a = np.zeros(n1 + 1, np.int64)
+        h1b = np.zeros(n2 + 1, np.int64)
+        prm = cfg.params()
+        self.check(self.lib.sfs2d_bg_hist(self.h, data.h, C.byref(prm), int(chrom), L.ptr(h2), L.ptr(h1a),
+                                          L.ptr(h1b)))
+        return h2.reshape(n1 + 1, n2 + 1), h1a, h1b
+
+    def plan(self, data: "DeviceData", cfg: ScanConfig) -> "Plan":
+        return Plan(self, data, cfg)
+
+    def scan(self, data: "DeviceData", cfg: ScanConfig, bg=None) -> np.ndarray:
+        """One-shot scan; returns the window records (numpy structured array, WINDOW_DTYPE)."""
+        pl = Plan(self, data, cfg)
+        try:
+            if cfg.bg_mode == L.BG_SUPPLIED:
+                pl.set_background(*bg)
+            pl.run()
+            pl.check()
+            return pl.read()
+        finally:
+            pl.close()
+
+
+class DeviceData:
+    def __init__(self, eng: Engine, p: Optional[PackedSNPs], dev=None):
+        self.eng = eng
+        self.h = C.c_void_p()
+        if p is not None:
+            self.packed = p
+            off = np.ascontiguousarray(p.chrom_off, np.int64)
+            eng.check(eng.lib.sfs2d_data_upload(eng.h, L.ptr(p.counts), L.ptr(p.pos), L.ptr(p.ann_id), p.n,
+                                                L.ptr(off), p.nchrom, C.byref(self.h)))
+        else:
+            d_counts, d_pos, d_ann, n, chrom_off, last_pos = dev
+            self.packed = None
+            off = np.ascontiguousarray(chrom_off, np.int64)
+            lp = np.ascontiguousarray(last_pos, np.uint32)
+            eng.check(eng.lib.sfs2d_data_wrap_device(eng.h, C.c_void_p(d_counts), C.c_void_p(d_pos),
+                                                     C.c_void_p(d_ann) if d_ann else None, int(n), L.ptr(off),
+                                                     L.ptr(lp), len(off) - 1, C.byref(self.h)))
+
+    def close(self):
+        if self.h:
+            self.eng.lib.sfs2d_data_free(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Plan:
+    def __init__(self, eng: Engine, data: DeviceData, cfg: ScanConfig):
+        self.eng, self.data, self.cfg = eng, data, cfg
+        self.h = C.c_void_p()
+        prm = cfg.params()
+        eng.check(eng.lib.sfs2d_plan_create(eng.h, data.h, C.byref(prm), C.byref(self.h)))
+        self.nrec = int(eng.lib.sfs2d_plan_num_records(self.h))
+
+    def set_background(self, bg2d, bg1a, bg1b):
+        n1p, n2p = self.cfg.n1p, self.cfg.n2p
+        b2 = np.ascontiguousarray(np.asarray(bg2d, np.float64).reshape(-1))
+        b1 = np.ascontiguousarray(np.asarray(bg1a, np.float64).reshape(-1)[: n1p + 1])
+        b1b = np.ascontiguousarray(np.asarray(bg1b, np.float64).reshape(-1)[: n2p + 1])
+        if b2.size != (2 * n1p + 1) * (2 * n2p + 1) or b1.size != n1p + 1 or b1b.size != n2p + 1:
+            raise ValueError("background arrays have the wrong size")
+        self.eng.check(self.eng.lib.sfs2d_plan_set_background(self.h, L.ptr(b2), L.ptr(b1), L.ptr(b1b)))
+
+    def run(self, out_dev_ptr: Optional[int] = None, phase: int = 0):
+        self.eng.check(self.eng.lib.sfs2d_plan_run_phase(self.h, phase,
+                                                         C.c_void_p(out_dev_ptr) if out_dev_ptr else None))
+
+    def check(self):
+        self.eng.check(self.eng.lib.sfs2d_plan_check(self.h))
+
+    def read(self) -> np.ndarray:
+        out = np.zeros(self.nrec, dtype=L.WINDOW_DTYPE)
+        n = C.c_int64()
+        self.eng.check(self.eng.lib.sfs2d_plan_read(self.h, L.ptr(out), self.nrec, C.byref(n)))
+        return out
+
+    def bg_buffer(self):
+        p = C.c_void_p()
+        nb = C.c_int64()
+        self.eng.check(self.eng.lib.sfs2d_plan_bg_buffer(self.h, C.byref(p), C.byref(nb)))
+        return p.value, nb.value
+
+    def time(self, iters: int = 10):
+        v = [C.c_double() for _ in range(4)]
+        self.eng.check(self.eng.lib.sfs2d_plan_time(self.h, iters, *[C.byref(x) for x in v]))
+        return tuple(x.value for x in v)
+
+    def set_timing(self, max_runs: int):
+        self.eng.check(self.eng.lib.sfs2d_plan_set_timing(self.h, int(max_runs)))
+
+    def timing_read(self):
+        n = C.c_int()
+        v = [C.c_double() for _ in range(3)]
+        self.eng.check(self.eng.lib.sfs2d_plan_timing_read(self.h, C.byref(n), *[C.byref(x) for x in v]))
+        return n.value, tuple(x.value for x in v)
+
+    def close(self):
+        if self.h:
+            self.eng.lib.sfs2d_plan_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,301 @@
+"""Drop-in replacement for the reference module ``scripts/src/twoDSFS_class.py``.
+
+Same class, method names, arguments, return shapes and error behaviour as the reference's
+``LikelihoodInference_jointSFS`` (twoDSFS_class.py:20-1737) for the window-scan path, plus the
+module-level ``col_names`` / ``chr_ids`` / ``save_csv_stats`` CSV writer (1788-1797, 1881-1907).
+Every window statistic is computed by the HIP kernels of ``csrc/sfs2d.hip`` on an MI355X
+(through ``sfs2d.engine``); there is no CPU fallback.
+
+Methods accept either the reference's SNP dict (``{"CHR-POS": {"calls": ..., "annotation": ...}}``)
+or an already packed ``sfs2d.PackedSNPs`` (skips the dict packing, which dominates host time).
+"""
+from __future__ import annotations
+
+import csv
+import os
+from typing import Optional
+
+import numpy as np
+
+from sfs2d import _lib as L
+from sfs2d import post
+from sfs2d.engine import Engine, ScanConfig
+from sfs2d.ingest import make_data_dict_vcf as _make_data_dict_vcf
+from sfs2d.pack import PackedSNPs, pack_snp_dict
+
+__all__ = ["LikelihoodInference_jointSFS", "save_csv_stats", "col_names", "chr_ids", "load_chr_ids"]
+
+_NO_ANN = 1 << 20   # an annotation id no SNP carries (variant_type absent from the data)
+
+col_names = ['chromosome', 'window_start', 'window_end', 'snp_count', 'T2D', 'T1D_p1', 'T1D_p2',
+             'new_term_p1', 'new_term_p2', 'T2D_diff']
+chr_ids: dict = {}
+
+
+def load_chr_ids(path: str) -> dict:
+    """Accession -> chromosome number map (chromosomes.txt; reference 1788-1797)."""
+    chr_ids.clear()
+    with open(path, "r") as fh:
+        for line in fh:
+            columns = line.strip().split("\t")
+            if len(columns) >= 2:
+                chr_ids[columns[0]] = columns[1]
+    return chr_ids
+
+
+if os.environ.get("SFS2D_CHROMOSOMES"):
+    load_chr_ids(os.environ["SFS2D_CHROMOSOMES"])
+
+
+def save_csv_stats(stats_dict, output):
+    """twoDSFS_class.py:1884-1907: one row per window, chromosome renamed through chr_ids."""
+    with open(output, 'w', newline='') as csvfile:
+        writer = csv.DictWriter(csvfile, fieldnames=col_names)
+        writer.writeheader()
+        for window_coords, result in stats_dict.items():
+            chromosome = window_coords.split(' ')[0]
+            chromosome_num = chr_ids.get(chromosome, chromosome)
+            window_start, window_end = window_coords.split(' ')[1].split('-')
+            writer.writerow({
+                'chromosome': chromosome_num, 'window_start': window_start, 'window_end': window_end,
+                'snp_count': result["snp_count"], 'T2D': result["T2D"], 'T1D_p1': result["T1D_pop1"],
+                'T1D_p2': result["T1D_pop2"], 'new_term_p1': result["new_term_pop1"],
+                'new_term_p2': result["new_term_pop2"], 'T2D_diff': result["T2D_diff"]})
+
+
+def _fold_counts(u: np.ndarray) -> np.ndarray:
+    """fold_1d_sfs on a dense unfolded spectrum: folded[f] = u[f] + u[2n-f], folded[n] = u[n]."""
+    n2 = len(u) - 1
+    n = n2 // 2
+    out = np.zeros(n + 1, dtype=u.dtype)
+    for f in range(n2 + 1):
+        out[min(f, n2 - f)] += u[f]
+    return out
+
+
+class LikelihoodInference_jointSFS:
+    def __init__(self, vcf_filename, popinfo_filename, start_position=None, end_position=None,
+                 pop1='uv', pop2='bv', pop1_size=18, pop2_size=14, variant_type=None, fold=True, device=0):
+        self.vcf_filename = vcf_filename
+        self.popinfo_filename = popinfo_filename
+        self.pop1 = pop1
+        self.pop2 = pop2
+        self.pop1_size = pop1_size
+        self.pop2_size = pop2_size
+        self.start_position = start_position
+        self.end_position = end_position
+        self.variant_type = variant_type
+        self.fold = fold
+        self.device = device
+
+    # ------------------------------------------------------------------ ingest
+    def make_data_dict_vcf(self, vcf_filename=None, popinfo_filename=None):
+        """twoDSFS_class.py:36-138 (quirks Q12/Q13 kept; see sfs2d.ingest)."""
+        return _make_data_dict_vcf(vcf_filename if vcf_filename is not None else self.vcf_filename,
+                                   popinfo_filename if popinfo_filename is not None else self.popinfo_filename)
+
+    # ------------------------------------------------------------------ plumbing
+    def _engine(self) -> Engine:
+        return Engine.get(self.device)
+
+    def _pack(self, data, pop1=None, pop2=None) -> PackedSNPs:
+        if isinstance(data, PackedSNPs):
+            return data
+        return pack_snp_dict(data, pop1 or self.pop1, pop2 or self.pop2)
+
+    def _cfg(self, p: PackedSNPs, **kw) -> ScanConfig:
+        ann = -1
+        if self.variant_type is not None:
+            ann = p.ann_names.index(self.variant_type) if self.variant_type in p.ann_names else _NO_ANN
+        start = None if self.start_position is None else int(self.start_position)
+        end = None if self.end_position is None else int(self.end_position)
+        return ScanConfig(n1p=self.pop1_size, n2p=self.pop2_size, fold=bool(self.fold), ann_want=ann,
+                          start_position=start, end_position=end, **kw)
+
+    def _scan(self, p: PackedSNPs, cfg: ScanConfig, bg=None):
+        eng = self._engine()
+        dev = eng.upload(p)
+        try:
+            recs = eng.scan(dev, cfg, bg)
+        finally:
+            dev.close()
+        return recs
+
+    def _bg_arrays(self, p: PackedSNPs, chrom: int):
+        """Unnormalised background of one chromosome (2D grid + folded 1D), computed on the GPU."""
+        eng = self._engine()
+        dev = eng.upload(p)
+        try:
+            h2, u1, u2 = eng.bg_hist(dev, self._cfg(p), chrom)
+        finally:
+            dev.close()
+        return h2, _fold_counts(u1), _fold_counts(u2)
+
+    # ------------------------------------------------------------------ window scans
+    def combined_scan(self, data_dict, window_size):
+        """Each chromosome is its own background (twoDSFS_class.py:787-991)."""
+        self.data_dict = data_dict
+        self.window_size = window_size
+        p = self._pack(data_dict)
+        recs = self._scan(p, self._cfg(p, window_mode=L.WINDOW_BP, window=window_size,
+                                       bg_mode=L.BG_PER_CHROM, prev_extra=True))
+        return post.combined_scan(recs, p, window_size, post.num_slots(recs))
+
+    def scan_chooseChr(self, data_dict, window_size, background_chromosome):
+        """One named chromosome as the background for every window (993-1159)."""
+        self.data_dict = data_dict
+        self.window_size = window_size
+        p = self._pack(data_dict)
+        if background_chromosome not in p.chrom_names:
+            raise ValueError(f"Background chromosome {background_chromosome} not found in the data.")
+        bg = self._bg_arrays(p, p.chrom_names.index(background_chromosome))
+        recs = self._scan(p, self._cfg(p, window_mode=L.WINDOW_BP, window=window_size,
+                                       bg_mode=L.BG_SUPPLIED), bg)
+        return post.fixed_bg_scan(recs, p, window_size, post.num_slots(recs))
+
+    def scan_precomputed_BG(self, data_dict, window_size, bg_2d_sfs, bg_1d_sfs_pop1, bg_1d_sfs_pop2):
+        """Caller-supplied (normalised or not) background SFS dicts (1161-1299)."""
+        self.data_dict = data_dict
+        self.window_size = window_size
+        p = self._pack(data_dict)
+        bg = (self._bg2d_array(bg_2d_sfs), self._bg1d_array(bg_1d_sfs_pop1, self.pop1_size),
+              self._bg1d_array(bg_1d_sfs_pop2, self.pop2_size))
+        recs = self._scan(p, self._cfg(p, window_mode=L.WINDOW_BP, window=window_size,
+                                       bg_mode=L.BG_SUPPLIED), bg)
+        return post.fixed_bg_scan(recs, p, window_size, post.num_slots(recs))
+
+    def scan_chooseChr_bySNPs(self, data_dict, snp_window_size, background_chromosome):
+        """Fixed-SNP windows against one named chromosome's NORMALISED background (1303-1420)."""
+        self.data_dict = data_dict
+        self.snp_window_size = snp_window_size
+        p = self._pack(data_dict)
+        if background_chromosome not in p.chrom_names:
+            raise ValueError(f"Background chromosome {background_chromosome} not found in the data.")
+        h2, f1, f2 = self._bg_arrays(p, p.chrom_names.index(background_chromosome))
+        bg = (np.array(self._normalize_values(h2.ravel().tolist())),
+              np.array(self._normalize_values(f1.tolist())), np.array(self._normalize_values(f2.tolist())))
+        recs = self._scan(p, self._cfg(p, window_mode=L.WINDOW_SNPS, window=snp_window_size,
+                                       bg_mode=L.BG_SUPPLIED), bg)
+        return post.bysnp_scan(recs, p, snp_window_size, with_diff=False, final_warning=True)
+
+    def scan_perChr_bySNPs(self, data_dict, snp_window_size):
+        """Fixed-SNP windows, each chromosome its own background (1422-1541)."""
+        self.data_dict = data_dict
+        self.num_snps = snp_window_size
+        p = self._pack(data_dict)
+        recs = self._scan(p, self._cfg(p, window_mode=L.WINDOW_SNPS, window=snp_window_size,
+                                       bg_mode=L.BG_PER_CHROM))
+        return post.bysnp_scan(recs, p, snp_window_size, with_diff=True, final_warning=False)
+
+    # ------------------------------------------------------------------ SFS primitives
+    def calculate_2d_sfs(self, data_dict):
+        """2D SFS dict over the grid (140-232), accumulated on the GPU."""
+        self.data_dict = data_dict
+        p = self._pack(data_dict)
+        n1, n2 = 2 * self.pop1_size, 2 * self.pop2_size
+        if p.n == 0:
+            return {(i, j): 0 for i in range(n1 + 1) for j in range(n2 + 1)}
+        eng = self._engine()
+        dev = eng.upload(p)
+        try:
+            h2, _, _ = eng.bg_hist(dev, self._cfg(p), -1)
+        finally:
+            dev.close()
+        return {(i, j): int(h2[i, j]) for i in range(n1 + 1) for j in range(n2 + 1)}
+
+    def calculate_1d_sfs(self, data_dict, pop, pop_size, start_position, end_position, variant_type):
+        """Unfolded 1D SFS dict of raw alt counts (398-444), accumulated on the GPU."""
+        self.data_dict = data_dict
+        self.pop = pop
+        self.pop_size = pop_size
+        self.start_position = start_position
+        self.end_position = end_position
+        self.variant_type = variant_type
+        p = self._pack(data_dict, pop1=pop, pop2=pop).single_pop(pop)
+        if p.n == 0:
+            return {i: 0 for i in range(2 * pop_size + 1)}
+        eng = self._engine()
+        dev = eng.upload(p)
+        ann = -1
+        if variant_type is not None:
+            ann = p.ann_names.index(variant_type) if variant_type in p.ann_names else _NO_ANN
+        cfg = ScanConfig(n1p=pop_size, n2p=pop_size, fold=False, ann_want=ann,
+                         start_position=None if start_position is None else int(start_position),
+                         end_position=None if end_position is None else int(end_position))
+        try:
+            _, u1, _ = eng.bg_hist(dev, cfg, -1)
+        finally:
+            dev.close()
+        return {i: int(u1[i]) for i in range(2 * pop_size + 1)}
+
+    def fold_1d_sfs(self, sfs_dict):
+        """446-463: minor = min(f, F - f) with F = max key."""
+        num_chromosomes = max(sfs_dict.keys())
+        folded = {}
+        for freq, count in sfs_dict.items():
+            m = min(freq, num_chromosomes - freq)
+            folded[m] = folded[m] + count if m in folded else count
+        return folded
+
+    @staticmethod
+    def _normalize_values(values):
+        total = sum(values[1:-1])
+        return [v / total for v in values]
+
+    def normalize_2d_sfs(self, sfs):
+        """234-247: divide by sum(values[1:-1]) in insertion order."""
+        self.sfs = sfs
+        vals = self._normalize_values(list(sfs.values()))
+        return dict(zip(sfs.keys(), vals))
+
+    def normalize_1d_sfs(self, sfs):
+        """465-476."""
+        self.sfs = sfs
+        vals = self._normalize_values(list(sfs.values()))
+        return dict(zip(sfs.keys(), vals))
+
+    def count_snps(self, window_data, variant_type):
+        """291-302."""
+        self.window_data = window_data
+        self.variant_type = variant_type
+        if variant_type is None:
+            return len(window_data)
+        return sum(1 for d in window_data.values() if d.get("annotation") == variant_type)
+
+    def new_term(self, T1D, T2D):
+        """779-785."""
+        self.T1D = T1D
+        self.T2D = T2D
+        return T2D - T1D
+
+    # dense-dict likelihoods: evaluated by the same GPU kernel on a synthetic SNP stream that
+    # reproduces the given foreground spectrum (one SNP per count, no fold)
+    def calculate_likelihood_2D(self, foreground_2d_sfs, background_2d_sfs):
+        """625-684."""
+        self.foreground_2d_sfs = foreground_2d_sfs
+        self.background_2d_sfs = background_2d_sfs
+        from sfs2d.dense import clr_2d
+        return clr_2d(self._engine(), foreground_2d_sfs, background_2d_sfs, guards=True)
+
+    def calculate_likelihood_1D(self, foreground_sfs, background_sfs):
+        """478-537."""
+        self.foreground_sfs = foreground_sfs
+        self.background_sfs = background_sfs
+        from sfs2d.dense import clr_1d
+        return clr_1d(self._engine(), foreground_sfs, background_sfs, guards=True)
+
+    # ------------------------------------------------------------------ helpers
+    def _bg2d_array(self, bg):
+        n1, n2 = 2 * self.pop1_size, 2 * self.pop2_size
+        out = np.zeros((n1 + 1) * (n2 + 1), np.float64)
+        keys = [(i, j) for i in range(n1 + 1) for j in range(n2 + 1)]
+        for k, key in enumerate(keys[1:-1], start=1):
+            out[k] = bg[key]            # background_2d_sfs[k] for k in bins[1:-1] (:658-661)
+        return out
+
+    @staticmethod
+    def _bg1d_array(bg, pop_size):
+        out = np.zeros(pop_size + 1, np.float64)
+        for k in range(1, pop_size):
+            out[k] = bg[k]              # background_sfs[k] for k in bins[1:-1] (:505-508)
+        return out

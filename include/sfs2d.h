@@ -1,0 +1,154 @@
+/*
+ * sfs2d.h -- C ABI of the MI355X windowed 2D-SFS composite-likelihood scan.
+ *
+ * Drop-in boundary for the hot path of uricchio/2DSFS-scan: the per-window 2D-SFS + folded
+ * 1D-SFS accumulation and the T2D / T1D multinomial log-likelihood ratios against a
+ * background SFS (scripts/src/twoDSFS_class.py, scripts/sims_scan.py).  The reference has no
+ * FFI layer -- its boundary is the Python class `LikelihoodInference_jointSFS`
+ * (twoDSFS_class.py:20-33) -- so these entry points are what that class's methods bind through
+ * ctypes:
+ *
+ *   sfs2d_data_upload / _wrap_device  <- the SNP dict built by make_data_dict_vcf (36-138),
+ *                                        packed into SoA (sorted as in combined_scan 828-835)
+ *   sfs2d_bg_hist                     <- calculate_2d_sfs (140-232) + calculate_1d_sfs (398-444)
+ *                                        over a whole chromosome / data set (background SFS)
+ *   sfs2d_plan_create + sfs2d_plan_run <- the window loop of combined_scan (787-991),
+ *                                        scan_chooseChr (993), scan_precomputed_BG (1161),
+ *                                        scan_*_bySNPs (1303, 1422), sims_scan.process_window (451):
+ *                                        per window calculate_2d_sfs + fold_1d_sfs(calculate_1d_sfs)
+ *                                        + calculate_likelihood_2D (625-684) / _1D (478-537)
+ *   sfs2d_scan                        <- one-shot plan_create + plan_run + copy-out
+ *
+ * Conventions: every call returns 0 on success or a negative SFS2D_E* code; the message is
+ * available from sfs2d_last_error(ctx).  Nothing throws or aborts across the ABI.  The caller
+ * owns every host buffer; the library owns the device buffers inside ctx / data / plan.
+ * One ctx per GPU; calls on one ctx must be serialised by the caller.  All work is enqueued on
+ * the ctx's HIP stream (sfs2d_ctx_set_stream to share a stream with another runtime).
+ */
+#ifndef SFS2D_H
+#define SFS2D_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SFS2D_ABI_VERSION 1
+
+/* status codes */
+#define SFS2D_OK 0
+#define SFS2D_E_ARG (-1)       /* invalid argument (sizes, modes, null pointers) */
+#define SFS2D_E_HIP (-2)       /* HIP runtime error (message has the HIP string) */
+#define SFS2D_E_NOMEM (-3)     /* device allocation failed */
+#define SFS2D_E_KEY (-4)       /* an alt count > 2*pop_size: the reference raises KeyError (calculate_1d_sfs:433) */
+#define SFS2D_E_GRID (-5)      /* a folded 2D bin lies outside the (2n1+1)x(2n2+1) grid */
+#define SFS2D_E_CAP (-6)       /* output capacity too small (*nwin_out holds the needed size) */
+
+/* window modes */
+#define SFS2D_WINDOW_BP 0      /* fixed-bp windows, window id (pos-1)//ws per chromosome (twoDSFS_class.py:894, 948) */
+#define SFS2D_WINDOW_SNPS 1    /* fixed SNP-count windows, incomplete tail dropped (1515-1535) */
+
+/* background modes */
+#define SFS2D_BG_PER_CHROM 0   /* each chromosome's own SNPs form its background (combined_scan 809-825) */
+#define SFS2D_BG_SUPPLIED 1    /* one background for all windows (scan_chooseChr / precomputed / sims) */
+
+/* plan flags */
+#define SFS2D_F_PREV_EXTRA 1u  /* also evaluate the previous window's 1D SFSs against the LAST window's
+                                  chromosome background (combined_scan final block, 951-989, quirk Q9) */
+
+/* window record flags */
+#define SFS2D_W_EMPTY 0x80000000u  /* slot holds no SNP (fixed-bp slot between SNPs): not a window */
+#define SFS2D_W_BG2_ZERO 0x1u      /* background 2D inner sum == 0  -> None / ZeroDivisionError */
+#define SFS2D_W_BG1A_ZERO 0x2u
+#define SFS2D_W_BG1B_ZERO 0x4u
+#define SFS2D_W_EXTRA 0x40000000u  /* record is the Q9 helper (see SFS2D_F_PREV_EXTRA) */
+
+typedef struct sfs2d_ctx sfs2d_ctx;
+typedef struct sfs2d_data sfs2d_data;
+typedef struct sfs2d_plan sfs2d_plan;
+
+typedef struct {
+  int32_t n1p, n2p;       /* pop1_size, pop2_size: diploid individuals (twoDSFS_class.py:22); grid (2n1p+1)x(2n2p+1) */
+  int32_t fold;           /* joint 2D fold: swap ref/alt in both pops if alt1+alt2 > n1p+n2p (197-206) */
+  int32_t window_mode;    /* SFS2D_WINDOW_BP / SFS2D_WINDOW_SNPS */
+  int64_t window;         /* window size in bp, or SNPs per window */
+  int32_t bg_mode;        /* SFS2D_BG_PER_CHROM / SFS2D_BG_SUPPLIED */
+  int32_t ann_want;       /* variant_type filter: annotation id to keep, -1 = no filter (185-187, 291-302) */
+  int32_t has_start, has_end; /* SFS position filter start_position / end_position (179-182) */
+  int64_t start_pos, end_pos;
+  uint32_t flags;         /* SFS2D_F_* */
+  uint32_t reserved;
+} sfs2d_params;
+
+/* one record per window slot (64 bytes) */
+typedef struct {
+  uint32_t chrom;         /* chromosome index in the data set's (sorted) chromosome list */
+  uint32_t wid;           /* window index within the chromosome: (pos-1)//ws, or SNP-window ordinal */
+  uint32_t begin, end;    /* SNP index range [begin, end) in the data set */
+  uint32_t snp_count;     /* count_snps (291-302): SNPs in the window matching variant_type */
+  uint32_t n2;            /* 2D foreground total over inner bins bins[1:-1] (N of T2D) */
+  uint32_t n2_all;        /* 2D foreground total over all bins (scan_*_bySNPs skip test, 1376/1496) */
+  uint32_t n1a, n1b;      /* folded 1D foreground totals over inner bins 1..pop_size-1 */
+  uint32_t flags;         /* SFS2D_W_* */
+  double t2d, t1d_p1, t1d_p2; /* NaN-boxed "None" is not used: validity = n>0 and !BG*_ZERO */
+} sfs2d_window;
+
+/* context */
+int sfs2d_ctx_create(int device, sfs2d_ctx** out);
+int sfs2d_ctx_destroy(sfs2d_ctx* ctx);
+const char* sfs2d_last_error(const sfs2d_ctx* ctx);
+int sfs2d_ctx_set_stream(sfs2d_ctx* ctx, void* hip_stream);   /* NULL = the ctx's own stream */
+int sfs2d_abi_version(void);
+
+/* data set: packed SNPs in scan order (sorted by chromosome string, then position) */
+int sfs2d_data_upload(sfs2d_ctx* ctx, const uint32_t* counts, const uint32_t* pos, const uint16_t* ann_id,
+                      int64_t n, const int64_t* chrom_off, int32_t nchrom, sfs2d_data** out);
+/* wrap caller-owned DEVICE arrays (no copy); chrom_off / chrom_last_pos are HOST arrays */
+int sfs2d_data_wrap_device(sfs2d_ctx* ctx, const uint32_t* d_counts, const uint32_t* d_pos,
+                           const uint16_t* d_ann_id, int64_t n, const int64_t* chrom_off,
+                           const uint32_t* chrom_last_pos, int32_t nchrom, sfs2d_data** out);
+int sfs2d_data_free(sfs2d_data* data);
+
+/* Background SFS histograms of chromosome `chrom` (-1: all SNPs of the data set), with the
+ * params' filters (position, variant_type, fold).  h2d: (2n1p+1)*(2n2p+1) int64, row-major
+ * (alt1, alt2); h1a / h1b: UNFOLDED 1D spectra of raw alt counts, 2*pop_size+1 int64 each. */
+int sfs2d_bg_hist(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* params, int32_t chrom,
+                  int64_t* h2d, int64_t* h1a, int64_t* h1b);
+
+/* Plans: everything that depends only on (data, params) is built once; plan_run replays the
+ * launches (captured in a hipGraph) with inputs and outputs resident in HBM. */
+int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* params, sfs2d_plan** out);
+/* number of output records the plan writes (window slots, +1 when SFS2D_F_PREV_EXTRA) */
+int64_t sfs2d_plan_num_records(const sfs2d_plan* plan);
+/* SFS2D_BG_SUPPLIED: background values (host doubles, integer or normalised): bg2d has
+ * (2n1p+1)*(2n2p+1) entries, bg1a / bg1b have n1p+1 / n2p+1 entries read at keys 1..pop_size-1
+ * (folded or, for the sims path, unfolded spectra: quirk Q7). */
+int sfs2d_plan_set_background(sfs2d_plan* plan, const double* bg2d, const double* bg1a, const double* bg1b);
+/* enqueue the scan; out_dev: device buffer of sfs2d_plan_num_records records (NULL = plan-owned) */
+int sfs2d_plan_run(sfs2d_plan* plan, sfs2d_window* out_dev);
+/* copy the last run's records to host (synchronises the stream) */
+int sfs2d_plan_read(sfs2d_plan* plan, sfs2d_window* out_host, int64_t cap, int64_t* nrec_out);
+/* device pointers of the plan's per-chromosome background histogram replicas (uint32), for a
+ * multi-GPU all-reduce between sfs2d_plan_run_phase(plan, 1) and (plan, 2). */
+int sfs2d_plan_bg_buffer(sfs2d_plan* plan, void** dev_ptr, int64_t* nbytes);
+int sfs2d_plan_run_phase(sfs2d_plan* plan, int phase, sfs2d_window* out_dev);
+/* last run's error word (0 = ok, else SFS2D_E_KEY / SFS2D_E_GRID); synchronises */
+int sfs2d_plan_check(sfs2d_plan* plan);
+/* live timing: record HIP events around each kernel of the next `max_runs` sfs2d_plan_run calls
+ * (0 = off), then read the average device time per kernel (k1 = bg+segmentation, k2 = background
+ * tables, k3 = window scan) over those runs (synchronises). */
+int sfs2d_plan_set_timing(sfs2d_plan* plan, int max_runs);
+int sfs2d_plan_timing_read(sfs2d_plan* plan, int* nruns, double* ms_k1, double* ms_k2, double* ms_k3);
+/* standalone timing loop: average device time per kernel over `iters` runs */
+int sfs2d_plan_time(sfs2d_plan* plan, int iters, double* ms_per_run, double* ms_k1, double* ms_k2, double* ms_k3);
+int sfs2d_plan_destroy(sfs2d_plan* plan);
+
+/* one-shot convenience: plan + run + read (+ supplied background when bg2d != NULL) */
+int sfs2d_scan(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* params, const double* bg2d,
+               const double* bg1a, const double* bg1b, sfs2d_window* out_host, int64_t cap, int64_t* nrec_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SFS2D_H */

@@ -1,0 +1,209 @@
+"""GPU parity: the drop-in modules (HIP kernels through the C ABI) against the reference's
+golden outputs (tests/golden, produced by the reference's own functions) and against the
+oracle's per-window records.  Integer counts bit-exact; float statistics within 1e-10 relative
+(golden_util.close); exact 0.0 / inf / NaN / None identity."""
+import numpy as np
+import pytest
+
+import golden_util as gu
+from oracle import sfs_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+_G = gu.Golden()
+
+
+def _class_obj(cfgd):
+    import twoDSFS_class as T
+    return T.LikelihoodInference_jointSFS(None, None, start_position=cfgd.get("start_position"),
+                                          end_position=cfgd.get("end_position"), pop1=cfgd["pop1"],
+                                          pop2=cfgd["pop2"], pop1_size=cfgd["n1p"], pop2_size=cfgd["n2p"],
+                                          variant_type=cfgd.get("variant_type"), fold=cfgd.get("fold", True))
+
+
+def _gpu_call(obj, p, fn, args):
+    if fn == "scan_precomputed_BG":
+        d = p  # PackedSNPs accepted by every method
+        bg2 = obj.normalize_2d_sfs(obj.calculate_2d_sfs(d))
+        bg1 = obj.normalize_1d_sfs(obj.fold_1d_sfs(obj.calculate_1d_sfs(
+            d, obj.pop1, obj.pop1_size, obj.start_position, obj.end_position, obj.variant_type)))
+        bg1b = obj.normalize_1d_sfs(obj.fold_1d_sfs(obj.calculate_1d_sfs(
+            d, obj.pop2, obj.pop2_size, obj.start_position, obj.end_position, obj.variant_type)))
+        return obj.scan_precomputed_BG(p, args[0], bg2, bg1, bg1b)
+    return getattr(obj, fn)(p, *args)
+
+
+def _cases():
+    out = []
+    for name in _G.cases():
+        for i, c in enumerate(_G.calls(name)):
+            if c["fn"] != "sims_process_window":
+                out.append((name, i))
+    return out
+
+
+@pytest.mark.parametrize("name,i", _cases(), ids=[f"{n}-{i}" for n, i in _cases()])
+def test_dropin_class_vs_reference(golden, name, i):
+    call = golden.calls(name)[i]
+    p = golden.packed(name)
+    cfgd = golden.cfg(name)
+    obj = _class_obj(cfgd)
+    ok, out, stdout = gu.run_capture(_gpu_call, obj, p, call["fn"], call["args"])
+    ref = call["out"]
+    if not ref["ok"]:
+        assert not ok, f"reference raised {ref['error']}, GPU path returned"
+        assert type(out).__name__ == ref["error"], repr(out)
+        assert str(out) == ref["message"]
+        return
+    assert ok, f"GPU path raised {out!r}"
+    errs = gu.compare_results(out, gu.decode_results(ref["results"]))
+    assert not errs, errs[:10]
+    assert stdout == ref["stdout"]
+
+
+@pytest.mark.parametrize("tag", ["sims_n10", "sims_n100"])
+def test_dropin_sims_vs_reference(golden, tag):
+    import sims_scan as S
+    call = golden.calls(tag)[0]
+    rep = golden.packed(tag)
+    bgd = golden.packed(f"{tag}_bgdata")
+    n = golden.cfg(tag)["n1p"]
+    bg2 = S.calculate_2d_sfs(bgd, "p1", "p2", n, n, start_position=0, end_position=500000, variant_type=None)
+    bg1 = S.calculate_1d_sfs(bgd, "p1", n, start_position=0, end_position=500000, variant_type=None)
+    bg1b = S.calculate_1d_sfs(bgd, "p2", n, start_position=0, end_position=500000, variant_type=None)
+    gb = golden.npz(f"{tag}_bg.npz")
+    assert np.array_equal(np.array([[bg2[(i, j)] for j in range(2 * n + 1)] for i in range(2 * n + 1)]), gb["bg2d"])
+    assert np.array_equal(np.array([bg1[k] for k in range(2 * n + 1)]), gb["bg1a"])
+    out = S.process_window(rep, bg2, bg1, bg1b, 500000, "p1", "p2", n, n, None, None, None)
+    errs = gu.compare_results(out, gu.decode_results(call["out"]["results"]))
+    assert not errs, errs[:10]
+
+
+def test_bg_hist_bitexact_chr1(golden):
+    from sfs2d.engine import Engine, ScanConfig
+    p = golden.packed("chr1")
+    eng = Engine.get(0)
+    dev = eng.upload(p)
+    h2, u1, u2 = eng.bg_hist(dev, ScanConfig(n1p=18, n2p=14), 0)
+    import twoDSFS_class as T
+    g = golden.npz("chr1_bg.npz")
+    assert np.array_equal(h2, g["bg2d"])
+    assert np.array_equal(T._fold_counts(u1), g["bg1a"])
+    assert np.array_equal(T._fold_counts(u2), g["bg1b"])
+
+
+def _records_vs_oracle(p, cfg_scan, ocfg, wins, bg_of, guards=True):
+    from sfs2d import _lib as L
+    from sfs2d.engine import Engine
+    eng = Engine.get(0)
+    dev = eng.upload(p)
+    recs = eng.scan(dev, cfg_scan)
+    body = recs[(recs["flags"] & (L.W_EMPTY | L.W_EXTRA)) == 0]
+    ref = O.window_records(p, wins, ocfg, bg_of, guards)
+    assert len(body) == len(ref)
+    for r, o in zip(body, ref):
+        for f in ("snp_count", "n2", "n2_all", "n1a", "n1b"):
+            assert int(r[f]) == o[f], (f, int(r[f]), o[f])
+        for f, g in (("t2d", "T2D"), ("t1d_p1", "T1D_p1"), ("t1d_p2", "T1D_p2")):
+            if o[g] is not None:
+                assert gu.close(float(r[f]), o[g]), (f, float(r[f]), o[g])
+    return body
+
+
+@pytest.mark.parametrize("n1p,n2p,ws", [(25, 25, 20000), (18, 14, 7000), (50, 50, 20000), (100, 75, 100000),
+                                          (3, 2, 500), (25, 25, 500000)])
+def test_records_per_chrom_bp(n1p, n2p, ws):
+    from sfs2d import _lib as L
+    from sfs2d.engine import ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(3, [4000, 2500, 1], n1p, n2p, seed=n1p * 7 + ws)
+    ocfg = O.Cfg(n1p, n2p)
+    bgs = O.chrom_backgrounds(p, ocfg)
+    _records_vs_oracle(p, ScanConfig(n1p=n1p, n2p=n2p, window=ws), ocfg, O.bp_windows(p, ws), lambda c: bgs[c])
+
+
+@pytest.mark.parametrize("S", [1, 64, 500, 4096])
+def test_records_per_chrom_snps(S):
+    from sfs2d import _lib as L
+    from sfs2d.engine import ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(2, [5000, 3333], 25, 25, seed=S)
+    ocfg = O.Cfg(25, 25)
+    bgs = O.chrom_backgrounds(p, ocfg)
+    wins, _ = O.snp_windows(p, S)
+    _records_vs_oracle(p, ScanConfig(n1p=25, n2p=25, window_mode=L.WINDOW_SNPS, window=S), ocfg, wins,
+                       lambda c: bgs[c])
+
+
+def test_config2_full_size_self_consistency():
+    """BASELINE config 2 (1e6 SNPs, n1=n2=50 haploid, 20 kb): every window's counts partition the
+    stream, the 2D/1D totals equal the background totals, and a 200-window sample matches the
+    oracle."""
+    from sfs2d import _lib as L
+    from sfs2d.engine import Engine, ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(1, 1_000_000, 25, 25, seed=12345)
+    eng = Engine.get(0)
+    dev = eng.upload(p)
+    recs = eng.scan(dev, ScanConfig(n1p=25, n2p=25, window=20000))
+    body = recs[(recs["flags"] & L.W_EMPTY) == 0]
+    assert int(body["snp_count"].sum()) == p.n
+    assert np.all(body["begin"][1:] == body["end"][:-1])
+    h2, u1, u2 = eng.bg_hist(dev, ScanConfig(n1p=25, n2p=25), 0)
+    assert int(body["n2"].sum()) == int(h2.ravel()[1:-1].sum())
+    ocfg = O.Cfg(25, 25)
+    bg = O.chrom_backgrounds(p, ocfg)[0]
+    wins = O.bp_windows(p, 20000)
+    assert len(wins) == len(body)
+    idx = np.linspace(0, len(wins) - 1, 200).astype(int)
+    ref = O.window_records(p, [wins[i] for i in idx], ocfg, lambda c: bg)
+    for i, o in zip(idx, ref):
+        r = body[i]
+        assert int(r["n2"]) == o["N2"] and int(r["n1a"]) == o["N1a"] and int(r["n1b"]) == o["N1b"]
+        assert gu.close(float(r["t2d"]), o["T2D"]) and gu.close(float(r["t1d_p1"]), o["T1D_p1"])
+        assert gu.close(float(r["t1d_p2"]), o["T1D_p2"])
+
+
+def test_plan_replay_is_deterministic():
+    """Self-cleaning state (slot table, background replicas, LDS) across repeated runs."""
+    from sfs2d.engine import Engine, ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(2, [20000, 7000], 25, 25, seed=9)
+    eng = Engine.get(0)
+    dev = eng.upload(p)
+    pl = eng.plan(dev, ScanConfig(n1p=25, n2p=25, window=20000, prev_extra=True))
+    outs = []
+    for _ in range(3):
+        pl.run()
+        pl.check()
+        outs.append(pl.read())
+    assert outs[0].tobytes() == outs[1].tobytes() == outs[2].tobytes()
+    pl.close()
+
+
+def test_key_error_on_counts_above_sample_size():
+    import twoDSFS_class as T
+    d = {"c-1": {"calls": {"uv": (0, 3), "bv": (2, 0)}, "annotation": "x"},
+         "c-5": {"calls": {"uv": (1, 1), "bv": (1, 1)}, "annotation": "x"}}
+    obj = T.LikelihoodInference_jointSFS(None, None, pop1_size=1, pop2_size=1)
+    with pytest.raises(KeyError):
+        obj.combined_scan(d, 100)
+
+
+def test_dense_primitives_vs_oracle(golden):
+    p = golden.packed("synth_n50")
+    import twoDSFS_class as T
+    obj = T.LikelihoodInference_jointSFS(None, None, pop1="p1", pop2="p2", pop1_size=25, pop2_size=25)
+    d = p.subset_chroms([0])
+    bg = obj.calculate_2d_sfs(d)
+    win = p.subset_chroms([2])
+    fg = obj.calculate_2d_sfs(win)
+    ocfg = O.Cfg(25, 25)
+    g_fg = O.sfs2d(win, np.arange(win.n), ocfg)
+    g_bg = O.sfs2d(d, np.arange(d.n), ocfg)
+    assert fg == {(i, j): int(g_fg[i, j]) for i in range(51) for j in range(51)}
+    assert gu.close(obj.calculate_likelihood_2D(fg, bg), O.clr2d(g_fg, g_bg))
+    f1 = obj.fold_1d_sfs(obj.calculate_1d_sfs(win, "p1", 25, None, None, None))
+    b1 = obj.fold_1d_sfs(obj.calculate_1d_sfs(d, "p1", 25, None, None, None))
+    o1 = O.clr1d(O.fold1d(O.sfs1d(win, np.arange(win.n), 1, ocfg)), O.fold1d(O.sfs1d(d, np.arange(d.n), 1, ocfg)))
+    assert gu.close(obj.calculate_likelihood_1D(f1, b1), o1)
