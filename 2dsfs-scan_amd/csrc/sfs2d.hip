@@ -43,12 +43,21 @@ namespace {
 
 constexpr int WAVE = 64;
 constexpr int BLOCK = 256;
-constexpr int LNX_N = 65536;   // ln(k) table for k < LNX_N (window bin counts / window totals)
+constexpr int LNX_N = 1 << 20;  // ln(k) table for k < LNX_N (window bin counts / window totals)
 constexpr int REPL = 8;        // replicas of the per-chromosome background histograms
 constexpr int PW_MAX_LEAVES = 256;
 
 enum : uint32_t { ERR_KEY = 1u, ERR_GRID = 2u };
-enum : uint32_t { BGF_B2_ZERO = 1u, BGF_B1A_ZERO = 2u, BGF_B1B_ZERO = 4u, BGF_NAN2 = 8u, BGF_NAN1A = 16u, BGF_NAN1B = 32u };
+enum : uint32_t { BGF_B2_ZERO = 1u, BGF_B1A_ZERO = 2u, BGF_B1B_ZERO = 4u, BGF_NAN2 = 8u, BGF_NAN1A = 16u, BGF_NAN1B = 32u,
+                  BGF_FLOATV = 64u };
+
+// x_k / N == b_k / B bitwise (then scipy's two logpmf calls see identical proportions and T is
+// exactly 0.0).  Integer backgrounds: exact cross-multiplication (all products < 2^53, and for
+// x*B < 2^52 distinct rationals cannot round to the same double); normalised backgrounds: the
+// reference's own division.
+__device__ __forceinline__ bool prop_ok(uint32_t x, double N, double v, double B, bool floatv) {
+  return floatv ? ((double)x / N == v) : ((double)x * B == v * N);
+}
 
 struct KParams {
   int n1p, n2p, n1, n2;  // diploid sizes and haploid sample sizes
@@ -75,8 +84,8 @@ struct Chunk {  // k_scan work item: window slots [slot_lo, slot_hi) of one chro
 };
 
 struct PL {     // per-bin background table entry
-  double p;     // b_k / B (unadjusted), compared bitwise with x_k / N
   double lp;    // log of the proportion scipy uses (p[-1] adjusted on the last inner bin)
+  double v;     // integer backgrounds: the count b_k; normalised (float) backgrounds: p_k = b_k / B
 };
 
 struct BgHead {
@@ -85,6 +94,20 @@ struct BgHead {
 };
 
 static_assert(sizeof(sfs2d_window) == 64, "window record must be 64 bytes");
+
+// Diagnostic build only (-DSFS2D_STAMPS): wall-clock stamps (s_memrealtime, 100 MHz) of block 0 at
+// phase boundaries, read back with sfs2d__debug_stamps.  The shipped library executes none.
+#ifdef SFS2D_STAMPS
+__device__ unsigned long long g_stamps[64];
+#define STAMP(i)                                                                   \
+  do {                                                                             \
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
 
 // ------------------------------------------------------------------------------------------
 // device helpers
@@ -120,6 +143,8 @@ __device__ __forceinline__ int fold_inner(int a, int n, int np_) {
   int f = min(a, n - a);
   return (f >= 1 && f <= np_ - 1) ? f : -1;
 }
+
+__device__ __forceinline__ uint32_t wid_of(uint32_t p, uint32_t ws) { return p ? (p - 1u) / ws : 0u; }
 
 __device__ __forceinline__ double lnx_of(const double* lnx, uint32_t x) {
   return x < (uint32_t)LNX_N ? lnx[x] : log((double)x);
@@ -208,55 +233,102 @@ __global__ void k_init_lnx(double* lnx) {
 // ------------------------------------------------------------------------------------------
 // K1: background histograms + fixed-bp window segmentation
 
+constexpr int BLOCK1 = 512;   // k_bg_seg workgroup
+
 template <bool DO_BG, bool DO_SEG, bool LDS_HIST>
-__global__ __launch_bounds__(BLOCK) void k_bg_seg(KParams P, const uint32_t* __restrict__ counts,
-                                                  const uint32_t* __restrict__ pos, const uint16_t* __restrict__ ann,
-                                                  const Tile* __restrict__ tiles, const long long* __restrict__ chrom_off,
-                                                  const unsigned long long* __restrict__ slot_base,
-                                                  uint32_t* __restrict__ repl, uint2* __restrict__ slots,
-                                                  uint32_t* __restrict__ err_word) {
+__global__ __launch_bounds__(BLOCK1) void k_bg_seg(KParams P, const uint32_t* __restrict__ counts,
+                                                   const uint32_t* __restrict__ pos, const uint16_t* __restrict__ ann,
+                                                   const Tile* __restrict__ tiles, const long long* __restrict__ chrom_off,
+                                                   const unsigned long long* __restrict__ slot_base,
+                                                   uint32_t* __restrict__ repl, uint2* __restrict__ slots,
+                                                   uint32_t* __restrict__ err_word) {
   extern __shared__ uint32_t sh_hist[];
+  STAMP(20);
   const Tile t = tiles[blockIdx.x];
   uint32_t* gh = repl + ((size_t)(blockIdx.x % REPL) * P.nchrom + t.chrom) * (size_t)P.nh;
   uint32_t* H = LDS_HIST ? sh_hist : gh;
   if (DO_BG && LDS_HIST) {
-    for (int k = threadIdx.x; k < P.nh; k += BLOCK) sh_hist[k] = 0u;
+    for (int k = threadIdx.x; k < P.nh; k += BLOCK1) sh_hist[k] = 0u;
     __syncthreads();
   }
   const long long cb = chrom_off[t.chrom], ce = chrom_off[t.chrom + 1];
   const unsigned long long sbase = DO_SEG ? slot_base[t.chrom] : 0ull;
-  const bool need_pos = DO_SEG || P.has_start || P.has_end;
+  const bool pos_filter = P.has_start || P.has_end;
+  const bool need_pos = DO_SEG || pos_filter;
+  const int lane = threadIdx.x & (WAVE - 1);
   uint32_t err = 0;
-  for (uint32_t i = t.begin + threadIdx.x; i < t.end; i += BLOCK) {
-    const uint32_t c = counts[i];
-    const uint32_t p = need_pos ? pos[i] : 0u;
-    if (DO_BG) {
-      const bool pass = snp_pass(P, p, ann, i);
-      const int k2 = bin2d(P, c, pass, err);
-      const int a1 = alt_raw((c >> 8) & 0xff, P.n1, pass, err);
-      const int a2 = alt_raw(c >> 24, P.n2, pass, err);
-      if (k2 >= 0) atomicAdd(&H[k2], 1u);
-      if (a1 >= 0) atomicAdd(&H[P.h1a + a1], 1u);
-      if (a2 >= 0) atomicAdd(&H[P.h1b + a2], 1u);
+
+  // one 16-B vector = 4 consecutive SNPs; elements outside [t.begin, t.end) are masked
+  auto process = [&](uint32_t i0, const uint4& cv, const uint4& pv, uint32_t pprev, uint32_t pnext) {
+    const uint32_t cc[4] = {cv.x, cv.y, cv.z, cv.w};
+    const uint32_t pp[4] = {pv.x, pv.y, pv.z, pv.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t i = i0 + k;
+      if (i < t.begin || i >= t.end) continue;
+      const uint32_t c = cc[k];
+      const uint32_t p = pp[k];
+      if (DO_BG) {
+        bool pass = true;
+        if (pos_filter) pass = snp_pass(P, p, ann, i);
+        else if (P.ann_want >= 0) pass = (int)ann[i] == P.ann_want;
+        const int k2 = bin2d(P, c, pass, err);
+        const int a1 = alt_raw((c >> 8) & 0xff, P.n1, pass, err);
+        const int a2 = alt_raw(c >> 24, P.n2, pass, err);
+        if (k2 >= 0) atomicAdd(&H[k2], 1u);
+        if (a1 >= 0) atomicAdd(&H[P.h1a + a1], 1u);
+        if (a2 >= 0) atomicAdd(&H[P.h1b + a2], 1u);
+      }
+      if (DO_SEG) {
+        // window id (pos-1)//ws: the reference's start += ws*((pos-start)//ws) from start=1 (:894, :948)
+        const uint32_t w = wid_of(p, P.ws);
+        const uint32_t qp = k ? pp[k - 1] : pprev;
+        const uint32_t qn = k < 3 ? pp[k + 1] : pnext;
+        const bool first = ((long long)i == cb) || (wid_of(qp, P.ws) != w);
+        const bool last = ((long long)i + 1 == ce) || (wid_of(qn, P.ws) != w);
+        const unsigned long long s = sbase + w;
+        if (first) slots[s].x = i + 1u;  // 0 = unset; the scan kernel clears what it consumed
+        if (last) slots[s].y = i + 1u;
+      }
     }
+  };
+  // neighbours of a vector's first / last SNP: from the adjacent lanes, else from memory
+  auto neighbours = [&](uint32_t i0, const uint4& pv, uint32_t& pprev, uint32_t& pnext) {
+    pprev = __shfl_up(pv.w, 1, WAVE);
+    pnext = __shfl_down(pv.x, 1, WAVE);
+    if (lane == 0 && (long long)i0 > cb && i0 > 0) pprev = pos[i0 - 1];
+    if ((lane == WAVE - 1 || i0 + 4 >= t.end) && (long long)i0 + 4 < ce) pnext = pos[i0 + 4];
+  };
+
+  STAMP(21);
+  // two vectors per thread in flight per step (8 SNPs, 32 B of counts + positions)
+  constexpr uint32_t STEP = 8 * BLOCK1;
+  const uint32_t ab = t.begin & ~3u;
+  for (uint32_t base = ab; base < t.end; base += STEP) {
+    const uint32_t ia = base + 4 * threadIdx.x, ib = ia + 4 * BLOCK1;
+    const bool la = ia < t.end, lb = ib < t.end;
+    const uint4 ca = la ? *reinterpret_cast<const uint4*>(counts + ia) : make_uint4(0, 0, 0, 0);
+    const uint4 cbv = lb ? *reinterpret_cast<const uint4*>(counts + ib) : make_uint4(0, 0, 0, 0);
+    const uint4 pa = (need_pos && la) ? *reinterpret_cast<const uint4*>(pos + ia) : make_uint4(0, 0, 0, 0);
+    const uint4 pb = (need_pos && lb) ? *reinterpret_cast<const uint4*>(pos + ib) : make_uint4(0, 0, 0, 0);
+    uint32_t pva = 0, pna = 0, pvb = 0, pnb = 0;
     if (DO_SEG) {
-      // window id (pos-1)//ws: the reference's start += ws*((pos-start)//ws) from start=1 (:894, :948)
-      const uint32_t w = p ? (p - 1u) / P.ws : 0u;
-      const bool first = ((long long)i == cb) || ((pos[i - 1] ? (pos[i - 1] - 1u) / P.ws : 0u) != w);
-      const bool last = ((long long)i + 1 == ce) || ((pos[i + 1] ? (pos[i + 1] - 1u) / P.ws : 0u) != w);
-      const unsigned long long s = sbase + w;
-      if (first) slots[s].x = i + 1u;  // 0 = unset; the scan kernel clears what it consumed
-      if (last) slots[s].y = i + 1u;
+      neighbours(ia, pa, pva, pna);
+      neighbours(ib, pb, pvb, pnb);
     }
+    process(ia, ca, pa, pva, pna);
+    process(ib, cbv, pb, pvb, pnb);
   }
+  STAMP(22);
   if (err) atomicOr(err_word, err);
   if (DO_BG && LDS_HIST) {
     __syncthreads();
-    for (int k = threadIdx.x; k < P.nh; k += BLOCK) {
+    for (int k = threadIdx.x; k < P.nh; k += BLOCK1) {
       const uint32_t v = sh_hist[k];
       if (v) atomicAdd(&gh[k], v);
     }
   }
+  STAMP(23);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -264,134 +336,169 @@ __global__ __launch_bounds__(BLOCK) void k_bg_seg(KParams P, const uint32_t* __r
 
 // numpy pairwise_sum leaf (numpy/_core/src/umath/loops_utils.h.src): n < 8 sequential from 0.0,
 // n <= 128: eight strided accumulators combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) + tail.
-__device__ double np_leaf_sum(const PL* a, int n) {
+// `a` is a generic pointer (LDS or global), element i at a[i * stride].
+__device__ double np_leaf_sum(const double* a, int stride, int n) {
   if (n < 8) {
     double r = 0.0;
-    for (int i = 0; i < n; ++i) r += a[i].p;
+    for (int i = 0; i < n; ++i) r += a[i * stride];
     return r;
   }
-  double r0 = a[0].p, r1 = a[1].p, r2 = a[2].p, r3 = a[3].p, r4 = a[4].p, r5 = a[5].p, r6 = a[6].p, r7 = a[7].p;
+  double r0 = a[0], r1 = a[stride], r2 = a[2 * stride], r3 = a[3 * stride];
+  double r4 = a[4 * stride], r5 = a[5 * stride], r6 = a[6 * stride], r7 = a[7 * stride];
   int i = 8;
   for (; i < n - (n % 8); i += 8) {
-    r0 += a[i].p; r1 += a[i + 1].p; r2 += a[i + 2].p; r3 += a[i + 3].p;
-    r4 += a[i + 4].p; r5 += a[i + 5].p; r6 += a[i + 6].p; r7 += a[i + 7].p;
+    const double* q = a + (size_t)i * stride;
+    r0 += q[0]; r1 += q[stride]; r2 += q[2 * stride]; r3 += q[3 * stride];
+    r4 += q[4 * stride]; r5 += q[5 * stride]; r6 += q[6 * stride]; r7 += q[7 * stride];
   }
   double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-  for (; i < n; ++i) res += a[i].p;
+  for (; i < n; ++i) res += a[(size_t)i * stride];
   return res;
 }
 
-__global__ __launch_bounds__(BLOCK) void k_bg_finalize(KParams P, int from_repl, int integer_values,
-                                                       uint32_t* __restrict__ repl, double* __restrict__ bgval,
-                                                       PL* __restrict__ tab, BgHead* __restrict__ head,
-                                                       const int2* __restrict__ pw_leaves, int pw_nleaves,
-                                                       const short* __restrict__ pw_prog, int pw_nprog) {
-  __shared__ double red[3][BLOCK / WAVE];
+constexpr int FBLOCK = 1024;            // k_bg_finalize workgroup
+constexpr int FIN_LDS_BINS = 12288;     // backgrounds with nt <= this keep values / proportions in LDS
+
+// One workgroup per background.  from_repl: per-chromosome background from the k_bg_seg replicas
+// (summed, folded, and cleared for the next run); else bgval was uploaded (supplied background).
+// The values v, then the proportions p (overwriting v), live in LDS when they fit.
+__global__ __launch_bounds__(FBLOCK) void k_bg_finalize(KParams P, int from_repl, int integer_values,
+                                                        uint32_t* __restrict__ repl, double* __restrict__ bgval,
+                                                        PL* __restrict__ tab, BgHead* __restrict__ head,
+                                                        const int2* __restrict__ pw_leaves, int pw_nleaves,
+                                                        const short* __restrict__ pw_prog, int pw_nprog) {
+  extern __shared__ double v_lds[];
+  __shared__ double red[3][FBLOCK / WAVE];
   __shared__ uint32_t u1[2 * 256 + 2];
   __shared__ double leafsum[PW_MAX_LEAVES];
+  __shared__ short prog_s[2 * PW_MAX_LEAVES];
+  __shared__ double padj1[2];
+  __shared__ double pw_stack[32];
   __shared__ double Bs[3];
   const int b = blockIdx.x;
-  double* v = bgval + (size_t)b * P.nt;
+  const int tid = threadIdx.x;
+  const bool in_lds = P.nt <= FIN_LDS_BINS;
+  double* gv = bgval + (size_t)b * P.nt;
+  double* V = in_lds ? v_lds : gv;
   PL* T = tab + (size_t)b * P.nt;
 
+  STAMP(0);
+  for (int i = tid; i < pw_nprog; i += FBLOCK) prog_s[i] = pw_prog[i];
   if (from_repl) {
-    // replica sum (and clear, so the next run starts from zero); 1D spectra are folded:
+    // replica sum with all REPL loads of a bin in flight; 1D spectra are folded:
     // folded[f] = u[f] + u[2n - f] (f < n), folded[n] = u[n] (fold_1d_sfs, :446-463)
-    for (int k = threadIdx.x; k < P.nh; k += BLOCK) {
+    const size_t rstride = (size_t)P.nchrom * P.nh;
+    for (int k = tid; k < P.nh; k += FBLOCK) {
+      uint32_t* q = repl + (size_t)b * P.nh + k;
+      uint32_t x[REPL];
+#pragma unroll
+      for (int r = 0; r < REPL; ++r) x[r] = q[r * rstride];
       uint32_t s = 0;
 #pragma unroll
-      for (int r = 0; r < REPL; ++r) {
-        uint32_t* q = repl + ((size_t)r * P.nchrom + b) * (size_t)P.nh + k;
-        s += *q;
-        *q = 0u;
-      }
-      if (k < P.nb2) v[k] = (double)s;
+      for (int r = 0; r < REPL; ++r) { s += x[r]; if (x[r]) q[r * rstride] = 0u; }
+      if (k < P.nb2) V[k] = (double)s;
       else u1[k - P.nb2] = s;
     }
     __syncthreads();
-    for (int f = threadIdx.x; f <= P.n1p; f += BLOCK)
-      v[P.t1a + f] = (double)u1[f] + (f < P.n1p ? (double)u1[P.n1 - f] : 0.0);
-    for (int f = threadIdx.x; f <= P.n2p; f += BLOCK)
-      v[P.t1b + f] = (double)u1[(P.n1 + 1) + f] + (f < P.n2p ? (double)u1[(P.n1 + 1) + P.n2 - f] : 0.0);
-    __syncthreads();
+    for (int f = tid; f <= P.n1p; f += FBLOCK)
+      V[P.t1a + f] = (double)u1[f] + (f < P.n1p ? (double)u1[P.n1 - f] : 0.0);
+    for (int f = tid; f <= P.n2p; f += FBLOCK)
+      V[P.t1b + f] = (double)u1[(P.n1 + 1) + f] + (f < P.n2p ? (double)u1[(P.n1 + 1) + P.n2 - f] : 0.0);
+  } else if (in_lds) {
+    for (int k = tid; k < P.nt; k += FBLOCK) V[k] = gv[k];
   }
+  __syncthreads();
 
+  STAMP(1);
   // inner sums B over bins[1:-1]: exact for integer values in any order; for normalised
   // (float) values the reference's builtin sum() is sequential, so one lane adds in order.
   const int M2 = P.nb2 - 2, M1a = P.n1p - 1, M1b = P.n2p - 1;
   if (integer_values) {
     double s2 = 0.0, sa = 0.0, sb = 0.0;
-    for (int k = threadIdx.x; k < M2; k += BLOCK) s2 += v[1 + k];
-    for (int k = threadIdx.x; k < M1a; k += BLOCK) sa += v[P.t1a + 1 + k];
-    for (int k = threadIdx.x; k < M1b; k += BLOCK) sb += v[P.t1b + 1 + k];
+    for (int k = tid; k < M2; k += FBLOCK) s2 += V[1 + k];
+    for (int k = tid; k < M1a; k += FBLOCK) sa += V[P.t1a + 1 + k];
+    for (int k = tid; k < M1b; k += FBLOCK) sb += V[P.t1b + 1 + k];
     s2 = wave_sum_d(s2); sa = wave_sum_d(sa); sb = wave_sum_d(sb);
-    if ((threadIdx.x & (WAVE - 1)) == 0) {
-      red[0][threadIdx.x / WAVE] = s2; red[1][threadIdx.x / WAVE] = sa; red[2][threadIdx.x / WAVE] = sb;
+    if ((tid & (WAVE - 1)) == 0) {
+      red[0][tid / WAVE] = s2; red[1][tid / WAVE] = sa; red[2][tid / WAVE] = sb;
     }
     __syncthreads();
-    if (threadIdx.x < 3) {
+    if (tid < 3) {
       double t = 0.0;
-      for (int w = 0; w < BLOCK / WAVE; ++w) t += red[threadIdx.x][w];
-      Bs[threadIdx.x] = t;
+      for (int w = 0; w < FBLOCK / WAVE; ++w) t += red[tid][w];
+      Bs[tid] = t;
     }
-  } else if (threadIdx.x == 0) {
+  } else if (tid == 0) {
     double s2 = 0.0, sa = 0.0, sb = 0.0;
-    for (int k = 0; k < M2; ++k) s2 += v[1 + k];
-    for (int k = 0; k < M1a; ++k) sa += v[P.t1a + 1 + k];
-    for (int k = 0; k < M1b; ++k) sb += v[P.t1b + 1 + k];
+    for (int k = 0; k < M2; ++k) s2 += V[1 + k];
+    for (int k = 0; k < M1a; ++k) sa += V[P.t1a + 1 + k];
+    for (int k = 0; k < M1b; ++k) sb += V[P.t1b + 1 + k];
     Bs[0] = s2; Bs[1] = sa; Bs[2] = sb;
   }
   __syncthreads();
   const double B2 = Bs[0], B1a = Bs[1], B1b = Bs[2];
+  STAMP(2);
 
-  // proportions p = v / B (Python true division == IEEE division here) and their logs
-  for (int k = threadIdx.x; k < P.nt; k += BLOCK) {
-    double B = k < P.nb2 ? B2 : (k < P.t1b ? B1a : B1b);
-    double p = (B != 0.0) ? v[k] / B : 0.0;
-    T[k].p = p;
-    T[k].lp = log(p);
+  // proportions p = v / B (Python true division == IEEE division here) and their logs; p
+  // overwrites v for the pairwise p[:-1] sums below
+  for (int k = tid; k < P.nt; k += FBLOCK) {
+    const double B = k < P.nb2 ? B2 : (k < P.t1b ? B1a : B1b);
+    const double val = V[k];
+    const double p = (B != 0.0) ? val / B : 0.0;
+    PL e;
+    e.lp = log(p);
+    e.v = integer_values ? val : p;
+    T[k] = e;
+    V[k] = p;
   }
   __syncthreads();
+  STAMP(3);
 
   // scipy multinomial._process_parameters: p[-1] <- 1 - sum(p[:-1]) when |.| > 1e-15, and the
   // whole logpmf is NaN if any p < 0.  sum(p[:-1]) is numpy's pairwise sum over the inner bins
   // except the last: the 2D tree plan (leaves + postfix program) comes from the host.
-  if (threadIdx.x < pw_nleaves) {
-    int2 lf = pw_leaves[threadIdx.x];
-    leafsum[threadIdx.x] = np_leaf_sum(T + 1 + lf.x, lf.y);
+  if (tid < pw_nleaves) {
+    const int2 lf = pw_leaves[tid];
+    leafsum[tid] = np_leaf_sum(V + 1 + lf.x, 1, lf.y);
+  } else if (tid == PW_MAX_LEAVES && M1a >= 1) {
+    padj1[0] = 1.0 - np_leaf_sum(V + P.t1a + 1, 1, M1a - 1);
+  } else if (tid == PW_MAX_LEAVES + WAVE && M1b >= 1) {
+    padj1[1] = 1.0 - np_leaf_sum(V + P.t1b + 1, 1, M1b - 1);
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t flags = 0;
+  STAMP(4);
+  if (tid == 0) {
+    uint32_t flags = integer_values ? 0u : BGF_FLOATV;
     if (B2 == 0.0) flags |= BGF_B2_ZERO;
     if (B1a == 0.0) flags |= BGF_B1A_ZERO;
     if (B1b == 0.0) flags |= BGF_B1B_ZERO;
     if (M2 >= 1 && B2 != 0.0) {
-      double st[24];
+      // postfix evaluation; the stack lives in LDS (a runtime-indexed private array would be scratch)
       int sp = 0;
       for (int i = 0; i < pw_nprog; ++i) {
-        short op = pw_prog[i];
-        if (op >= 0) st[sp++] = leafsum[op];
-        else { double r = st[--sp]; st[sp - 1] = st[sp - 1] + r; }
+        const short op = prog_s[i];
+        if (op >= 0) pw_stack[sp++] = leafsum[op];
+        else { const double r = pw_stack[--sp]; pw_stack[sp - 1] = pw_stack[sp - 1] + r; }
       }
-      double S = sp ? st[0] : 0.0;
-      double padj = 1.0 - S;
+      const double S = sp ? pw_stack[0] : 0.0;
+      const double padj = 1.0 - S;
       if (padj < -1e-15) flags |= BGF_NAN2;
       else if (fabs(padj) > 1e-15) T[1 + M2 - 1].lp = log(padj);
     }
     if (M1a >= 1 && B1a != 0.0) {
-      double padj = 1.0 - np_leaf_sum(T + P.t1a + 1, M1a - 1);
+      const double padj = padj1[0];
       if (padj < -1e-15) flags |= BGF_NAN1A;
       else if (fabs(padj) > 1e-15) T[P.t1a + M1a].lp = log(padj);
     }
     if (M1b >= 1 && B1b != 0.0) {
-      double padj = 1.0 - np_leaf_sum(T + P.t1b + 1, M1b - 1);
+      const double padj = padj1[1];
       if (padj < -1e-15) flags |= BGF_NAN1B;
       else if (fabs(padj) > 1e-15) T[P.t1b + M1b].lp = log(padj);
     }
     BgHead h;
     h.B2 = B2; h.B1a = B1a; h.B1b = B1b; h.flags = flags; h.pad = 0;
     head[b] = h;
+    STAMP(5);
   }
 }
 
@@ -465,7 +572,7 @@ __device__ __forceinline__ WinOut eval_window(const KParams& P, const uint32_t* 
       if (x) {
         const PL t = T2[k2];
         s2 += (double)x * (lnx_of(lnx, x) - t.lp);
-        q2 &= ((double)x / N2 == t.p);
+        q2 &= prop_ok(x, N2, t.v, hb.B2, hb.flags & BGF_FLOATV);
       }
     }
     if (f1 >= 0) {
@@ -473,7 +580,7 @@ __device__ __forceinline__ WinOut eval_window(const KParams& P, const uint32_t* 
       if (x) {
         const PL t = T1a[f1];
         sa += (double)x * (lnx_of(lnx, x) - t.lp);
-        qa &= ((double)x / N1a == t.p);
+        qa &= prop_ok(x, N1a, t.v, hb.B1a, hb.flags & BGF_FLOATV);
       }
     }
     if (f2 >= 0) {
@@ -481,7 +588,7 @@ __device__ __forceinline__ WinOut eval_window(const KParams& P, const uint32_t* 
       if (x) {
         const PL t = T1b[f2];
         sb += (double)x * (lnx_of(lnx, x) - t.lp);
-        qb &= ((double)x / N1b == t.p);
+        qb &= prop_ok(x, N1b, t.v, hb.B1b, hb.flags & BGF_FLOATV);
       }
     }
   }
@@ -513,8 +620,6 @@ __device__ __forceinline__ void write_rec(sfs2d_window* o, uint32_t chrom, uint3
   *o = r;
 }
 
-__device__ __forceinline__ uint32_t wid_of(uint32_t p, uint32_t ws) { return p ? (p - 1u) / ws : 0u; }
-
 // first index j in [cb, e) such that SNPs j..e-1 share the fixed-bp window of SNP e-1.
 // Wave-level (every wave of the group computes the same answer).
 __device__ uint32_t window_begin_back(const uint32_t* __restrict__ pos, long long cb, uint32_t e, uint32_t ws) {
@@ -528,6 +633,13 @@ __device__ uint32_t window_begin_back(const uint32_t* __restrict__ pos, long lon
     if (m) return (uint32_t)(hi - __builtin_ctzll(m));
     hi -= WAVE;
   }
+}
+
+// Per-element bins of the window's first 512 SNPs, kept in registers between the two phases:
+// bits 0-15 inner 2D bin (0xffff none), 16-23 / 24-31 folded inner 1D bins (0xff none).
+__device__ __forceinline__ uint32_t pack_bins(int k2, int f1, int f2) {
+  return (uint32_t)(k2 < 0 ? 0xffff : k2) | ((uint32_t)(f1 < 0 ? 0xff : f1) << 16) |
+         ((uint32_t)(f2 < 0 ? 0xff : f2) << 24);
 }
 
 template <int G, bool P16>
@@ -580,34 +692,337 @@ __global__ __launch_bounds__(BLOCK) void k_scan(KParams P, const uint32_t* __res
         b = (uint32_t)(cb + (long long)wid * P.ws);
         e = b + P.ws;
       }
-      WinOut w = eval_window<G, P16>(P, counts, pos, ann, b, e, T, hb, lnx, H2, H1, redd, redu, err);
+      const WinOut w = eval_window<G, P16>(P, counts, pos, ann, b, e, T, hb, lnx, H2, H1, redd, redu, err);
       if (lane == 0) {
         write_rec(out + s, ch.chrom, wid, b, e, w, bg_zero_flags(hb));
         if (mode_bp) slots[s] = make_uint2(0u, 0u);   // leave the slot table clean for the next run
       }
     }
-  } else if (g == 0) {
-    // Q9 helper (combined_scan's final block, twoDSFS_class.py:951-989): the window before the
-    // last one, evaluated against the LAST window's chromosome background (ch.chrom).
-    const long long ce = chrom_off[ch.chrom + 1];
-    const uint32_t bl = window_begin_back(pos, cb, (uint32_t)ce, P.ws);
-    WinOut w;
-    memset(&w, 0, sizeof(w));
-    uint32_t pb = 0, pe = 0, pc = ch.chrom, flags = SFS2D_W_EXTRA | bg_zero_flags(hb);
-    if (bl > 0) {
-      pe = bl;
-      int c2 = (int)ch.chrom;
-      while (c2 > 0 && chrom_off[c2] >= (long long)pe) --c2;
-      pc = (uint32_t)c2;
-      pb = window_begin_back(pos, chrom_off[c2], pe, P.ws);
-      w = eval_window<G, P16>(P, counts, pos, ann, pb, pe, T, hb, lnx, H2, H1, redd, redu, err);
-    } else {
-      flags |= SFS2D_W_EMPTY;
-    }
-    if (lane == 0) write_rec(out + extra_rec, pc, bl, pb, pe, w, flags);
   }
   if (err) atomicOr(err_word, err);
 }
+
+// ------------------------------------------------------------------------------------------
+// K3 (small grids): one wavefront per window, windows software-pipelined.
+//
+// Per window: the first 512 SNPs arrive as two 16-B loads per lane (issued while the previous
+// window finishes), their bins are kept in registers (pack_bins) between the histogram pass and
+// the take pass, longer windows stream further 512-SNP chunks.  In the take pass every lane
+// gathers table entries and ln x for all its elements at once (no load behind a branch), then
+// the owner lanes accumulate.  Counts come from ballots; only three fp64 sums are reduced.
+
+struct Win {
+  uint32_t b, e;
+  uint4 v0, v1;   // first chunk (SNPs [b & ~3, +512))
+  bool has;
+};
+
+__device__ __forceinline__ uint4 ld4(const uint32_t* __restrict__ a, uint32_t i, uint32_t e) {
+  return i < e ? *reinterpret_cast<const uint4*>(a + i) : make_uint4(0, 0, 0, 0);
+}
+
+// Branch-free classification of one SNP (same rules as bin2d / alt_raw / fold_inner).
+struct Cls {
+  int k2, g1, g2;          // 2D bin, folded 1D bins
+  bool v2, in2, v1a, v1b;  // inner 2D bin / any 2D bin (incl. (n1,n2)) / inner folded 1D bins
+};
+
+__device__ __forceinline__ Cls classify_bf(const KParams& P, uint32_t c, bool pass, uint32_t& err) {
+  const int r1 = c & 0xff, a1 = (c >> 8) & 0xff, r2 = (c >> 16) & 0xff, a2 = c >> 24;
+  const bool sw = P.fold & (a1 + a2 > P.n1p + P.n2p);
+  const int x1 = sw ? r1 : a1, x2 = sw ? r2 : a2;
+  const bool nz = (x1 | x2) != 0;
+  const bool oob = (x1 > P.n1) | (x2 > P.n2);
+  const bool ka = a1 > P.n1, kb = a2 > P.n2;
+  err |= (pass & nz & oob) ? ERR_GRID : 0u;
+  err |= (pass & (ka | kb)) ? ERR_KEY : 0u;
+  Cls r;
+  r.k2 = x1 * (P.n2 + 1) + x2;
+  r.in2 = pass & nz & !oob;
+  r.v2 = r.in2 & (r.k2 != P.nb2 - 1);
+  r.g1 = min(a1, P.n1 - a1);
+  r.g2 = min(a2, P.n2 - a2);
+  r.v1a = pass & (a1 != 0) & !ka & (r.g1 >= 1) & (r.g1 <= P.n1p - 1);
+  r.v1b = pass & (a2 != 0) & !kb & (r.g2 >= 1) & (r.g2 <= P.n2p - 1);
+  return r;
+}
+
+// Take pass over 8 elements for histogram h (0: 2D, 1: pop1 1D, 2: pop2 1D): LDS take-and-clear
+// (skipped elements hit the lane's private trash word), then every table / ln-x gather is issued
+// before any is used.  Called in a runtime loop over h so that only one histogram's 8 gathers are
+// live at a time (the compiler otherwise interleaves all three and runs out of registers).
+template <bool P16>
+__device__ __forceinline__ double take_accumulate(int h, const uint32_t (&bins)[8], uint32_t* W, uint32_t trash,
+                                                  int toff, const PL* __restrict__ T, const double* __restrict__ lnx) {
+  const uint32_t shift = h == 0 ? 0u : (h == 1 ? 16u : 24u);
+  const uint32_t msk = h == 0 ? 0xffffu : 0xffu;
+  uint32_t x[8];
+  int kk[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t k = (bins[j] >> shift) & msk;
+    const bool valid = k != msk;
+    uint32_t xv;
+    if (P16 && h == 0) {
+      const uint32_t sh = (k & 1) << 4;
+      const uint32_t old = atomicAnd(&W[valid ? (k >> 1) : trash], valid ? ~(0xffffu << sh) : 0u);
+      xv = valid ? (old >> sh) & 0xffffu : 0u;
+    } else {
+      const uint32_t old = atomicExch(&W[valid ? (uint32_t)toff + k : trash], 0u);
+      xv = valid ? old : 0u;
+    }
+    x[j] = xv;
+    kk[j] = xv ? (int)k : 0;
+  }
+  double lp[8], lx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    lp[j] = T[kk[j]].lp;
+    lx[j] = lnx[x[j]];          // x < LNX_N: windows of >= LNX_N SNPs take the exact path
+  }
+  double s = 0.0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += x[j] ? (double)x[j] * (lx[j] - lp[j]) : 0.0;
+  return s;
+}
+
+// |T| this small may be an exactly proportional window (reference: T == 0.0 exactly, which its
+// truthiness guard reads as False): such windows are re-evaluated with the exact bin-by-bin test.
+__device__ __forceinline__ bool suspect_zero(double S, uint32_t N, const double* lnx) {
+  const double n = (double)N;
+  return N && fabs(2.0 * (S - n * lnx[N])) <= 1e-9 * (n + 1.0);
+}
+
+__device__ __forceinline__ double clr_fast(double S, uint32_t N, bool nan_bg, const double* lnx) {
+  return nan_bg ? __builtin_nan("") : 2.0 * (S - (double)N * lnx[N]);
+}
+
+constexpr int TRASH = WAVE;   // lane-private scratch words after each wave's histograms
+
+template <bool P16>
+__global__ __launch_bounds__(BLOCK) void k_scan_w(KParams P, const uint32_t* __restrict__ counts,
+                                                  const uint32_t* __restrict__ pos, const uint16_t* __restrict__ ann,
+                                                  const Chunk* __restrict__ chunks, const long long* __restrict__ chrom_off,
+                                                  uint2* __restrict__ slots, const PL* __restrict__ tab,
+                                                  const BgHead* __restrict__ head, int bg_per_chrom,
+                                                  const double* __restrict__ lnx, sfs2d_window* __restrict__ out,
+                                                  uint32_t* __restrict__ err_word, int mode_bp) {
+  extern __shared__ uint32_t lds[];
+  STAMP(10);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int h2w = P16 ? (P.nb2 + 1) / 2 : P.nb2;
+  const int core = h2w + (P.n1p + 1) + (P.n2p + 1);
+  uint32_t* W = lds + wv * (core + TRASH);    // [2D bins | 1D pop1 | 1D pop2 | trash x 64]
+  const int t1a = h2w, t1b = h2w + P.n1p + 1;
+  const uint32_t trash = (uint32_t)(core + lane);
+  for (int k = lane; k < core + TRASH; k += WAVE) W[k] = 0u;
+
+  const Chunk ch = chunks[blockIdx.x];
+  const long long cb = chrom_off[ch.chrom];
+  const PL* T = tab + (bg_per_chrom ? (size_t)ch.chrom * P.nt : 0);
+  const BgHead hb = head[bg_per_chrom ? ch.chrom : 0];
+  const bool filt = P.ann_want >= 0 || P.has_start || P.has_end;
+  const bool posf = P.has_start || P.has_end;
+  const uint32_t zflags = bg_zero_flags(hb);
+  uint32_t err = 0;
+  group_sync<WAVE>();
+
+  auto bounds = [&](uint32_t s, uint2 sr, Win& w) {
+    if (mode_bp) {
+      w.has = sr.x != 0u;
+      w.b = sr.x - 1u;
+      w.e = sr.y;
+    } else {
+      w.has = true;
+      w.b = (uint32_t)(cb + (long long)(ch.wid_lo + (s - ch.slot_lo)) * P.ws);
+      w.e = w.b + P.ws;
+    }
+    if (w.has) {
+      const uint32_t i0 = (w.b & ~3u) + 4 * lane;
+      w.v0 = ld4(counts, i0, w.e);
+      w.v1 = ld4(counts, i0 + 4 * WAVE, w.e);
+    }
+  };
+  // element -> (pass, variant ok); filters read ann / pos at a clamped (always valid) index
+  auto passes = [&](uint32_t i, const Win& w, bool& var_ok) -> bool {
+    const bool valid = (i >= w.b) & (i < w.e);
+    var_ok = valid;
+    if (!filt) return valid;
+    const uint32_t ic = min(max(i, w.b), w.e - 1);
+    var_ok = valid & ((P.ann_want < 0) | ((int)ann[ic] == P.ann_want));
+    bool ok = var_ok;
+    if (posf) {
+      const long long p = (long long)pos[ic];
+      ok = ok & (!P.has_start | (p >= P.start_pos)) & (!P.has_end | (p <= P.end_pos));
+    }
+    return ok;
+  };
+
+  uint32_t s = ch.slot_lo + wv;
+  if (s >= ch.slot_hi) return;
+  Win cur;
+  STAMP(11);
+  bounds(s, mode_bp ? slots[s] : make_uint2(0, 0), cur);
+  int it = 0;
+  for (; s < ch.slot_hi; s += BLOCK / WAVE, ++it) {
+    const uint32_t sn = s + BLOCK / WAVE;
+    const bool more = sn < ch.slot_hi;
+    const uint2 srn = (mode_bp && more) ? slots[sn] : make_uint2(0, 0);
+    const uint32_t wid = ch.wid_lo + (s - ch.slot_lo);
+    uint32_t nvar = 0, nlast = 0, n2 = 0, n1a = 0, n1b = 0;
+    uint32_t kb[8];
+    const uint32_t a0 = cur.b & ~3u;
+    if (cur.has) {
+      // ---- histogram pass
+      for (uint32_t base = a0; base < cur.e; base += 8 * WAVE) {
+        const uint32_t i0 = base + 4 * lane, i1 = i0 + 4 * WAVE;
+        const uint4 c0 = base == a0 ? cur.v0 : ld4(counts, i0, cur.e);
+        const uint4 c1 = base == a0 ? cur.v1 : ld4(counts, i1, cur.e);
+        const uint32_t cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t i = (j < 4 ? i0 : i1) + (j & 3);
+          bool var_ok;
+          const bool pass = passes(i, cur, var_ok);
+          const Cls r = classify_bf(P, cc[j], pass, err);
+          if (filt) nvar += __popcll(__ballot(var_ok));
+          if (!P.fold) nlast += __popcll(__ballot(r.in2 & !r.v2));
+          n2 += __popcll(__ballot(r.v2));
+          if (base == a0) kb[j] = r.v2 ? (uint32_t)r.k2 : 0xffffu;
+          if (P16) atomicAdd(&W[r.v2 ? (uint32_t)(r.k2 >> 1) : trash], 1u << ((r.k2 & 1) << 4));
+          else atomicAdd(&W[r.v2 ? (uint32_t)r.k2 : trash], 1u);
+          atomicAdd(&W[r.v1a ? (uint32_t)(t1a + r.g1) : trash], 1u);
+          atomicAdd(&W[r.v1b ? (uint32_t)(t1b + r.g2) : trash], 1u);
+          __builtin_amdgcn_sched_barrier(0);   // one element at a time: keeps its lane masks short-lived
+        }
+      }
+    }
+    if (it == 0) STAMP(12);
+    // next window: slot record is in, issue its first chunk now (overlaps the take pass)
+    Win nxt;
+    nxt.has = false;
+    if (more) bounds(sn, srn, nxt);
+    if (cur.has) {
+      group_sync<WAVE>();
+      if (!filt) nvar = cur.e - cur.b;
+      double s2 = 0.0, sa = 0.0, sb = 0.0;
+      for (uint32_t base = a0; base < cur.e; base += 8 * WAVE) {
+        uint32_t bins[8];
+        if (base == a0) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bins[j] = kb[j];
+        } else {
+          const uint32_t i0 = base + 4 * lane, i1 = i0 + 4 * WAVE;
+          const uint4 c0 = ld4(counts, i0, cur.e), c1 = ld4(counts, i1, cur.e);
+          const uint32_t cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+          uint32_t e2 = 0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const uint32_t i = (j < 4 ? i0 : i1) + (j & 3);
+            bool var_ok;
+            const Cls r = classify_bf(P, cc[j], passes(i, cur, var_ok), e2);
+            bins[j] = r.v2 ? (uint32_t)r.k2 : 0xffffu;
+          }
+        }
+        s2 += take_accumulate<P16>(0, bins, W, trash, 0, T, lnx);
+      }
+      // the folded 1D spectra have pop_size-1 inner bins: one lane per bin reads and clears it
+      auto bin_pass = [&](int toff, int np_, const PL* Th, uint32_t& N) -> double {
+        double acc = 0.0;
+        uint32_t cnt = 0;
+        for (int k = 1 + lane; k <= np_ - 1; k += WAVE) {
+          const uint32_t x = W[toff + k];
+          W[toff + k] = 0u;
+          const double lp = Th[x ? k : 0].lp;
+          acc += x ? (double)x * (lnx[x] - lp) : 0.0;
+          cnt += x;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, WAVE);
+        N = cnt;
+        return wave_sum_d(acc);
+      };
+      if (it == 0) STAMP(13);
+      sa = bin_pass(t1a, P.n1p, T + P.t1a, n1a);
+      sb = bin_pass(t1b, P.n2p, T + P.t1b, n1b);
+      s2 = wave_sum_d(s2);
+      WinOut w;
+      if (cur.e - cur.b >= (uint32_t)LNX_N || suspect_zero(s2, n2, lnx) || suspect_zero(sa, n1a, lnx) ||
+          suspect_zero(sb, n1b, lnx)) {
+        // rare: exact re-evaluation with the bin-by-bin proportionality test
+        w = eval_window<WAVE, P16>(P, counts, pos, ann, cur.b, cur.e, T, hb, lnx, W, W + t1a, nullptr, nullptr, err);
+        if (lane == 0) atomicAdd(err_word + 1, 1u);   // statistics: windows that took the exact path
+      } else {
+        w.snp_count = nvar; w.n2_all = n2 + nlast; w.n2 = n2; w.n1a = n1a; w.n1b = n1b;
+        w.t2d = clr_fast(s2, n2, hb.flags & BGF_NAN2, lnx);
+        w.t1a = clr_fast(sa, n1a, hb.flags & BGF_NAN1A, lnx);
+        w.t1b = clr_fast(sb, n1b, hb.flags & BGF_NAN1B, lnx);
+      }
+      if (lane == 0) {
+        write_rec(out + s, ch.chrom, wid, cur.b, cur.e, w, zflags);
+        if (mode_bp) slots[s] = make_uint2(0u, 0u);   // leave the slot table clean for the next run
+      }
+      if (it == 0) STAMP(14);
+    } else if (lane == 0) {
+      sfs2d_window r;
+      memset(&r, 0, sizeof(r));
+      r.chrom = ch.chrom; r.wid = wid; r.flags = SFS2D_W_EMPTY;
+      out[s] = r;
+    }
+    cur = nxt;
+  }
+  STAMP(15);
+  if (err) atomicOr(err_word, err);
+}
+
+// Q9 helper (combined_scan's final block, twoDSFS_class.py:951-989): the window before the last
+// one, evaluated against the LAST window's chromosome background.  One workgroup, launched only
+// for plans with SFS2D_F_PREV_EXTRA.
+template <int G, bool P16>
+__global__ __launch_bounds__(BLOCK) void k_scan_extra(KParams P, const uint32_t* __restrict__ counts,
+                                                      const uint32_t* __restrict__ pos, const uint16_t* __restrict__ ann,
+                                                      uint32_t chrom_last, const long long* __restrict__ chrom_off,
+                                                      const PL* __restrict__ tab, const BgHead* __restrict__ head,
+                                                      int bg_per_chrom, const double* __restrict__ lnx,
+                                                      sfs2d_window* __restrict__ out, uint32_t* __restrict__ err_word,
+                                                      long long extra_rec) {
+  extern __shared__ uint32_t lds[];
+  constexpr int NG = BLOCK / G;
+  const int g = threadIdx.x / G;
+  const int lane = threadIdx.x & (G - 1);
+  const int h2w = P16 ? (P.nb2 + 1) / 2 : P.nb2;
+  const int per = h2w + (P.n1p + 1) + (P.n2p + 1);
+  uint32_t* H2 = lds + g * per;
+  uint32_t* H1 = H2 + h2w;
+  double* redd = reinterpret_cast<double*>(lds + NG * per + ((NG * per) & 1));
+  unsigned long long* redu = reinterpret_cast<unsigned long long*>(redd + 32);
+  for (int k = lane; k < per; k += G) H2[k] = 0u;
+  group_sync<G>();
+  if (g != 0) return;
+  uint32_t err = 0;
+  const long long cb = chrom_off[chrom_last];
+  const PL* T = tab + (bg_per_chrom ? (size_t)chrom_last * P.nt : 0);
+  const BgHead hb = head[bg_per_chrom ? chrom_last : 0];
+  const long long ce = chrom_off[chrom_last + 1];
+  const uint32_t bl = window_begin_back(pos, cb, (uint32_t)ce, P.ws);
+  WinOut w;
+  memset(&w, 0, sizeof(w));
+  uint32_t pb = 0, pe = 0, pc = chrom_last, flags = SFS2D_W_EXTRA | bg_zero_flags(hb);
+  if (bl > 0) {
+    pe = bl;
+    int c2 = (int)chrom_last;
+    while (c2 > 0 && chrom_off[c2] >= (long long)pe) --c2;
+    pc = (uint32_t)c2;
+    pb = window_begin_back(pos, chrom_off[c2], pe, P.ws);
+    w = eval_window<G, P16>(P, counts, pos, ann, pb, pe, T, hb, lnx, H2, H1, redd, redu, err);
+  } else {
+    flags |= SFS2D_W_EMPTY;
+  }
+  if (lane == 0) write_rec(out + extra_rec, pc, bl, pb, pe, w, flags);
+  if (err) atomicOr(err_word, err);
+}
+
 
 // ------------------------------------------------------------------------------------------
 // host side
@@ -663,6 +1078,7 @@ struct sfs2d_plan {
   bool p16 = true;
   size_t scan_lds = 0, bg_lds = 0;
   int64_t nslots = 0, nrec = 0, extra_rec = -1;
+  uint32_t last_chrom = 0;
   std::vector<Tile> tiles;
   std::vector<Chunk> chunks;
   Tile* d_tiles = nullptr;
@@ -720,6 +1136,13 @@ void plan_free(sfs2d_plan* p) {
 template <int G, bool P16>
 hipError_t launch_scan(sfs2d_plan* pl, sfs2d_window* out) {
   const sfs2d_data* d = pl->data;
+  if (G == WAVE) {
+    hipLaunchKernelGGL((k_scan_w<P16>), dim3((unsigned)pl->chunks.size()), dim3(BLOCK), pl->scan_lds,
+                       pl->ctx->stream, pl->K, d->counts, d->pos, d->ann, pl->d_chunks, d->d_chrom_off,
+                       pl->d_slots, pl->d_tab, pl->d_head, pl->prm.bg_mode == SFS2D_BG_PER_CHROM ? 1 : 0,
+                       pl->ctx->d_lnx, out, pl->d_err, pl->prm.window_mode == SFS2D_WINDOW_BP ? 1 : 0);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL((k_scan<G, P16>), dim3((unsigned)pl->chunks.size()), dim3(BLOCK), pl->scan_lds,
                      pl->ctx->stream, pl->K, d->counts, d->pos, d->ann, pl->d_chunks, d->d_chrom_off,
                      pl->d_slots, pl->d_tab, pl->d_head, pl->prm.bg_mode == SFS2D_BG_PER_CHROM ? 1 : 0,
@@ -731,7 +1154,7 @@ hipError_t launch_scan(sfs2d_plan* pl, sfs2d_window* out) {
 template <bool B, bool S, bool L>
 hipError_t launch_bgseg1(sfs2d_plan* pl) {
   const sfs2d_data* d = pl->data;
-  hipLaunchKernelGGL((k_bg_seg<B, S, L>), dim3((unsigned)pl->tiles.size()), dim3(BLOCK), L ? pl->bg_lds : 0,
+  hipLaunchKernelGGL((k_bg_seg<B, S, L>), dim3((unsigned)pl->tiles.size()), dim3(BLOCK1), L ? pl->bg_lds : 0,
                      pl->ctx->stream, pl->K, d->counts, d->pos, d->ann, pl->d_tiles, d->d_chrom_off,
                      pl->d_slot_base, pl->d_repl, pl->d_slots, pl->d_err);
   return hipGetLastError();
@@ -746,15 +1169,33 @@ hipError_t launch_bgseg(sfs2d_plan* pl) {
 }
 
 hipError_t launch_finalize(sfs2d_plan* pl, int from_repl, int integer_values) {
-  hipLaunchKernelGGL(k_bg_finalize, dim3(pl->nbg), dim3(BLOCK), 0, pl->ctx->stream, pl->K, from_repl, integer_values,
+  const size_t lds = pl->K.nt <= FIN_LDS_BINS ? sizeof(double) * pl->K.nt : 0;
+  hipLaunchKernelGGL(k_bg_finalize, dim3(pl->nbg), dim3(FBLOCK), lds, pl->ctx->stream, pl->K, from_repl, integer_values,
                      pl->d_repl, pl->d_bgval, pl->d_tab, pl->d_head, pl->d_leaves, pl->nleaves, pl->d_prog, pl->nprog);
   return hipGetLastError();
 }
 
+template <int G, bool P16>
+hipError_t launch_extra(sfs2d_plan* pl, sfs2d_window* out) {
+  const sfs2d_data* d = pl->data;
+  hipLaunchKernelGGL((k_scan_extra<G, P16>), dim3(1), dim3(BLOCK), pl->scan_lds, pl->ctx->stream, pl->K, d->counts,
+                     d->pos, d->ann, pl->last_chrom, d->d_chrom_off, pl->d_tab, pl->d_head,
+                     pl->prm.bg_mode == SFS2D_BG_PER_CHROM ? 1 : 0, pl->ctx->d_lnx, out, pl->d_err,
+                     (long long)pl->extra_rec);
+  return hipGetLastError();
+}
+
 hipError_t launch_scan_any(sfs2d_plan* pl, sfs2d_window* out) {
-  if (pl->chunks.empty()) return hipSuccess;
-  if (pl->G == 64) return pl->p16 ? launch_scan<64, true>(pl, out) : launch_scan<64, false>(pl, out);
-  return pl->p16 ? launch_scan<256, true>(pl, out) : launch_scan<256, false>(pl, out);
+  hipError_t e = hipSuccess;
+  if (!pl->chunks.empty()) {
+    if (pl->G == 64) e = pl->p16 ? launch_scan<64, true>(pl, out) : launch_scan<64, false>(pl, out);
+    else e = pl->p16 ? launch_scan<256, true>(pl, out) : launch_scan<256, false>(pl, out);
+  }
+  if (e == hipSuccess && pl->extra_rec >= 0) {
+    if (pl->G == 64) e = pl->p16 ? launch_extra<64, true>(pl, out) : launch_extra<64, false>(pl, out);
+    else e = pl->p16 ? launch_extra<256, true>(pl, out) : launch_extra<256, false>(pl, out);
+  }
+  return e;
 }
 
 }  // namespace
@@ -828,9 +1269,13 @@ int sfs2d_data_upload(sfs2d_ctx* ctx, const uint32_t* counts, const uint32_t* po
   d->ctx = ctx;
   d->owned = true;
   int rc = data_meta(ctx, d, chrom_off, nchrom, n);
-  if (!rc) rc = dalloc(ctx, &d->counts, (size_t)n + 1);
-  if (!rc) rc = dalloc(ctx, &d->pos, (size_t)n + 1);
-  if (!rc) rc = dalloc(ctx, &d->ann, (size_t)n + 1);
+  // padded: the kernels issue aligned 16-B loads that may run up to 15 bytes past element n-1
+  const size_t npad = ((size_t)n + 3) / 4 * 4 + 64;
+  if (!rc) rc = dalloc(ctx, &d->counts, npad);
+  if (!rc) rc = dalloc(ctx, &d->pos, npad);
+  if (!rc) rc = dalloc(ctx, &d->ann, npad);
+  if (!rc && (hipMemset(d->counts, 0, npad * 4) != hipSuccess || hipMemset(d->pos, 0, npad * 4) != hipSuccess))
+    rc = set_err(ctx, SFS2D_E_HIP, "hipMemset");
   if (rc) { hipFree(d->counts); hipFree(d->pos); hipFree(d->ann); hipFree(d->d_chrom_off); delete d; return rc; }
   hipError_t e = hipSuccess;
   if (n) {
@@ -869,6 +1314,10 @@ int sfs2d_data_wrap_device(sfs2d_ctx* ctx, const uint32_t* d_counts, const uint3
   d->owned = false;
   int rc = data_meta(ctx, d, chrom_off, nchrom, n);
   if (rc) { hipFree(d->d_chrom_off); delete d; return rc; }
+  if (((uintptr_t)d_counts & 15) || ((uintptr_t)d_pos & 15)) {
+    hipFree(d->d_chrom_off); delete d;
+    return set_err(ctx, SFS2D_E_ARG, "device arrays must be 16-byte aligned (and readable to round_up(n, 4))");
+  }
   d->counts = const_cast<uint32_t*>(d_counts);
   d->pos = const_cast<uint32_t*>(d_pos);
   if (d_ann_id) {
@@ -981,12 +1430,19 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
   const int h2w = pl->p16 ? (K.nb2 + 1) / 2 : K.nb2;
   const int per = h2w + (K.n1p + 1) + (K.n2p + 1);
   const int ng = BLOCK / pl->G;
-  pl->scan_lds = (size_t)(ng * per + 2) * 4 + 32 * 8 + 32 * 8;
+  pl->scan_lds = (size_t)(ng * (per + TRASH) + 2) * 4 + 32 * 8 + 32 * 8;
   if (pl->scan_lds > 160 * 1024) {
     delete pl;
     return set_err(ctx, SFS2D_E_ARG, "2D grid too large for LDS with 32-bit bins (windows of >= 65536 SNPs)");
   }
-  const uint32_t CH = (uint32_t)(pl->G == 64 ? 8 : 2);   // slots per chunk (per workgroup)
+  // slots per workgroup: enough workgroups to fill 256 CUs several times, then longer chunks
+  uint32_t CH;
+  if (pl->G == 64) {
+    const int64_t per_wave = (pl->nslots + 4 * 1024 - 1) / (4 * 1024);
+    CH = (uint32_t)(4 * std::max<int64_t>(1, std::min<int64_t>(8, per_wave)));
+  } else {
+    CH = 2;
+  }
   for (int c = 0; c < nc; ++c) {
     for (unsigned long long s = slot_base[c]; s < slot_base[c + 1]; s += CH) {
       Chunk ch{};
@@ -996,16 +1452,13 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
       pl->chunks.push_back(ch);
     }
   }
-  if (pl->extra_rec >= 0) {
-    Chunk ch{};
-    ch.chrom = last_c; ch.kind = 1;
-    pl->chunks.push_back(ch);
-  }
+  pl->last_chrom = last_c;
 
   // background / segmentation tiles (never crossing a chromosome)
   if (pl->do_bg || pl->do_seg) {
     const int64_t n = data->n;
-    int64_t T = std::max<int64_t>(1024, std::min<int64_t>(65536, (n / 2048 + 255) / 256 * 256));
+    // ~1000+ tiles for big inputs (several workgroups per CU), >= 4096 SNPs each (flush amortised)
+    int64_t T = std::max<int64_t>(4096, std::min<int64_t>(65536, (n / 768 + 4095) / 4096 * 4096));
     for (int c = 0; c < nc; ++c)
       for (int64_t s = data->chrom_off[c]; s < data->chrom_off[c + 1]; s += T) {
         Tile t{};
@@ -1038,7 +1491,7 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
   rc = rc ? rc : dalloc(ctx, &pl->d_leaves, leaves.size());
   rc = rc ? rc : dalloc(ctx, &pl->d_prog, prog.size());
   rc = rc ? rc : dalloc(ctx, &pl->d_out, (size_t)pl->nrec);
-  rc = rc ? rc : dalloc(ctx, &pl->d_err, 1);
+  rc = rc ? rc : dalloc(ctx, &pl->d_err, 4);
   if (rc) { plan_free(pl); delete pl; return rc; }
   hipError_t e = hipSuccess;
 #define PCPY(dst, v) if (e == hipSuccess && !(v).empty()) e = hipMemcpyAsync(dst, (v).data(), sizeof((v)[0]) * (v).size(), hipMemcpyHostToDevice, st)
@@ -1050,7 +1503,7 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
 #undef PCPY
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_slots, 0, sizeof(uint2) * ((size_t)pl->nslots + 1), st);
   if (e == hipSuccess && pl->do_bg) e = hipMemsetAsync(pl->d_repl, 0, sizeof(uint32_t) * (size_t)REPL * nc * K.nh, st);
-  if (e == hipSuccess) e = hipMemsetAsync(pl->d_err, 0, sizeof(uint32_t), st);
+  if (e == hipSuccess) e = hipMemsetAsync(pl->d_err, 0, 4 * sizeof(uint32_t), st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_out, 0, sizeof(sfs2d_window) * (size_t)pl->nrec, st);
   for (auto& ev : pl->ev) if (e == hipSuccess) e = hipEventCreate(&ev);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
@@ -1062,11 +1515,17 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
     if (pl->do_bg && pl->do_seg) hipFuncSetAttribute((const void*)k_bg_seg<true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->bg_lds);
     if (pl->do_bg) hipFuncSetAttribute((const void*)k_bg_seg<true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->bg_lds);
   }
+  hipFuncSetAttribute((const void*)k_bg_finalize, hipFuncAttributeMaxDynamicSharedMemorySize,
+                      (int)(sizeof(double) * FIN_LDS_BINS));
   if (pl->scan_lds > 64 * 1024) {
     hipFuncSetAttribute((const void*)k_scan<64, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
     hipFuncSetAttribute((const void*)k_scan<64, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
     hipFuncSetAttribute((const void*)k_scan<256, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
     hipFuncSetAttribute((const void*)k_scan<256, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
+    hipFuncSetAttribute((const void*)k_scan_extra<64, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
+    hipFuncSetAttribute((const void*)k_scan_extra<64, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
+    hipFuncSetAttribute((const void*)k_scan_extra<256, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
+    hipFuncSetAttribute((const void*)k_scan_extra<256, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
   }
   pl->bg_ready = false;
   *out = pl;
@@ -1176,6 +1635,25 @@ int sfs2d_plan_check(sfs2d_plan* pl) {
     if (e & ERR_KEY) return set_err(ctx, SFS2D_E_KEY, "allele count above 2*pop_size (reference: KeyError in calculate_1d_sfs)");
     return set_err(ctx, SFS2D_E_GRID, "folded 2D bin outside the (2n1+1)x(2n2+1) grid");
   }
+  return 0;
+}
+
+// diagnostic: stamps of a -DSFS2D_STAMPS build (returns SFS2D_E_ARG in the shipped build)
+int sfs2d__debug_stamps(unsigned long long* out64) {
+#ifdef SFS2D_STAMPS
+  if (hipMemcpyFromSymbol(out64, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 64) != hipSuccess) return SFS2D_E_HIP;
+  return 0;
+#else
+  (void)out64;
+  return SFS2D_E_ARG;
+#endif
+}
+
+int sfs2d_plan_stats(sfs2d_plan* pl, uint32_t* exact_windows) {
+  if (!pl || !exact_windows) return SFS2D_E_ARG;
+  sfs2d_ctx* ctx = pl->ctx;
+  HIPCHK(ctx, hipMemcpyAsync(exact_windows, pl->d_err + 1, 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return 0;
 }
 

@@ -178,6 +178,11 @@ class Plan:
         self.eng.check(self.eng.lib.sfs2d_plan_time(self.h, iters, *[C.byref(x) for x in v]))
         return tuple(x.value for x in v)
 
+    def stats(self) -> int:
+        v = C.c_uint32()
+        self.eng.check(self.eng.lib.sfs2d_plan_stats(self.h, C.byref(v)))
+        return int(v.value)
+
     def set_timing(self, max_runs: int):
         self.eng.check(self.eng.lib.sfs2d_plan_set_timing(self.h, int(max_runs)))
 

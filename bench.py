@@ -172,7 +172,8 @@ def main():
                                    "n1=n2=50 haploid (pop_size 25/25), per-chromosome background",
                        "snps_per_gpu": p.n, "windows_per_gpu": nwin_rank, "window_bp": WS,
                        "parallelism": f"windows sharded by chromosome over {world} GPU(s); RCCL all-gather"},
-            "kernels_ms": {"k1_bg_seg": k1, "k2_bg_finalize": k2, "k3_scan": k3, "timed_runs": nr},
+            "kernels_ms": {"k1_bg_seg": k1, "k2_bg_finalize": k2, "k3_scan": k3, "timed_runs": nr,
+                           "exact_path_windows": pl.stats()},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "note": "k_scan, algorithmic bytes 4 B/SNP + 72 B/slot; 8 MB input is MALL-resident"},

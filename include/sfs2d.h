@@ -133,6 +133,8 @@ int sfs2d_plan_read(sfs2d_plan* plan, sfs2d_window* out_host, int64_t cap, int64
  * multi-GPU all-reduce between sfs2d_plan_run_phase(plan, 1) and (plan, 2). */
 int sfs2d_plan_bg_buffer(sfs2d_plan* plan, void** dev_ptr, int64_t* nbytes);
 int sfs2d_plan_run_phase(sfs2d_plan* plan, int phase, sfs2d_window* out_dev);
+/* cumulative number of windows re-evaluated on the exact path (|T| ~ 0: proportionality test) */
+int sfs2d_plan_stats(sfs2d_plan* plan, uint32_t* exact_windows);
 /* last run's error word (0 = ok, else SFS2D_E_KEY / SFS2D_E_GRID); synchronises */
 int sfs2d_plan_check(sfs2d_plan* plan);
 /* live timing: record HIP events around each kernel of the next `max_runs` sfs2d_plan_run calls

@@ -102,8 +102,8 @@ def _records_vs_oracle(p, cfg_scan, ocfg, wins, bg_of, guards=True):
     ref = O.window_records(p, wins, ocfg, bg_of, guards)
     assert len(body) == len(ref)
     for r, o in zip(body, ref):
-        for f in ("snp_count", "n2", "n2_all", "n1a", "n1b"):
-            assert int(r[f]) == o[f], (f, int(r[f]), o[f])
+        for f, g in (("snp_count", "snp_count"), ("n2", "N2"), ("n2_all", "N2_all"), ("n1a", "N1a"), ("n1b", "N1b")):
+            assert int(r[f]) == o[g], (f, int(r[f]), o[g])
         for f, g in (("t2d", "T2D"), ("t1d_p1", "T1D_p1"), ("t1d_p2", "T1D_p2")):
             if o[g] is not None:
                 assert gu.close(float(r[f]), o[g]), (f, float(r[f]), o[g])

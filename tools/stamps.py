@@ -1,0 +1,31 @@
+#!/usr/bin/env python3
+"""Diagnostic: per-phase wall-clock stamps of block 0 of each kernel (needs libsfs2d_stamps.so,
+built with -DSFS2D_STAMPS).  usage: SFS2D_LIB=.../libsfs2d_stamps.so python tools/stamps.py config2"""
+import ctypes as C
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "2dsfs-scan_amd"))
+from sfs2d import _lib as L  # noqa: E402
+from sfs2d.engine import Engine, ScanConfig  # noqa: E402
+from sfs2d.synth import synth_genome  # noqa: E402
+
+which = sys.argv[1] if len(sys.argv) > 1 else "config2"
+p = synth_genome(1 if which == "config2" else 32, 1_000_000 if which == "config2" else 1_562_500, 25, 25, seed=1)
+eng = Engine.get(0)
+dev = eng.upload(p)
+pl = eng.plan(dev, ScanConfig(n1p=25, n2p=25, window=20000))
+for _ in range(3):
+    pl.run()
+pl.check()
+buf = (C.c_ulonglong * 64)()
+assert L.lib().sfs2d__debug_stamps(buf) == 0
+t = list(buf)
+def d(a, b):
+    return (t[b] - t[a]) * 0.01 if t[a] and t[b] else float("nan")
+print(which, "K1 blk0: zero %.2f  loop %.2f  flush %.2f us" % (d(20, 21), d(21, 22), d(22, 23)))
+print(which, "K2 blk0: repl %.2f  Bsum %.2f  p/lp %.2f  leaves %.2f  tail %.2f us" % (d(0, 1), d(1, 2), d(2, 3), d(3, 4), d(4, 5)))
+print(which, "K3 blk0: prologue %.2f  phaseA(1st) %.2f  take2D %.2f  1D+reduce+store %.2f  rest %.2f us" % (
+    d(10, 11), d(11, 12), d(12, 13), d(13, 14), d(14, 15)))
+print(which, "gaps: K1end->K2start %.2f  K2end->K3start %.2f us" % (d(23, 0), d(5, 10)))
