@@ -1,0 +1,1192 @@
+// sfs2d_kernels.hpp -- gfx950 (MI355X) device code of the windowed 2D-SFS composite-likelihood scan.
+//
+// Reference path (uricchio/2DSFS-scan, scripts/src/twoDSFS_class.py): per genomic window,
+// calculate_2d_sfs (140-232) + fold_1d_sfs(calculate_1d_sfs) (398-463) and the multinomial
+// log-likelihood ratios calculate_likelihood_2D (625-684) / _1D (478-537) against a background SFS.
+// The reference builds dense dict grids per window and calls scipy.stats.multinomial.logpmf twice.
+// Here the statistic is evaluated in its sparse closed form over the bins the window touches:
+//
+//   T = 2 * ( sum_{k: x_k>0} x_k * (ln x_k - lp_k)  -  N ln N ),   lp_k = ln(b_k / B)
+//
+// (the gammaln terms of the two logpmf calls cancel), keeping the reference's value semantics:
+// T = 0.0 exactly when x_k/N == b_k/B bitwise on every touched bin (both logpmf calls then see
+// identical proportions), +inf when a touched bin has b_k == 0 (xlogy(x, 0) = -inf), NaN when
+// scipy's p[-1] <- 1 - sum(p[:-1]) replacement makes the background's last inner proportion
+// negative (emulated with numpy's pairwise summation order), and the None conditions (N == 0 or
+// B == 0) reported through counts / flags.
+//
+// For the 2D spectrum the fast path sums per SNP instead of per bin: with r_i the number of
+// earlier SNPs of the window in SNP i's bin (returned by the LDS histogram atomic itself),
+//   sum_k x_k ln x_k = sum_i D(r_i),  D(r) = (r+1) ln(r+1) - r ln r     (telescoping)
+//   sum_k x_k lp_k   = sum_i lp_{k(i)}
+// so each SNP adds D(r_i) - lp_{k(i)} with no second pass over the histogram.
+//
+//   k_prep        one pass over SNP tiles (counts + positions, 8 B/SNP): filters and the joint fold
+//                 applied once, per-SNP packed bins written (4 B/SNP), per-chromosome background
+//                 histograms (LDS-privatised, flushed into REPL replicas) and inner 2D sums,
+//                 fixed-bp segmentation of the window slots.
+//   k_bg_slice    per-chromosome background tables, many workgroups per background: each slice of
+//                 2D bins sums its replicas, writes proportions / logs and its numpy pairwise leaves;
+//                 one block per background folds the 1D spectra; the last block to finish combines
+//                 the leaves (numpy's tree) and applies scipy's p[-1] rule.
+//   k_bg_finalize one workgroup per supplied background (set once per plan, float or integer).
+//   k_scan_w      the hot loop (small grids): one wavefront per window, 8 per workgroup sharing the
+//                 background's log-proportion table and the D / x ln x tables in LDS; bins streamed
+//                 with 16-B loads; one fp64 DPP reduction per spectrum; one 64-B record per window.
+//   k_scan_g      large grids: one workgroup per window (exact evaluation).
+//   k_scan_extra  combined_scan's final-window helper (quirk Q9).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "sfs2d.h"
+
+namespace sfs2dk {
+
+constexpr int WAVE = 64;
+constexpr int BLOCK = 256;        // k_scan_g / k_scan_extra workgroup
+constexpr int SBLOCK = 512;       // k_scan_w workgroup (8 wavefronts, one window each)
+constexpr int BLOCK1 = 512;       // k_prep workgroup
+constexpr int FBLOCK = 1024;      // k_bg_finalize workgroup
+constexpr int KBLOCK = 512;       // k_bg_slice workgroup
+constexpr int LNX_N = 1 << 20;    // ln(k) table for k < LNX_N (bin counts / window totals)
+constexpr int LNT = 512;          // D(r) and x ln x tables staged in LDS by k_scan_w
+constexpr int REPL = 8;           // replicas of the per-chromosome background histograms
+constexpr int PW_MAX_LEAVES = 256;
+constexpr int LEAVES_PER_SLICE = 4;
+constexpr int FIN_LDS_BINS = 12288;  // backgrounds with nt <= this keep values / proportions in LDS
+constexpr int TRASH = WAVE;       // lane-private scratch words after each wave's histograms
+constexpr int R1 = 4;             // replicas of the folded 1D window histograms (lane & 3)
+
+enum : uint32_t { ERR_KEY = 1u, ERR_GRID = 2u };
+enum : uint32_t {
+  BGF_B2_ZERO = 1u, BGF_B1A_ZERO = 2u, BGF_B1B_ZERO = 4u, BGF_NAN2 = 8u, BGF_NAN1A = 16u, BGF_NAN1B = 32u,
+  BGF_FLOATV = 64u
+};
+
+// per-SNP packed bins written by k_prep:
+//   bits 0-15  inner 2D bin k = x1*(n2+1)+x2 after the fold (0 = none: (0,0) is never counted)
+//   bits 16-22 folded inner 1D bin of pop1 (1..pop_size-1; 0 = none)
+//   bits 23-29 folded inner 1D bin of pop2
+//   bit  30    annotation matches variant_type (count_snps)
+//   bit  31    counted in the 2D SFS in its last bin (n1, n2), which bins[1:-1] excludes
+constexpr uint32_t B_VAR = 1u << 30, B_LAST = 1u << 31;
+
+struct KParams {
+  int n1p, n2p, n1, n2;  // diploid sizes and haploid sample sizes
+  int nb2;               // (n1+1)*(n2+1) 2D bins
+  int nh;                // background histogram words per chromosome: nb2 + (n1+1) + (n2+1)
+  int h1a, h1b;          // offsets of the unfolded 1D histograms inside a background histogram
+  int nt;                // table entries per background: nb2 + (n1p+1) + (n2p+1)
+  int t1a, t1b;          // offsets of the folded 1D tables
+  int fold;
+  int ann_want;          // -1: no variant_type filter
+  int has_start, has_end;
+  long long start_pos, end_pos;
+  unsigned int ws;       // bp window size (fixed-bp) or SNPs per window
+  unsigned int wmag;     // (p-1)/ws as a multiply-high: q = (t + ((n - t) >> wsh1)) >> wsh2, t = mulhi(n, wmag)
+  int wsh1, wsh2;
+  int nchrom;
+};
+
+struct Tile {   // k_prep work item: SNPs [begin, end) of chromosome chrom = [cb, ce), slots from sbase
+  uint32_t chrom, begin, end, cb, ce, sbase, pad0, pad1;
+};
+
+struct Chunk {  // k_scan work item: window slots [slot_lo, slot_hi) of one chromosome
+  uint32_t chrom, slot_lo, slot_hi, wid_lo, cb, pad0, pad1, pad2;
+};
+
+struct PL {     // per-bin background table entry
+  double lp;    // log of the proportion scipy uses (p[-1] adjusted on the last inner bin)
+  double v;     // integer backgrounds: the count b_k; normalised (float) backgrounds: p_k = b_k / B
+};
+
+struct BgHead {
+  double B2, B1a, B1b;
+  uint32_t flags, pad;
+};
+
+struct Bg1D {   // k_bg_slice: the 1D block's results for the tail
+  double B1a, B1b;
+  uint32_t flags, pad;
+};
+
+struct WinOut {
+  uint32_t snp_count, n2, n2_all, n1a, n1b;
+  double t2d, t1a, t1b;
+};
+
+static_assert(sizeof(sfs2d_window) == 64, "window record must be 64 bytes");
+static_assert(sizeof(Tile) == 32 && sizeof(Chunk) == 32, "work items are 32 bytes");
+
+// Diagnostic build only (-DSFS2D_STAMPS): wall-clock stamps (s_memrealtime, 100 MHz) of block 0 at
+// phase boundaries, read back with sfs2d__debug_stamps.  The shipped library executes none.
+#ifdef SFS2D_STAMPS
+__device__ unsigned long long g_stamps[64];
+#define STAMP(i)                                                                                 \
+  do {                                                                                           \
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[i] = __builtin_amdgcn_s_memrealtime();     \
+  } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
+
+// ------------------------------------------------------------------------------------------ helpers
+
+__device__ __forceinline__ uint32_t wid_of(uint32_t p, uint32_t ws) { return p ? (p - 1u) / ws : 0u; }
+
+// the same window id with the division replaced by a multiply-high (host-side magic numbers)
+__device__ __forceinline__ uint32_t wid_fast(const KParams& P, uint32_t p) {
+  const uint32_t n = p - 1u;
+  const uint32_t t = __umulhi(n, P.wmag);
+  return p ? (t + ((n - t) >> P.wsh1)) >> P.wsh2 : 0u;
+}
+
+__device__ __forceinline__ double lnx_of(const double* lnx, uint32_t x) {
+  return x < (uint32_t)LNX_N ? lnx[x] : log((double)x);
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+  return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+  return v;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+  return v;
+}
+
+// fp64 wave sum on the DPP path (xor-1 and xor-2 quad permutes, row half-mirror, row mirror: every
+// lane then holds its 16-lane row's sum) and four readlanes; the result is wave-uniform and its
+// rounding order is fixed (deterministic).  All 64 lanes must be active.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(u & 0xffffffffull), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double((long long)(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const unsigned long long u = __double_as_longlong(v);
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(u & 0xffffffffull), l);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(u >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_d<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_d<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_d<0x141>(v);   // row_half_mirror
+  v += dpp_d<0x140>(v);   // row_mirror
+  return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+}
+
+// the same for u32 (per-lane packed 16-bit counters: the fields do not carry into each other as
+// long as every field's total stays below 65536)
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
+
+__device__ __forceinline__ uint32_t wave_sum_dpp_u(uint32_t v) {
+  v += dpp_u<0xB1>(v);
+  v += dpp_u<0x4E>(v);
+  v += dpp_u<0x141>(v);
+  v += dpp_u<0x140>(v);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+
+// x_k / N == b_k / B bitwise.  Integer backgrounds: exact cross-multiplication (all products
+// < 2^53, and for x*B < 2^52 distinct rationals cannot round to the same double); normalised
+// backgrounds: the reference's own division.
+__device__ __forceinline__ bool prop_ok(uint32_t x, double N, double v, double B, bool floatv) {
+  return floatv ? ((double)x / N == v) : ((double)x * B == v * N);
+}
+
+__device__ __forceinline__ uint4 ld4(const uint32_t* __restrict__ a, uint32_t i, uint32_t e) {
+  return i < e ? *reinterpret_cast<const uint4*>(a + i) : make_uint4(0, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t bg_zero_flags(const BgHead& hb) {
+  return ((hb.flags & BGF_B2_ZERO) ? SFS2D_W_BG2_ZERO : 0u) | ((hb.flags & BGF_B1A_ZERO) ? SFS2D_W_BG1A_ZERO : 0u) |
+         ((hb.flags & BGF_B1B_ZERO) ? SFS2D_W_BG1B_ZERO : 0u);
+}
+
+__device__ __forceinline__ void write_rec(sfs2d_window* o, uint32_t chrom, uint32_t wid, uint32_t b, uint32_t e,
+                                          const WinOut& w, uint32_t flags) {
+  sfs2d_window r;
+  r.chrom = chrom; r.wid = wid; r.begin = b; r.end = e;
+  r.snp_count = w.snp_count; r.n2 = w.n2; r.n2_all = w.n2_all; r.n1a = w.n1a; r.n1b = w.n1b;
+  r.flags = flags;
+  r.t2d = w.t2d; r.t1d_p1 = w.t1a; r.t1d_p2 = w.t1b;
+  *o = r;
+}
+
+__device__ __forceinline__ void write_empty(sfs2d_window* o, uint32_t chrom, uint32_t wid) {
+  sfs2d_window r;
+  memset(&r, 0, sizeof(r));
+  r.chrom = chrom; r.wid = wid; r.flags = SFS2D_W_EMPTY;
+  *o = r;
+}
+
+// One SNP: filters (position: twoDSFS_class.py:179-182; variant_type: 185-187), the joint fold on
+// individual counts (197-206; ties not folded), the (0,0) skip (212-213), raw 1D alt counts
+// (428-433) and their fold against 2*pop_size (446-463), restricted to the inner bins that
+// bins[1:-1] keeps (486-488, 635).  Returns the packed bins word (see B_VAR / B_LAST).
+// k2all / u1a / u1b: the unfolded background histogram words to count (-1: none).
+__device__ __forceinline__ uint32_t classify(const KParams& P, uint32_t c, bool var_ok, bool pos_ok, uint32_t& err,
+                                            int& k2all, int& u1a, int& u1b) {
+  const int r1 = c & 0xff, a1 = (c >> 8) & 0xff, r2 = (c >> 16) & 0xff, a2 = c >> 24;
+  const bool pass = var_ok & pos_ok;
+  const bool sw = P.fold & (a1 + a2 > P.n1p + P.n2p);
+  const int x1 = sw ? r1 : a1, x2 = sw ? r2 : a2;
+  const bool nz = (x1 | x2) != 0;
+  const bool oob = (x1 > P.n1) | (x2 > P.n2);
+  const bool ka = a1 > P.n1, kb = a2 > P.n2;
+  err |= (pass & nz & oob) ? ERR_GRID : 0u;           // out-of-grid key: unsupported (documented)
+  err |= (pass & (ka | kb)) ? ERR_KEY : 0u;            // reference: KeyError in calculate_1d_sfs
+  const int k2 = x1 * (P.n2 + 1) + x2;
+  const bool in2 = pass & nz & !oob;
+  const bool last = in2 & (k2 == P.nb2 - 1);
+  const int g1 = min(a1, P.n1 - a1), g2 = min(a2, P.n2 - a2);
+  const bool v1a = pass & (a1 != 0) & !ka & (g1 >= 1) & (g1 <= P.n1p - 1);
+  const bool v1b = pass & (a2 != 0) & !kb & (g2 >= 1) & (g2 <= P.n2p - 1);
+  k2all = in2 ? k2 : -1;
+  u1a = (pass & (a1 != 0) & !ka) ? a1 : -1;
+  u1b = (pass & (a2 != 0) & !kb) ? a2 : -1;
+  return (uint32_t)((in2 & !last) ? k2 : 0) | ((uint32_t)(v1a ? g1 : 0) << 16) | ((uint32_t)(v1b ? g2 : 0) << 23) |
+         (var_ok ? B_VAR : 0u) | (last ? B_LAST : 0u);
+}
+
+__device__ __forceinline__ uint32_t bin_k2(uint32_t w) { return w & 0xffffu; }
+__device__ __forceinline__ uint32_t bin_g1(uint32_t w) { return (w >> 16) & 0x7fu; }
+__device__ __forceinline__ uint32_t bin_g2(uint32_t w) { return (w >> 23) & 0x7fu; }
+
+// ------------------------------------------------------------------------------------------ K0
+
+// ln k for k < LNX_N; F(x) = x ln x for x < LNT; D(r) = F(r+1) - F(r) for r < LNT-1 and
+// D(LNT-1) = 0 (k_scan_w adds the ranks from LNT-1 on per bin, as F(x) - F(LNT-1))
+__global__ void k_init_lnx(double* lnx, double* dtab, double* ftab) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < LNX_N) lnx[i] = i ? log((double)i) : 0.0;
+  if (i < LNT) {
+    const double a = i ? (double)i * log((double)i) : 0.0;
+    const double b = (double)(i + 1) * log((double)(i + 1));
+    dtab[i] = i < LNT - 1 ? b - a : 0.0;
+    ftab[i] = a;
+  }
+}
+
+// ------------------------------------------------------------------------------------------ K1
+
+template <bool DO_BG, bool DO_SEG, bool LDS_HIST, bool DO_BINS>
+__global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __restrict__ counts,
+                                                 const uint32_t* __restrict__ pos, const uint16_t* __restrict__ ann,
+                                                 const Tile* __restrict__ tiles, uint32_t* __restrict__ repl,
+                                                 uint2* __restrict__ slots, uint32_t* __restrict__ bins,
+                                                 uint32_t* __restrict__ bcount, uint32_t* __restrict__ err_word) {
+  extern __shared__ uint32_t sh_hist[];
+  __shared__ uint32_t sh_b2;
+  STAMP(20);
+  const Tile t = tiles[blockIdx.x];
+  uint32_t* gh = repl + ((size_t)(blockIdx.x % REPL) * P.nchrom + t.chrom) * (size_t)P.nh;
+  uint32_t* H = LDS_HIST ? sh_hist : gh;
+  if (DO_BG) {
+    if (LDS_HIST)
+      for (int k = threadIdx.x; k < P.nh; k += BLOCK1) sh_hist[k] = 0u;
+    if (threadIdx.x == 0) sh_b2 = 0u;
+    __syncthreads();
+  }
+  const bool pos_filter = P.has_start || P.has_end;
+  const bool need_pos = DO_SEG || pos_filter;
+  const bool filt = P.ann_want >= 0;
+  const int lane = threadIdx.x & (WAVE - 1);
+  uint32_t err = 0, b2 = 0;
+  STAMP(21);
+
+  // one 16-B vector = 4 consecutive SNPs; elements outside [t.begin, t.end) are masked.
+  // wprev / wnext: window ids of the SNPs just before / after the vector.
+  auto process = [&](uint32_t i0, const uint4& cv, const uint4& pv, const uint2& av, uint32_t wprev, uint32_t wnext) {
+    const uint32_t cc[4] = {cv.x, cv.y, cv.z, cv.w};
+    const uint32_t pp[4] = {pv.x, pv.y, pv.z, pv.w};
+    const uint32_t aa[4] = {av.x & 0xffffu, av.x >> 16, av.y & 0xffffu, av.y >> 16};
+    uint32_t w[4];
+    if (DO_SEG) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w[k] = wid_fast(P, pp[k]);
+    }
+    uint32_t bw[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t i = i0 + k;
+      const bool in = (i >= t.begin) & (i < t.end);
+      bool var_ok = in, pos_ok = true;
+      if (filt) var_ok = in & ((int)aa[k] == P.ann_want);
+      if (pos_filter) {
+        const long long p = (long long)pp[k];
+        pos_ok = (!P.has_start | (p >= P.start_pos)) & (!P.has_end | (p <= P.end_pos));
+      }
+      int k2all, u1a, u1b;
+      bw[k] = classify(P, cc[k], var_ok, pos_ok, err, k2all, u1a, u1b);
+      if (DO_BG && in) {
+        if (k2all >= 0) atomicAdd(&H[k2all], 1u);
+        if (u1a >= 0) atomicAdd(&H[P.h1a + u1a], 1u);
+        if (u1b >= 0) atomicAdd(&H[P.h1b + u1b], 1u);
+        b2 += bin_k2(bw[k]) ? 1u : 0u;
+      }
+      if (DO_SEG && in) {
+        // window id (pos-1)//ws: the reference's start += ws*((pos-start)//ws) from start=1 (:894, :948)
+        const uint32_t qp = k ? w[k - 1] : wprev;
+        const uint32_t qn = k < 3 ? w[k + 1] : wnext;
+        const bool first = (i == t.cb) || (qp != w[k]);
+        const bool last = (i + 1 == t.ce) || (qn != w[k]);
+        const size_t s = (size_t)t.sbase + w[k];
+        if (first) slots[s].x = i + 1u;  // 0 = unset; the scan kernel clears what it consumed
+        if (last) slots[s].y = i + 1u;
+      }
+    }
+    if (DO_BINS) {
+      if (i0 >= t.begin && i0 + 4 <= t.end) {
+        *reinterpret_cast<uint4*>(bins + i0) = make_uint4(bw[0], bw[1], bw[2], bw[3]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (i0 + k >= t.begin && i0 + k < t.end) bins[i0 + k] = bw[k];
+      }
+    }
+  };
+
+  // two vectors per thread in flight per step (8 SNPs, 32 B of counts + positions); the lanes at
+  // the wave edges fetch their neighbour positions in the same batch
+  constexpr uint32_t STEP = 8 * BLOCK1;
+  const uint32_t ab = t.begin & ~3u;
+  for (uint32_t base = ab; base < t.end; base += STEP) {
+    const uint32_t ia = base + 4 * threadIdx.x, ib = ia + 4 * BLOCK1;
+    const bool la = ia < t.end, lb = ib < t.end;
+    const uint4 ca = la ? *reinterpret_cast<const uint4*>(counts + ia) : make_uint4(0, 0, 0, 0);
+    const uint4 cbv = lb ? *reinterpret_cast<const uint4*>(counts + ib) : make_uint4(0, 0, 0, 0);
+    const uint4 pa = (need_pos && la) ? *reinterpret_cast<const uint4*>(pos + ia) : make_uint4(0, 0, 0, 0);
+    const uint4 pb = (need_pos && lb) ? *reinterpret_cast<const uint4*>(pos + ib) : make_uint4(0, 0, 0, 0);
+    const uint2 aav = (filt && la) ? *reinterpret_cast<const uint2*>(ann + ia) : make_uint2(0, 0);
+    const uint2 abv = (filt && lb) ? *reinterpret_cast<const uint2*>(ann + ib) : make_uint2(0, 0);
+    uint32_t wpa = 0, wna = 0, wpb = 0, wnb = 0;
+    if (DO_SEG) {
+      // neighbour positions at the wave edges and past the tile end, loaded with the vectors
+      uint32_t xa_prev = 0, xa_next = 0, xb_prev = 0, xb_next = 0;
+      if (lane == 0 && ia > 0) xa_prev = pos[ia - 1];
+      if ((lane == WAVE - 1 || ia + 4 >= t.end) && ia + 4 < t.ce) xa_next = pos[ia + 4];
+      if (lane == 0 && ib > 0) xb_prev = pos[ib - 1];
+      if ((lane == WAVE - 1 || ib + 4 >= t.end) && ib + 4 < t.ce) xb_next = pos[ib + 4];
+      wpa = __shfl_up(wid_fast(P, pa.w), 1, WAVE);
+      wna = __shfl_down(wid_fast(P, pa.x), 1, WAVE);
+      wpb = __shfl_up(wid_fast(P, pb.w), 1, WAVE);
+      wnb = __shfl_down(wid_fast(P, pb.x), 1, WAVE);
+      if (lane == 0) { wpa = wid_fast(P, xa_prev); wpb = wid_fast(P, xb_prev); }
+      if (lane == WAVE - 1 || ia + 4 >= t.end) wna = wid_fast(P, xa_next);
+      if (lane == WAVE - 1 || ib + 4 >= t.end) wnb = wid_fast(P, xb_next);
+    }
+    process(ia, ca, pa, aav, wpa, wna);
+    process(ib, cbv, pb, abv, wpb, wnb);
+  }
+  STAMP(22);
+  if (err) atomicOr(err_word, err);
+  if (DO_BG) {
+    b2 = wave_sum_u(b2);
+    if (lane == 0 && b2) atomicAdd(&sh_b2, b2);
+    __syncthreads();
+    if (LDS_HIST)
+      for (int k = threadIdx.x; k < P.nh; k += BLOCK1) {
+        const uint32_t v = sh_hist[k];
+        if (v) atomicAdd(&gh[k], v);
+      }
+    if (threadIdx.x == 0 && sh_b2) atomicAdd(&bcount[t.chrom], sh_b2);
+  }
+  STAMP(23);
+}
+
+// ------------------------------------------------------------------------------------------ K2
+
+// numpy pairwise_sum leaf (numpy/_core/src/umath/loops_utils.h.src): n < 8 sequential from 0.0,
+// n <= 128: eight strided accumulators combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) + tail.
+__device__ double np_leaf_sum(const double* a, int n) {
+  if (n < 8) {
+    double r = 0.0;
+    for (int i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8) {
+    r0 += a[i]; r1 += a[i + 1]; r2 += a[i + 2]; r3 += a[i + 3];
+    r4 += a[i + 4]; r5 += a[i + 5]; r6 += a[i + 6]; r7 += a[i + 7];
+  }
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; i < n; ++i) res += a[i];
+  return res;
+}
+
+// the same leaf with its eight accumulators on eight lanes (r = lane within the group of 8): each
+// accumulator is its own sequential sum, so the result is bitwise np_leaf_sum's
+__device__ __forceinline__ double np_leaf_sum8(const double* a, int n, int r, double* acc8) {
+  if (n >= 8) {
+    double x = a[r];
+    for (int i = 8 + r; i < n - (n % 8); i += 8) x += a[i];
+    acc8[r] = x;
+  }
+  __syncthreads();
+  double res = 0.0;
+  if (r == 0) {
+    if (n < 8) {
+      for (int i = 0; i < n; ++i) res += a[i];
+    } else {
+      res = ((acc8[0] + acc8[1]) + (acc8[2] + acc8[3])) + ((acc8[4] + acc8[5]) + (acc8[6] + acc8[7]));
+      for (int i = n - (n % 8); i < n; ++i) res += a[i];
+    }
+  }
+  return res;
+}
+
+// proportion and log entry of one background bin
+__device__ __forceinline__ double put_bin(PL* T, double* LP, int k, double v, double B, int integer_values) {
+  const double p = (B != 0.0) ? v / B : 0.0;
+  PL e;
+  e.lp = log(p);
+  e.v = integer_values ? v : p;
+  T[k] = e;
+  LP[k] = e.lp;
+  return p;
+}
+
+// scipy multinomial._process_parameters on one spectrum: p[-1] <- 1 - sum(p[:-1]) when
+// |.| > 1e-15; the whole logpmf is NaN when that p is < 0
+__device__ __forceinline__ uint32_t adjust_last(PL* T, double* LP, int klast, double padj, uint32_t nan_flag) {
+  if (padj < -1e-15) return nan_flag;
+  if (fabs(padj) > 1e-15) {
+    T[klast].lp = log(padj);
+    LP[klast] = T[klast].lp;
+  }
+  return 0u;
+}
+
+// Per-run per-chromosome backgrounds (integer counts).  grid = (nslices + 1, nbg): blocks
+// [0, nslices) own 2D bin ranges aligned to numpy's pairwise leaves, block nslices folds the 1D
+// spectra; the last block of a background to finish combines the leaves and writes its head.
+// The replicas, the inner-sum counters and the completion counter are left zeroed.
+// slices[s] = {kb, ke, leaf_lo, leaf_hi}; leaves[j] = {offset into p[1:], n}; nodes: numpy's tree
+// (children ids into [leaves | nodes], ordered children-first).
+__global__ __launch_bounds__(KBLOCK) void k_bg_slice(KParams P, uint32_t* __restrict__ repl,
+                                                     uint32_t* __restrict__ bcount, PL* __restrict__ tab,
+                                                     double* __restrict__ LPg, BgHead* __restrict__ head,
+                                                     double* __restrict__ leafsum, Bg1D* __restrict__ bg1d,
+                                                     uint32_t* __restrict__ done, const int4* __restrict__ slices,
+                                                     int nslices, const int2* __restrict__ leaves, int nleaves,
+                                                     const int2* __restrict__ nodes, int nnodes) {
+  __shared__ double pv[4 * 128 + 8];
+  __shared__ double acc8[KBLOCK];
+  __shared__ uint32_t u1[2 * 256 + 2];
+  __shared__ double red[KBLOCK / WAVE][2];
+  __shared__ int last_blk;
+  const int b = blockIdx.y;
+  const int s = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & (WAVE - 1);
+  const size_t rstride = (size_t)P.nchrom * P.nh;
+  uint32_t* R = repl + (size_t)b * P.nh;
+  PL* T = tab + (size_t)b * P.nt;
+  double* LP = LPg + (size_t)b * P.nt;
+  STAMP(0);
+
+  if (s < nslices) {
+    const int4 sl = slices[s];
+    const double B2 = (double)bcount[b];
+    // replica sums (all REPL loads of a bin in flight), proportions, logs
+    for (int k = sl.x + tid; k < sl.y; k += KBLOCK) {
+      uint32_t x[REPL];
+#pragma unroll
+      for (int r = 0; r < REPL; ++r) x[r] = R[k + r * rstride];
+      uint32_t sum = 0;
+#pragma unroll
+      for (int r = 0; r < REPL; ++r) {
+        sum += x[r];
+        if (x[r]) R[k + r * rstride] = 0u;
+      }
+      pv[k - sl.x] = put_bin(T, LP, k, (double)sum, B2, 1);
+    }
+    __syncthreads();
+    STAMP(1);
+    // numpy pairwise leaves over p[1 : nb2-2] (eight lanes per leaf)
+    const int g = tid >> 3, r = tid & 7;
+    const int j = sl.z + g;
+    if (j < sl.w) {
+      const int2 lf = leaves[j];
+      const double* a = pv + (1 + lf.x - sl.x);
+      if (lf.y >= 8) {
+        double x = a[r];
+        for (int i = 8 + r; i < lf.y - (lf.y % 8); i += 8) x += a[i];
+        acc8[tid] = x;
+      }
+    }
+    __syncthreads();
+    if (j < sl.w && r == 0) {
+      const int2 lf = leaves[j];
+      const double* a = pv + (1 + lf.x - sl.x);
+      const double* q = acc8 + tid;
+      double res = 0.0;
+      if (lf.y < 8) {
+        for (int i = 0; i < lf.y; ++i) res += a[i];
+      } else {
+        res = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+        for (int i = lf.y - (lf.y % 8); i < lf.y; ++i) res += a[i];
+      }
+      leafsum[(size_t)b * nleaves + j] = res;
+    }
+    STAMP(2);
+  } else {
+    // the 1D spectra: replica sums of the unfolded histograms, fold_1d_sfs (:446-463), inner sums
+    const int nu = P.nh - P.nb2;
+    for (int k = tid; k < nu; k += KBLOCK) {
+      uint32_t x[REPL];
+#pragma unroll
+      for (int r = 0; r < REPL; ++r) x[r] = R[P.nb2 + k + r * rstride];
+      uint32_t sum = 0;
+#pragma unroll
+      for (int r = 0; r < REPL; ++r) {
+        sum += x[r];
+        if (x[r]) R[P.nb2 + k + r * rstride] = 0u;
+      }
+      u1[k] = sum;
+    }
+    __syncthreads();
+    // folded[f] = u[f] + u[2n - f] (f < n), folded[n] = u[n]; inner sums over f = 1 .. n-1
+    double fa = 0.0, fb = 0.0, sa = 0.0, sb = 0.0;
+    if (tid <= P.n1p) {
+      fa = (double)u1[tid] + (tid < P.n1p ? (double)u1[P.n1 - tid] : 0.0);
+      if (tid >= 1 && tid <= P.n1p - 1) sa = fa;
+    }
+    if (tid <= P.n2p) {
+      fb = (double)u1[P.n1 + 1 + tid] + (tid < P.n2p ? (double)u1[P.n1 + 1 + P.n2 - tid] : 0.0);
+      if (tid >= 1 && tid <= P.n2p - 1) sb = fb;
+    }
+    sa = wave_sum_d(sa);
+    sb = wave_sum_d(sb);
+    if (lane == 0) { red[tid / WAVE][0] = sa; red[tid / WAVE][1] = sb; }
+    __syncthreads();
+    double B1a = 0.0, B1b = 0.0;
+    for (int w = 0; w < KBLOCK / WAVE; ++w) { B1a += red[w][0]; B1b += red[w][1]; }
+    // proportions; p kept in LDS for the p[:-1] sums
+    if (tid <= P.n1p) pv[tid] = put_bin(T, LP, P.t1a + tid, fa, B1a, 1);
+    if (tid <= P.n2p) pv[256 + tid] = put_bin(T, LP, P.t1b + tid, fb, B1b, 1);
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t flags = 0;
+      const int M1a = P.n1p - 1, M1b = P.n2p - 1;
+      if (B1a == 0.0) flags |= BGF_B1A_ZERO;
+      if (B1b == 0.0) flags |= BGF_B1B_ZERO;
+      if (M1a >= 1 && B1a != 0.0)
+        flags |= adjust_last(T, LP, P.t1a + M1a, 1.0 - np_leaf_sum(pv + 1, M1a - 1), BGF_NAN1A);
+      if (M1b >= 1 && B1b != 0.0)
+        flags |= adjust_last(T, LP, P.t1b + M1b, 1.0 - np_leaf_sum(pv + 256 + 1, M1b - 1), BGF_NAN1B);
+      Bg1D o;
+      o.B1a = B1a; o.B1b = B1b; o.flags = flags; o.pad = 0;
+      bg1d[b] = o;
+    }
+  }
+
+  // completion: the last block of this background combines (threadfence-reduction pattern)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (tid == 0) last_blk = atomicAdd(&done[b], 1u) == (uint32_t)nslices;
+  __syncthreads();
+  if (!last_blk) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  STAMP(3);
+  if (tid == 0) {
+    const double B2 = (double)bcount[b];
+    const Bg1D o = bg1d[b];
+    uint32_t flags = o.flags;
+    if (B2 == 0.0) flags |= BGF_B2_ZERO;
+    const int M2 = P.nb2 - 2;
+    if (M2 >= 1 && B2 != 0.0) {
+      double* node = acc8;   // leaves then internal nodes (<= 2 * PW_MAX_LEAVES entries)
+      for (int j = 0; j < nleaves; ++j) node[j] = leafsum[(size_t)b * nleaves + j];
+      for (int i = 0; i < nnodes; ++i) {
+        const int2 ab = nodes[i];
+        node[nleaves + i] = node[ab.x] + node[ab.y];
+      }
+      const double S = (nleaves + nnodes) ? node[nleaves + nnodes - 1] : 0.0;
+      flags |= adjust_last(T, LP, M2, 1.0 - S, BGF_NAN2);
+    }
+    BgHead h;
+    h.B2 = B2; h.B1a = o.B1a; h.B1b = o.B1b; h.flags = flags; h.pad = 0;
+    head[b] = h;
+    bcount[b] = 0u;
+    done[b] = 0u;
+    STAMP(4);
+  }
+}
+
+// One workgroup per supplied background (sfs2d_plan_set_background; once per plan).  Values v,
+// then the proportions p (overwriting v), live in LDS when nt <= FIN_LDS_BINS.
+__global__ __launch_bounds__(FBLOCK) void k_bg_finalize(KParams P, int integer_values, const double* __restrict__ bgval,
+                                                        double* __restrict__ scratch, PL* __restrict__ tab,
+                                                        double* __restrict__ LPg, BgHead* __restrict__ head,
+                                                        const int2* __restrict__ pw_leaves, int pw_nleaves,
+                                                        const int2* __restrict__ pw_nodes, int pw_nnodes) {
+  extern __shared__ double v_lds[];
+  __shared__ double red[FBLOCK / WAVE];
+  __shared__ double node[2 * PW_MAX_LEAVES];
+  __shared__ double Bs[3];
+  const int tid = threadIdx.x;
+  const int lane = tid & (WAVE - 1);
+  const bool in_lds = P.nt <= FIN_LDS_BINS;
+  double* V = in_lds ? v_lds : scratch;
+  PL* T = tab;
+  double* LP = LPg;
+  const int M2 = P.nb2 - 2, M1a = P.n1p - 1, M1b = P.n2p - 1;
+  double s2 = 0.0;
+  for (int k = tid; k < P.nt; k += FBLOCK) {
+    const double x = bgval[k];
+    V[k] = x;
+    if (k >= 1 && k <= M2) s2 += x;
+  }
+  __syncthreads();
+  // inner sums B over bins[1:-1]: exact for integer values in any order; for normalised (float)
+  // values the reference's builtin sum() is sequential, so one lane adds them in order
+  if (integer_values) {
+    s2 = wave_sum_d(s2);
+    if (lane == 0) red[tid / WAVE] = s2;
+    if (tid < WAVE) {
+      double sa = 0.0, sb = 0.0;
+      for (int k = tid; k < M1a; k += WAVE) sa += V[P.t1a + 1 + k];
+      for (int k = tid; k < M1b; k += WAVE) sb += V[P.t1b + 1 + k];
+      sa = wave_sum_d(sa);
+      sb = wave_sum_d(sb);
+      if (tid == 0) { Bs[1] = sa; Bs[2] = sb; }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double t = 0.0;
+      for (int w = 0; w < FBLOCK / WAVE; ++w) t += red[w];
+      Bs[0] = t;
+    }
+  } else if (tid == 0) {
+    double a = 0.0, sa = 0.0, sb = 0.0;
+    for (int k = 0; k < M2; ++k) a += V[1 + k];
+    for (int k = 0; k < M1a; ++k) sa += V[P.t1a + 1 + k];
+    for (int k = 0; k < M1b; ++k) sb += V[P.t1b + 1 + k];
+    Bs[0] = a; Bs[1] = sa; Bs[2] = sb;
+  }
+  __syncthreads();
+  const double B2 = Bs[0], B1a = Bs[1], B1b = Bs[2];
+  for (int k = tid; k < P.nt; k += FBLOCK) {
+    const double B = k < P.nb2 ? B2 : (k < P.t1b ? B1a : B1b);
+    V[k] = put_bin(T, LP, k, V[k], B, integer_values);
+  }
+  __syncthreads();
+  if (tid < pw_nleaves) {
+    const int2 lf = pw_leaves[tid];
+    node[tid] = np_leaf_sum(V + 1 + lf.x, lf.y);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int i = 0; i < pw_nnodes; ++i) {
+      const int2 ab = pw_nodes[i];
+      node[pw_nleaves + i] = node[ab.x] + node[ab.y];
+    }
+    uint32_t flags = integer_values ? 0u : BGF_FLOATV;
+    if (B2 == 0.0) flags |= BGF_B2_ZERO;
+    if (B1a == 0.0) flags |= BGF_B1A_ZERO;
+    if (B1b == 0.0) flags |= BGF_B1B_ZERO;
+    if (M2 >= 1 && B2 != 0.0) {
+      const int nn = pw_nleaves + pw_nnodes;
+      flags |= adjust_last(T, LP, M2, 1.0 - (nn ? node[nn - 1] : 0.0), BGF_NAN2);
+    }
+    if (M1a >= 1 && B1a != 0.0) flags |= adjust_last(T, LP, P.t1a + M1a, 1.0 - np_leaf_sum(V + P.t1a + 1, M1a - 1), BGF_NAN1A);
+    if (M1b >= 1 && B1b != 0.0) flags |= adjust_last(T, LP, P.t1b + M1b, 1.0 - np_leaf_sum(V + P.t1b + 1, M1b - 1), BGF_NAN1B);
+    BgHead h;
+    h.B2 = B2; h.B1a = B1a; h.B1b = B1b; h.flags = flags; h.pad = 0;
+    head[0] = h;
+  }
+}
+
+// ------------------------------------------------------------------------------------------ K3
+
+template <int G>
+__device__ __forceinline__ void group_sync() {
+  if (G == WAVE) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  } else {
+    __syncthreads();
+  }
+}
+
+// group-wide sums; G > WAVE uses a small LDS scratch (G/64 waves x 8 slots)
+template <int G>
+__device__ __forceinline__ double group_sum_d(double v, double* red, int slot) {
+  v = wave_sum_d(v);
+  if (G == WAVE) return v;
+  const int w = threadIdx.x / WAVE;
+  if ((threadIdx.x & (WAVE - 1)) == 0) red[w * 8 + slot] = v;
+  __syncthreads();
+  double t = 0.0;
+  for (int i = 0; i < G / WAVE; ++i) t += red[i * 8 + slot];
+  __syncthreads();
+  return t;
+}
+
+template <int G>
+__device__ __forceinline__ unsigned long long group_sum_u64(unsigned long long v, unsigned long long* red, int slot) {
+  v = wave_sum_u64(v);
+  if (G == WAVE) return v;
+  const int w = threadIdx.x / WAVE;
+  if ((threadIdx.x & (WAVE - 1)) == 0) red[w * 8 + slot] = v;
+  __syncthreads();
+  unsigned long long t = 0;
+  for (int i = 0; i < G / WAVE; ++i) t += red[i * 8 + slot];
+  __syncthreads();
+  return t;
+}
+
+// T from the owner-lane sum: T = 2*(S - N ln N), with the reference's special values
+__device__ __forceinline__ double clr_value(double S, uint32_t N, bool prop, bool nan_bg, const double* lnx) {
+  if (nan_bg) return __builtin_nan("");
+  if (prop) return 0.0;
+  return 2.0 * (S - (double)N * lnx_of(lnx, N));
+}
+
+template <bool P16>
+__device__ __forceinline__ void h2_add(uint32_t* h, uint32_t k) {
+  if (P16) atomicAdd(&h[k >> 1], 1u << ((k & 1) << 4));
+  else atomicAdd(&h[k], 1u);
+}
+
+template <bool P16>
+__device__ __forceinline__ uint32_t h2_take(uint32_t* h, uint32_t k) {  // read-and-clear; one lane gets x
+  if (P16) {
+    const uint32_t sh = (k & 1) << 4;
+    return (atomicAnd(&h[k >> 1], ~(0xffffu << sh)) >> sh) & 0xffffu;
+  }
+  return atomicExch(&h[k], 0u);
+}
+
+// Exact evaluation of one window [b, e) by a group of G lanes: per element take-and-clear with the
+// bin-by-bin proportionality test.  Used for large grids, for windows whose fast-path |T| is ~0
+// (possibly exactly proportional), for windows of >= LNX_N SNPs, and for the Q9 helper.
+// S1: word stride of the 1D histograms (k_scan_w keeps R1 replicas per bin; this uses the first).
+template <int G, bool P16, int S1>
+__device__ __forceinline__ WinOut eval_exact(const KParams& P, const uint32_t* __restrict__ bins, uint32_t b,
+                                             uint32_t e, const PL* __restrict__ T, const BgHead& hb,
+                                             const double* __restrict__ lnx, uint32_t* H2, uint32_t* H1a,
+                                             uint32_t* H1b, double* redd, unsigned long long* redu) {
+  const int lane = threadIdx.x & (G - 1);
+  const bool floatv = hb.flags & BGF_FLOATV;
+  uint32_t c_var = 0, c2 = 0, c_last = 0, c1a = 0, c1b = 0;
+  for (uint32_t i = b + lane; i < e; i += G) {
+    const uint32_t w = bins[i];
+    const uint32_t k2 = bin_k2(w), g1 = bin_g1(w), g2 = bin_g2(w);
+    c_var += (w & B_VAR) ? 1u : 0u;
+    c_last += (w & B_LAST) ? 1u : 0u;
+    if (k2) { ++c2; h2_add<P16>(H2, k2); }
+    if (g1) { ++c1a; atomicAdd(&H1a[g1 * S1], 1u); }
+    if (g2) { ++c1b; atomicAdd(&H1b[g2 * S1], 1u); }
+  }
+  group_sync<G>();
+  const unsigned long long r0 = group_sum_u64<G>((unsigned long long)c2 | ((unsigned long long)c_last << 32), redu, 0);
+  const unsigned long long r1 = group_sum_u64<G>((unsigned long long)c1a | ((unsigned long long)c1b << 32), redu, 1);
+  const unsigned long long r2 = group_sum_u64<G>((unsigned long long)c_var, redu, 2);
+  WinOut o;
+  o.n2 = (uint32_t)r0;
+  o.n2_all = o.n2 + (uint32_t)(r0 >> 32);
+  o.n1a = (uint32_t)r1;
+  o.n1b = (uint32_t)(r1 >> 32);
+  o.snp_count = (uint32_t)r2;
+  const double N2 = (double)o.n2, N1a = (double)o.n1a, N1b = (double)o.n1b;
+  double s2 = 0.0, sa = 0.0, sb = 0.0;
+  bool q2 = true, qa = true, qb = true;   // x_k/N == p_k bitwise on every touched bin
+  for (uint32_t i = b + lane; i < e; i += G) {
+    const uint32_t w = bins[i];
+    const uint32_t k2 = bin_k2(w), g1 = bin_g1(w), g2 = bin_g2(w);
+    if (k2) {
+      const uint32_t x = h2_take<P16>(H2, k2);
+      if (x) {
+        const PL t = T[k2];
+        s2 += (double)x * (lnx_of(lnx, x) - t.lp);
+        q2 &= prop_ok(x, N2, t.v, hb.B2, floatv);
+      }
+    }
+    if (g1) {
+      const uint32_t x = atomicExch(&H1a[g1 * S1], 0u);
+      if (x) {
+        const PL t = T[P.t1a + g1];
+        sa += (double)x * (lnx_of(lnx, x) - t.lp);
+        qa &= prop_ok(x, N1a, t.v, hb.B1a, floatv);
+      }
+    }
+    if (g2) {
+      const uint32_t x = atomicExch(&H1b[g2 * S1], 0u);
+      if (x) {
+        const PL t = T[P.t1b + g2];
+        sb += (double)x * (lnx_of(lnx, x) - t.lp);
+        qb &= prop_ok(x, N1b, t.v, hb.B1b, floatv);
+      }
+    }
+  }
+  s2 = group_sum_d<G>(s2, redd, 0);
+  sa = group_sum_d<G>(sa, redd, 1);
+  sb = group_sum_d<G>(sb, redd, 2);
+  const unsigned long long bad = group_sum_u64<G>((unsigned long long)(!q2) | ((unsigned long long)(!qa) << 21) |
+                                                  ((unsigned long long)(!qb) << 42), redu, 3);
+  o.t2d = clr_value(s2, o.n2, (bad & 0x1fffffull) == 0, hb.flags & BGF_NAN2, lnx);
+  o.t1a = clr_value(sa, o.n1a, ((bad >> 21) & 0x1fffffull) == 0, hb.flags & BGF_NAN1A, lnx);
+  o.t1b = clr_value(sb, o.n1b, (bad >> 42) == 0, hb.flags & BGF_NAN1B, lnx);
+  return o;
+}
+
+// |T| this small may be an exactly proportional window (reference: T == 0.0 exactly, which its
+// truthiness guard reads as False): such windows are re-evaluated on the exact path.
+__device__ __forceinline__ bool suspect_zero(double t, uint32_t N) {
+  return N && fabs(t) <= 1e-9 * ((double)N + 1.0);
+}
+
+struct Win {
+  uint32_t b, e;
+  uint4 v0, v1;   // bins of the first chunk (SNPs [b & ~3, +512))
+  bool has;
+};
+
+// F(x) = x ln x from the LDS table, the global ln table beyond it
+__device__ __forceinline__ double xlnx(uint32_t x, const double* Ft, const double* lnx) {
+  return x < (uint32_t)LNT ? Ft[x] : (double)x * lnx[x];
+}
+
+// K3 for small grids.  Workgroup LDS: [lp table of the chunk's background (nb2 doubles) | D | F |
+// per wave: 2D bins (u16-packed when P16) | R1 x folded pop1 1D | R1 x pop2 1D | 64 trash words].
+// Per window (one wavefront): pass over its bins (first 512 prefetched with the previous window):
+// ballots give every count, the 2D atomic returns the SNP's rank r in its bin and the SNP adds
+// D(r) - lp_k; the 1D atomics land in lane-&3 replicas; then one lane per 1D bin adds
+// x ln x - x lp; the touched 2D words are cleared; three DPP sums; one record.
+template <bool P16>
+__global__ __launch_bounds__(SBLOCK) void k_scan_w(KParams P, const uint32_t* __restrict__ bins,
+                                                   const Chunk* __restrict__ chunks, uint2* __restrict__ slots,
+                                                   const PL* __restrict__ tab, const double* __restrict__ LPg,
+                                                   const BgHead* __restrict__ head, int bg_per_chrom,
+                                                   const double* __restrict__ lnx, const double* __restrict__ dfg,
+                                                   sfs2d_window* __restrict__ out, uint32_t* __restrict__ err_word,
+                                                   int mode_bp) {
+  extern __shared__ double ldsd[];
+  STAMP(10);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & (WAVE - 1);
+  const Chunk ch = chunks[blockIdx.x];
+  const int bg = bg_per_chrom ? (int)ch.chrom : 0;
+  const PL* T = tab + (size_t)bg * P.nt;
+  const double* LP = LPg + (size_t)bg * P.nt;
+  const BgHead hb = head[bg];
+
+  double* LPl = ldsd;                 // nb2 (rounded up to even: the histograms are 16-B aligned)
+  double* Dt = LPl + ((P.nb2 + 1) & ~1);   // LNT
+  double* Ft = Dt + LNT;              // LNT
+  const int h2w = P16 ? ((P.nb2 + 1) / 2 + 3) & ~3 : (P.nb2 + 3) & ~3;
+  const int h1w = R1 * (P.n1p + 1), h1wb = R1 * (P.n2p + 1);
+  const int per = h2w + h1w + h1wb + TRASH;
+  uint32_t* W = reinterpret_cast<uint32_t*>(Ft + LNT) + wv * per;
+  uint32_t* H1a = W + h2w;
+  uint32_t* H1b = H1a + h1w;
+  const uint32_t trash = (uint32_t)(h2w + h1w + h1wb + lane);   // word offset from W
+  const uint32_t rep = lane & (R1 - 1);
+
+  for (int k = threadIdx.x; k < P.nb2; k += SBLOCK) LPl[k] = LP[k];
+  for (int k = threadIdx.x; k < 2 * LNT; k += SBLOCK) Dt[k] = dfg[k];
+  for (int k = lane; k < per; k += WAVE) W[k] = 0u;
+  // lp of the 1D bins owned by this lane in the per-bin pass (bins 1+lane, 65+lane)
+  double lpa[2], lpb[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int k = 1 + lane + WAVE * j;
+    lpa[j] = k <= P.n1p - 1 ? LP[P.t1a + k] : 0.0;
+    lpb[j] = k <= P.n2p - 1 ? LP[P.t1b + k] : 0.0;
+  }
+  const bool filt = P.ann_want >= 0;
+  const uint32_t zflags = bg_zero_flags(hb);
+  const bool nan2 = hb.flags & BGF_NAN2, nan1a = hb.flags & BGF_NAN1A, nan1b = hb.flags & BGF_NAN1B;
+
+  auto bounds = [&](uint32_t s, uint2 sr, Win& w) {
+    if (mode_bp) {
+      w.has = sr.x != 0u;
+      w.b = sr.x - 1u;
+      w.e = sr.y;
+    } else {
+      w.has = true;
+      w.b = ch.cb + (ch.wid_lo + (s - ch.slot_lo)) * P.ws;
+      w.e = w.b + P.ws;
+    }
+    if (w.has) {
+      const uint32_t i0 = (w.b & ~3u) + 4 * lane;
+      w.v0 = ld4(bins, i0, w.e);
+      w.v1 = ld4(bins, i0 + 4 * WAVE, w.e);
+    }
+  };
+
+  uint32_t s = ch.slot_lo + wv;
+  Win cur;
+  cur.has = false;
+  if (s < ch.slot_hi) bounds(s, mode_bp ? slots[s] : make_uint2(0, 0), cur);
+  __syncthreads();
+  if (s >= ch.slot_hi) return;
+  STAMP(11);
+  int it = 0;
+  for (; s < ch.slot_hi; s += SBLOCK / WAVE, ++it) {
+    const uint32_t sn = s + SBLOCK / WAVE;
+    const bool more = sn < ch.slot_hi;
+    const uint2 srn = (mode_bp && more) ? slots[sn] : make_uint2(0, 0);
+    const uint32_t wid = ch.wid_lo + (s - ch.slot_lo);
+    if (!cur.has) {
+      if (lane == 0) write_empty(out + s, ch.chrom, wid);
+      Win nxt;
+      nxt.has = false;
+      if (more) bounds(sn, srn, nxt);
+      cur = nxt;
+      continue;
+    }
+    // per-lane counters, two 16-bit fields each: {n2 | nlast}, {n1a | n1b}, nvar (a lane sees at
+    // most 1/64 of a window; windows of >= LNX_N SNPs are recounted on the exact path)
+    uint32_t cA = 0, cB = 0, cV = 0;
+    double acc2 = 0.0;
+    uint32_t kw[8];   // the first chunk's 2D words, cleared after the window
+    const uint32_t a0 = cur.b & ~3u;
+    const bool one_chunk = cur.e <= a0 + 8 * WAVE;
+    bool ov = false;   // some SNP's rank in its 2D bin reached LNT (only in windows > LNT SNPs)
+    for (uint32_t base = a0; base < cur.e; base += 8 * WAVE) {
+      const uint32_t i0 = base + 4 * lane, i1 = i0 + 4 * WAVE;
+      const uint4 c0 = base == a0 ? cur.v0 : ld4(bins, i0, cur.e);
+      const uint4 c1 = base == a0 ? cur.v1 : ld4(bins, i1, cur.e);
+      const uint32_t cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      // two halves of four SNPs: atomics, then every table read of the half, then the sums
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        uint32_t rk[4], kk[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int j = 4 * h + jj;
+          const uint32_t i = (h ? i1 : i0) + jj;
+          const uint32_t w = (i >= cur.b && i < cur.e) ? cc[j] : 0u;   // the vectors overhang [b, e)
+          const uint32_t k2 = bin_k2(w), g1 = bin_g1(w), g2 = bin_g2(w);
+          cA += (k2 ? 1u : 0u) + ((w >> 15) & 0x10000u);
+          cB += (g1 ? 1u : 0u) + (g2 ? 0x10000u : 0u);
+          cV += (w >> 30) & 1u;
+          const uint32_t word = k2 ? (P16 ? (k2 >> 1) : k2) : trash;
+          const uint32_t sh = P16 ? ((k2 & 1) << 4) : 0u;
+          const uint32_t old = atomicAdd(&W[word], 1u << sh);
+          rk[jj] = k2 ? (P16 ? ((old >> sh) & 0xffffu) : old) : 0u;   // the trash word's value is junk
+          kk[jj] = k2;
+          if (base == a0) kw[j] = word;
+          atomicAdd(&W[g1 ? (uint32_t)(h2w + g1 * R1 + rep) : trash], 1u);
+          atomicAdd(&W[g2 ? (uint32_t)(h2w + h1w + g2 * R1 + rep) : trash], 1u);
+        }
+        double d[4], lp[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          d[jj] = Dt[min(rk[jj], (uint32_t)LNT - 1u)];   // D[LNT-1] = 0: ranks past the table add 0
+          lp[jj] = LPl[kk[jj]];
+        }
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          ov |= rk[jj] >= (uint32_t)(LNT - 1);
+          acc2 += kk[jj] ? d[jj] - lp[jj] : 0.0;
+        }
+      }
+    }
+    if (it == 0) STAMP(12);
+    // next window: its slot record is in, issue its first chunk now
+    Win nxt;
+    nxt.has = false;
+    if (more) bounds(sn, srn, nxt);
+    group_sync<WAVE>();
+    // 1D spectra: one lane per folded inner bin reads (and clears) its R1 replicas
+    double acca = 0.0, accb = 0.0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = 1 + lane + WAVE * j;
+      if (k <= P.n1p - 1) {
+        uint4* q = reinterpret_cast<uint4*>(H1a + k * R1);
+        const uint4 v = *q;
+        *q = make_uint4(0, 0, 0, 0);
+        const uint32_t x = v.x + v.y + v.z + v.w;
+        acca += x ? xlnx(x, Ft, lnx) - (double)x * lpa[j] : 0.0;
+      }
+      if (k <= P.n2p - 1) {
+        uint4* q = reinterpret_cast<uint4*>(H1b + k * R1);
+        const uint4 v = *q;
+        *q = make_uint4(0, 0, 0, 0);
+        const uint32_t x = v.x + v.y + v.z + v.w;
+        accb += x ? xlnx(x, Ft, lnx) - (double)x * lpb[j] : 0.0;
+      }
+    }
+    // bins with x > LNT-1 SNPs: the ranks from LNT-1 on add F(x) - F(LNT-1) (read before the clear)
+    if (__ballot(ov)) {
+      constexpr uint32_t L1 = LNT - 1;
+      const double fl = Ft[L1];
+      for (int k = lane; k < h2w; k += WAVE) {
+        const uint32_t v = W[k];
+        const uint32_t xa = P16 ? (v & 0xffffu) : v, xb = P16 ? (v >> 16) : 0u;
+        if (xa > L1) acc2 += (double)xa * lnx_of(lnx, xa) - fl;
+        if (xb > L1) acc2 += (double)xb * lnx_of(lnx, xb) - fl;
+      }
+    }
+    // clear the 2D words this window touched
+    if (one_chunk) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) W[kw[j]] = 0u;
+    } else {
+      uint4* q = reinterpret_cast<uint4*>(W);
+      for (int k = lane; k < h2w / 4; k += WAVE) q[k] = make_uint4(0, 0, 0, 0);
+    }
+    if (it == 0) STAMP(13);
+    const double s2 = wave_sum_dpp(acc2), sa = wave_sum_dpp(acca), sb = wave_sum_dpp(accb);
+    cA = wave_sum_dpp_u(cA);
+    cB = wave_sum_dpp_u(cB);
+    const uint32_t n2 = cA & 0xffffu, nlast = cA >> 16, n1a = cB & 0xffffu, n1b = cB >> 16;
+    const uint32_t nvar = filt ? wave_sum_dpp_u(cV) : cur.e - cur.b;
+    WinOut w;
+    w.snp_count = nvar; w.n2_all = n2 + nlast; w.n2 = n2; w.n1a = n1a; w.n1b = n1b;
+    w.t2d = 2.0 * (s2 - xlnx(n2, Ft, lnx));
+    w.t1a = 2.0 * (sa - xlnx(n1a, Ft, lnx));
+    w.t1b = 2.0 * (sb - xlnx(n1b, Ft, lnx));
+    if (cur.e - cur.b >= 65536u || suspect_zero(w.t2d, n2) || suspect_zero(w.t1a, n1a) ||
+        suspect_zero(w.t1b, n1b)) {
+      // rare: exact re-evaluation with the bin-by-bin proportionality test (histograms are clean)
+      group_sync<WAVE>();
+      w = eval_exact<WAVE, P16, R1>(P, bins, cur.b, cur.e, T, hb, lnx, W, H1a, H1b, nullptr, nullptr);
+      if (lane == 0) atomicAdd(err_word + 1, 1u);   // statistics: windows that took the exact path
+    } else {
+      if (nan2) w.t2d = __builtin_nan("");
+      if (nan1a) w.t1a = __builtin_nan("");
+      if (nan1b) w.t1b = __builtin_nan("");
+    }
+    if (lane == 0) {
+      write_rec(out + s, ch.chrom, wid, cur.b, cur.e, w, zflags);
+      if (mode_bp) slots[s] = make_uint2(0u, 0u);   // leave the slot table clean for the next run
+    }
+    group_sync<WAVE>();
+    if (it == 0) STAMP(14);
+    cur = nxt;
+  }
+  STAMP(15);
+}
+
+// K3 for large grids: one workgroup per window, exact evaluation.
+template <bool P16>
+__global__ __launch_bounds__(BLOCK) void k_scan_g(KParams P, const uint32_t* __restrict__ bins,
+                                                  const Chunk* __restrict__ chunks, uint2* __restrict__ slots,
+                                                  const PL* __restrict__ tab, const BgHead* __restrict__ head,
+                                                  int bg_per_chrom, const double* __restrict__ lnx,
+                                                  sfs2d_window* __restrict__ out, int mode_bp) {
+  extern __shared__ uint32_t lds[];
+  const int h2w = P16 ? (P.nb2 + 1) / 2 : P.nb2;
+  const int core = h2w + (P.n1p + 1) + (P.n2p + 1);
+  uint32_t* H2 = lds;
+  uint32_t* H1a = H2 + h2w;
+  uint32_t* H1b = H1a + (P.n1p + 1);
+  double* redd = reinterpret_cast<double*>(lds + core + TRASH + ((core + TRASH) & 1));
+  unsigned long long* redu = reinterpret_cast<unsigned long long*>(redd + 32);
+  for (int k = threadIdx.x; k < core; k += BLOCK) H2[k] = 0u;
+  __syncthreads();
+  const Chunk ch = chunks[blockIdx.x];
+  const int bg = bg_per_chrom ? (int)ch.chrom : 0;
+  const PL* T = tab + (size_t)bg * P.nt;
+  const BgHead hb = head[bg];
+  for (uint32_t s = ch.slot_lo; s < ch.slot_hi; ++s) {
+    const uint32_t wid = ch.wid_lo + (s - ch.slot_lo);
+    uint32_t b, e;
+    if (mode_bp) {
+      const uint2 sr = slots[s];
+      __syncthreads();
+      if (sr.x == 0u) {
+        if (threadIdx.x == 0) write_empty(out + s, ch.chrom, wid);
+        continue;
+      }
+      b = sr.x - 1u;
+      e = sr.y;
+    } else {
+      b = ch.cb + wid * P.ws;
+      e = b + P.ws;
+    }
+    const WinOut w = eval_exact<BLOCK, P16, 1>(P, bins, b, e, T, hb, lnx, H2, H1a, H1b, redd, redu);
+    if (threadIdx.x == 0) {
+      write_rec(out + s, ch.chrom, wid, b, e, w, bg_zero_flags(hb));
+      if (mode_bp) slots[s] = make_uint2(0u, 0u);
+    }
+  }
+}
+
+// first index j in [cb, e) such that SNPs j..e-1 share the fixed-bp window of SNP e-1 (per wave)
+__device__ uint32_t window_begin_back(const uint32_t* __restrict__ pos, long long cb, uint32_t e, uint32_t ws) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  const uint32_t w = wid_of(pos[e - 1], ws);
+  long long hi = (long long)e - 1;   // pos[hi] is in the window
+  while (true) {
+    const long long j = hi - 1 - lane;
+    const bool outside = (j < cb) || (wid_of(pos[j], ws) != w);
+    const unsigned long long m = __ballot(outside);
+    if (m) return (uint32_t)(hi - __builtin_ctzll(m));
+    hi -= WAVE;
+  }
+}
+
+// Q9 helper (combined_scan's final block, twoDSFS_class.py:951-989): the window before the last
+// one, evaluated against the LAST window's chromosome background.  One wavefront; launched only
+// for plans with SFS2D_F_PREV_EXTRA.
+template <bool P16>
+__global__ __launch_bounds__(WAVE) void k_scan_extra(KParams P, const uint32_t* __restrict__ bins,
+                                                     const uint32_t* __restrict__ pos, uint32_t chrom_last,
+                                                     const long long* __restrict__ chrom_off,
+                                                     const PL* __restrict__ tab, const BgHead* __restrict__ head,
+                                                     int bg_per_chrom, const double* __restrict__ lnx,
+                                                     sfs2d_window* __restrict__ out, long long extra_rec) {
+  extern __shared__ uint32_t lds[];
+  const int h2w = P16 ? (P.nb2 + 1) / 2 : P.nb2;
+  const int core = h2w + (P.n1p + 1) + (P.n2p + 1);
+  uint32_t* H2 = lds;
+  uint32_t* H1a = H2 + h2w;
+  uint32_t* H1b = H1a + (P.n1p + 1);
+  for (int k = threadIdx.x; k < core; k += WAVE) H2[k] = 0u;
+  group_sync<WAVE>();
+  const long long cb = chrom_off[chrom_last];
+  const PL* T = tab + (bg_per_chrom ? (size_t)chrom_last * P.nt : 0);
+  const BgHead hb = head[bg_per_chrom ? chrom_last : 0];
+  const long long ce = chrom_off[chrom_last + 1];
+  const uint32_t bl = window_begin_back(pos, cb, (uint32_t)ce, P.ws);
+  WinOut w;
+  memset(&w, 0, sizeof(w));
+  uint32_t pb = 0, pe = 0, pc = chrom_last, flags = SFS2D_W_EXTRA | bg_zero_flags(hb);
+  if (bl > 0) {
+    pe = bl;
+    int c2 = (int)chrom_last;
+    while (c2 > 0 && chrom_off[c2] >= (long long)pe) --c2;
+    pc = (uint32_t)c2;
+    pb = window_begin_back(pos, chrom_off[c2], pe, P.ws);
+    w = eval_exact<WAVE, P16, 1>(P, bins, pb, pe, T, hb, lnx, H2, H1a, H1b, nullptr, nullptr);
+  } else {
+    flags |= SFS2D_W_EMPTY;
+  }
+  if (threadIdx.x == 0) write_rec(out + extra_rec, pc, bl, pb, pe, w, flags);
+}
+
+}  // namespace sfs2dk

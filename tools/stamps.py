@@ -25,7 +25,7 @@ t = list(buf)
 def d(a, b):
     return (t[b] - t[a]) * 0.01 if t[a] and t[b] else float("nan")
 print(which, "K1 blk0: zero %.2f  loop %.2f  flush %.2f us" % (d(20, 21), d(21, 22), d(22, 23)))
-print(which, "K2 blk0: repl %.2f  Bsum %.2f  p/lp %.2f  leaves %.2f  tail %.2f us" % (d(0, 1), d(1, 2), d(2, 3), d(3, 4), d(4, 5)))
-print(which, "K3 blk0: prologue %.2f  phaseA(1st) %.2f  take2D %.2f  1D+reduce+store %.2f  rest %.2f us" % (
+print(which, "K2 slice0: repl+p/lp %.2f  leaves %.2f us; tail block: %.2f us" % (d(0, 1), d(1, 2), d(3, 4)))
+print(which, "K3 blk0: prologue %.2f  2D pass(1st) %.2f  1D+clear %.2f  reduce+store %.2f  rest %.2f us" % (
     d(10, 11), d(11, 12), d(12, 13), d(13, 14), d(14, 15)))
-print(which, "gaps: K1end->K2start %.2f  K2end->K3start %.2f us" % (d(23, 0), d(5, 10)))
+print(which, "gaps: K1end->K2start %.2f  K2end->K3start %.2f us" % (d(23, 0), d(4, 10)))
