@@ -27,34 +27,47 @@ using namespace sfs2dk;
 namespace {
 
 // numpy pairwise_sum recursion over n elements: n <= 128 -> leaf (np_leaf_sum), else split at
-// n2 = n/2 - (n/2 % 8).  Leaves are numbered left to right; internal nodes get ids nleaves + i in
-// an order where children precede parents (post-order), the root last.
+// n2 = n/2 - (n/2 % 8).  Leaves are numbered left to right; internal nodes get ids nleaves + i
+// sorted by height (children before parents, the root last), with level = height - 1, so that a
+// node can be combined as soon as its level is reached (same sums, same order inside each node).
 struct PwTree {
   std::vector<int2> leaves;   // {offset, n}
-  std::vector<int2> nodes;    // children ids (leaf ids < nleaves, node ids >= nleaves)
+  std::vector<int4> nodes;    // {child a, child b, level, 0} (leaf ids < nleaves, node ids >= nleaves)
+  int nlevels = 0;
 };
 
-int pw_build(int lo, int n, PwTree& t, std::vector<int2>& raw) {
-  // returns a provisional id: >= 0 leaf, < 0 internal node -(i+1) in post-order
+int pw_build(int lo, int n, PwTree& t, std::vector<int2>& raw, std::vector<int>& height) {
+  // returns a provisional id: >= 0 leaf, < 0 internal node -(i+1)
   if (n <= 128) {
     t.leaves.push_back(make_int2(lo, n));
     return (int)t.leaves.size() - 1;
   }
   int n2 = n / 2;
   n2 -= n2 % 8;
-  const int a = pw_build(lo, n2, t, raw);
-  const int b = pw_build(lo + n2, n - n2, t, raw);
+  const int a = pw_build(lo, n2, t, raw, height);
+  const int b = pw_build(lo + n2, n - n2, t, raw, height);
+  auto h = [&](int id) { return id >= 0 ? 0 : height[-id - 1]; };
   raw.push_back(make_int2(a, b));
+  height.push_back(std::max(h(a), h(b)) + 1);
   return -(int)raw.size();
 }
 
 PwTree pw_plan(int n) {
   PwTree t;
   std::vector<int2> raw;
-  if (n > 0) pw_build(0, n, t, raw);
+  std::vector<int> height;
+  if (n > 0) pw_build(0, n, t, raw, height);
   const int L = (int)t.leaves.size();
-  auto remap = [&](int id) { return id >= 0 ? id : L + (-id - 1); };
-  for (const int2& r : raw) t.nodes.push_back(make_int2(remap(r.x), remap(r.y)));
+  std::vector<int> order(raw.size());
+  for (size_t i = 0; i < raw.size(); ++i) order[i] = (int)i;
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return height[x] < height[y]; });
+  std::vector<int> newid(raw.size());
+  for (size_t i = 0; i < order.size(); ++i) newid[order[i]] = L + (int)i;
+  auto remap = [&](int id) { return id >= 0 ? id : newid[-id - 1]; };
+  for (int i : order) {
+    t.nodes.push_back(make_int4(remap(raw[i].x), remap(raw[i].y), height[i] - 1, 0));
+    t.nlevels = std::max(t.nlevels, height[i]);
+  }
   return t;
 }
 
@@ -103,6 +116,9 @@ struct sfs2d_plan {
   KParams K{};
   int nbg = 0;
   bool do_bg = false, do_seg = false, lds_hist = true, bg_ready = false;
+  bool fused = false;       // per-chromosome tables built inside k_scan_w (parity-alternating replicas)
+  int hr = 1;               // k_prep LDS histogram copies per word
+  uint64_t runs = 0;        // completed runs (the replica parity of a fused plan)
   int G = 64;
   bool p16 = true;
   size_t scan_lds = 0, bg_lds = 0, extra_lds = 0;
@@ -124,9 +140,9 @@ struct sfs2d_plan {
   Bg1D* d_bg1d = nullptr;
   double* d_leafsum = nullptr;
   int2* d_leaves = nullptr;
-  int2* d_nodes = nullptr;
+  int4* d_nodes = nullptr;
   int4* d_slices = nullptr;
-  int nleaves = 0, nnodes = 0;
+  int nleaves = 0, nnodes = 0, nlevels = 0;
   uint32_t* d_bins = nullptr;     // packed per-SNP bins written by k_prep, read by the scan kernels
   sfs2d_window* d_out = nullptr;
   uint32_t* d_err = nullptr;
@@ -170,15 +186,24 @@ void plan_free(sfs2d_plan* p) {
   for (auto& e : p->tev) if (e) hipEventDestroy(e);
 }
 
+int plan_par(const sfs2d_plan* pl) { return pl->fused ? (int)(pl->runs & 1) : 0; }
+
+template <bool P16, bool FUSED>
+void launch_scan_w(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
+  hipLaunchKernelGGL((k_scan_w<P16, FUSED>), dim3((unsigned)pl->chunks.size()), dim3(SBLOCK), pl->scan_lds,
+                     pl->ctx->stream, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
+                     per_chrom, pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, bp, pl->d_repl, pl->d_bcount,
+                     plan_par(pl), pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels);
+}
+
 template <bool P16>
 hipError_t launch_scan(sfs2d_plan* pl, sfs2d_window* out) {
   const int per_chrom = pl->prm.bg_mode == SFS2D_BG_PER_CHROM ? 1 : 0;
   const int bp = pl->prm.window_mode == SFS2D_WINDOW_BP ? 1 : 0;
-  if (pl->G == WAVE)
-    hipLaunchKernelGGL((k_scan_w<P16>), dim3((unsigned)pl->chunks.size()), dim3(SBLOCK), pl->scan_lds, pl->ctx->stream,
-                       pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head, per_chrom,
-                       pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, bp);
-  else
+  if (pl->G == WAVE) {
+    if (pl->fused) launch_scan_w<P16, true>(pl, out, per_chrom, bp);
+    else launch_scan_w<P16, false>(pl, out, per_chrom, bp);
+  } else
     hipLaunchKernelGGL((k_scan_g<P16>), dim3((unsigned)pl->chunks.size()), dim3(BLOCK), pl->scan_lds, pl->ctx->stream,
                        pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_head, per_chrom,
                        pl->ctx->d_lnx, out, bp);
@@ -188,9 +213,11 @@ hipError_t launch_scan(sfs2d_plan* pl, sfs2d_window* out) {
 template <bool B, bool S, bool L, bool N>
 hipError_t launch_prep1(sfs2d_plan* pl) {
   const sfs2d_data* d = pl->data;
+  const int par = plan_par(pl);
   hipLaunchKernelGGL((k_prep<B, S, L, N>), dim3((unsigned)pl->tiles.size()), dim3(BLOCK1), (B && L) ? pl->bg_lds : 0,
-                     pl->ctx->stream, pl->K, d->counts, d->pos, d->ann, pl->d_tiles, pl->d_repl, pl->d_slots,
-                     pl->d_bins, pl->d_bcount, pl->d_err);
+                     pl->ctx->stream, pl->K, d->counts, d->pos, d->ann, pl->d_tiles,
+                     pl->d_repl + (size_t)par * REPL * pl->K.nchrom * pl->K.nh, pl->d_slots, pl->d_bins,
+                     pl->d_bcount + (size_t)par * pl->K.nchrom, pl->d_err, L ? pl->hr : 1);
   return hipGetLastError();
 }
 
@@ -402,7 +429,7 @@ static int make_kparams(sfs2d_ctx* ctx, const sfs2d_params* prm, int nchrom, KPa
   if (prm->bg_mode != SFS2D_BG_PER_CHROM && prm->bg_mode != SFS2D_BG_SUPPLIED) return set_err(ctx, SFS2D_E_ARG, "bad bg_mode");
   K->n1p = prm->n1p; K->n2p = prm->n2p; K->n1 = 2 * prm->n1p; K->n2 = 2 * prm->n2p;
   K->nb2 = (K->n1 + 1) * (K->n2 + 1);
-  K->h1a = K->nb2; K->h1b = K->nb2 + K->n1 + 1; K->nh = K->h1b + K->n2 + 1;
+  K->h1a = K->nb2; K->h1b = K->nb2 + K->n1 + 1; K->nh = (K->h1b + K->n2 + 1 + 3) & ~3;   // 16-B rows
   K->t1a = K->nb2; K->t1b = K->nb2 + K->n1p + 1; K->nt = K->t1b + K->n2p + 1;
   K->fold = prm->fold ? 1 : 0;
   K->ann_want = prm->ann_want;
@@ -480,10 +507,12 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
     const int core = (pl->p16 ? (K.nb2 + 1) / 2 : K.nb2) + (K.n1p + 1) + (K.n2p + 1);
     pl->extra_lds = (size_t)core * 4;
     if (pl->G == WAVE) {
-      // k_scan_w: lp table (even-rounded) + D + F tables, then 8 per-wave histogram blocks
+      // k_scan_w: lp table (even-rounded) + D + F tables, then 8 per-wave histogram blocks (also the
+      // fused prologue's scratch: u1 words, 1D proportions, leaf accumulators and sums)
       const int h2w = pl->p16 ? (((K.nb2 + 1) / 2 + 3) & ~3) : ((K.nb2 + 3) & ~3);
       const int per = h2w + R1 * (K.n1p + 1) + R1 * (K.n2p + 1) + TRASH;
-      pl->scan_lds = sizeof(double) * (size_t)(((K.nb2 + 1) & ~1) + 2 * LNT) + (size_t)(SBLOCK / WAVE) * per * 4;
+      const size_t hist_words = std::max<size_t>((size_t)(SBLOCK / WAVE) * per, 2 * (1536 + 256) + 16);
+      pl->scan_lds = sizeof(double) * (size_t)(((K.nt + 1) & ~1) + 2 * LNT) + hist_words * 4;
     } else {
       pl->scan_lds = (size_t)(core + TRASH + 2) * 4 + 32 * 8 + 32 * 8;
     }
@@ -492,9 +521,12 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
     delete pl;
     return set_err(ctx, SFS2D_E_ARG, "2D grid too large for LDS with 32-bit bins (windows of >= 65536 SNPs)");
   }
+  pl->fused = pl->do_bg && pl->G == WAVE;
   if (pl->scan_lds > 64 * 1024) {
-    hipFuncSetAttribute((const void*)k_scan_w<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
-    hipFuncSetAttribute((const void*)k_scan_w<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
+    hipFuncSetAttribute((const void*)k_scan_w<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
+    hipFuncSetAttribute((const void*)k_scan_w<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
+    hipFuncSetAttribute((const void*)k_scan_w<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
+    hipFuncSetAttribute((const void*)k_scan_w<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
     hipFuncSetAttribute((const void*)k_scan_g<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
     hipFuncSetAttribute((const void*)k_scan_g<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
   }
@@ -509,8 +541,8 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
   uint32_t CH = 2;
   if (pl->G == WAVE) {
     int occ = 0;
-    const hipError_t oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<true>, SBLOCK, pl->scan_lds)
-                                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<false>, SBLOCK, pl->scan_lds);
+    const hipError_t oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<true, true>, SBLOCK, pl->scan_lds)
+                                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<false, true>, SBLOCK, pl->scan_lds);
     if (oe != hipSuccess || occ < 1) occ = 1;
     const int64_t cap = (int64_t)occ * ctx->ncu;
     auto nchunks = [&](uint32_t L) {
@@ -548,7 +580,8 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
         pl->tiles.push_back(t);
       }
   }
-  pl->bg_lds = (size_t)K.nh * 4;
+  pl->hr = (size_t)K.nh * 4 * 4 <= 64 * 1024 ? 4 : 1;
+  pl->bg_lds = (size_t)K.nh * 4 * pl->hr;
   pl->lds_hist = pl->bg_lds <= 150 * 1024;
   if (pl->lds_hist && pl->bg_lds > 64 * 1024) {
     hipFuncSetAttribute((const void*)k_prep<true, true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->bg_lds);
@@ -562,6 +595,7 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
   const PwTree pw = pw_plan(K.nb2 - 3);
   pl->nleaves = (int)pw.leaves.size();
   pl->nnodes = (int)pw.nodes.size();
+  pl->nlevels = pw.nlevels;
   if (pl->nleaves > PW_MAX_LEAVES) { delete pl; return set_err(ctx, SFS2D_E_ARG, "grid too large for the pairwise plan"); }
   for (int j = 0; j < pl->nleaves; j += LEAVES_PER_SLICE) {
     const int jl = std::min(pl->nleaves, j + LEAVES_PER_SLICE);
@@ -576,8 +610,9 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
   rc = rc ? rc : dalloc(ctx, &pl->d_tiles, pl->tiles.size());
   rc = rc ? rc : dalloc(ctx, &pl->d_chunks, pl->chunks.size());
   rc = rc ? rc : dalloc(ctx, &pl->d_slots, (size_t)pl->nslots + 1);
-  rc = rc ? rc : dalloc(ctx, &pl->d_repl, pl->do_bg ? (size_t)REPL * nc * K.nh : 1);
-  rc = rc ? rc : dalloc(ctx, &pl->d_bcount, (size_t)std::max(1, nc));
+  const size_t nrepl = pl->do_bg ? (size_t)(pl->fused ? 2 : 1) * REPL * nc * K.nh : 1;
+  rc = rc ? rc : dalloc(ctx, &pl->d_repl, nrepl);
+  rc = rc ? rc : dalloc(ctx, &pl->d_bcount, (size_t)2 * std::max(1, nc));
   rc = rc ? rc : dalloc(ctx, &pl->d_done, (size_t)pl->nbg);
   rc = rc ? rc : dalloc(ctx, &pl->d_bgval, (size_t)pl->nbg * K.nt);
   rc = rc ? rc : dalloc(ctx, &pl->d_tab, (size_t)pl->nbg * K.nt);
@@ -602,8 +637,8 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
   PCPY(pl->d_slices, pl->slices);
 #undef PCPY
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_slots, 0, sizeof(uint2) * ((size_t)pl->nslots + 1), st);
-  if (e == hipSuccess && pl->do_bg) e = hipMemsetAsync(pl->d_repl, 0, sizeof(uint32_t) * (size_t)REPL * nc * K.nh, st);
-  if (e == hipSuccess) e = hipMemsetAsync(pl->d_bcount, 0, sizeof(uint32_t) * std::max(1, nc), st);
+  if (e == hipSuccess && pl->do_bg) e = hipMemsetAsync(pl->d_repl, 0, sizeof(uint32_t) * nrepl, st);
+  if (e == hipSuccess) e = hipMemsetAsync(pl->d_bcount, 0, sizeof(uint32_t) * 2 * std::max(1, nc), st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_done, 0, sizeof(uint32_t) * pl->nbg, st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_err, 0, 4 * sizeof(uint32_t), st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_bins, 0, sizeof(uint32_t) * nbins, st);
@@ -655,11 +690,12 @@ int sfs2d_plan_run_phase(sfs2d_plan* pl, int phase, sfs2d_window* out_dev) {
   }
   if (te) HIPCHK(ctx, hipEventRecord(te[1], ctx->stream));
   if (phase == 0 || phase == 2) {
-    if (pl->do_bg) HIPCHK(ctx, launch_bg_slices(pl));
+    if (pl->do_bg && !pl->fused) HIPCHK(ctx, launch_bg_slices(pl));
     if (te) HIPCHK(ctx, hipEventRecord(te[2], ctx->stream));
     sfs2d_window* out = out_dev ? out_dev : pl->d_out;
     HIPCHK(ctx, launch_scan_any(pl, out));
     pl->last_out = out;
+    pl->runs++;
   }
   if (te) {
     HIPCHK(ctx, hipEventRecord(te[3], ctx->stream));
@@ -705,7 +741,8 @@ int sfs2d_plan_run(sfs2d_plan* pl, sfs2d_window* out_dev) { return sfs2d_plan_ru
 
 int sfs2d_plan_bg_buffer(sfs2d_plan* pl, void** dev_ptr, int64_t* nbytes) {
   if (!pl || !dev_ptr || !nbytes) return SFS2D_E_ARG;
-  *dev_ptr = pl->d_repl;
+  // the replica buffer the next run's k_prep accumulates into (fused plans alternate two)
+  *dev_ptr = pl->d_repl + (size_t)plan_par(pl) * REPL * pl->data->nchrom * pl->K.nh;
   *nbytes = pl->do_bg ? (int64_t)REPL * pl->data->nchrom * pl->K.nh * 4 : 0;
   return 0;
 }
@@ -766,9 +803,10 @@ int sfs2d_plan_time(sfs2d_plan* pl, int iters, double* ms_run, double* ms_k1, do
     HIPCHK(ctx, hipEventRecord(pl->ev[0], st));
     HIPCHK(ctx, launch_prep(pl, true));
     HIPCHK(ctx, hipEventRecord(pl->ev[1], st));
-    if (pl->do_bg) HIPCHK(ctx, launch_bg_slices(pl));
+    if (pl->do_bg && !pl->fused) HIPCHK(ctx, launch_bg_slices(pl));
     HIPCHK(ctx, hipEventRecord(pl->ev[2], st));
     HIPCHK(ctx, launch_scan_any(pl, pl->d_out));
+    pl->runs++;
     HIPCHK(ctx, hipEventRecord(pl->ev[3], st));
     HIPCHK(ctx, hipEventSynchronize(pl->ev[3]));
     float a = 0, b = 0, c = 0, d = 0;
@@ -844,7 +882,7 @@ int sfs2d_bg_hist(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* pr
   pl.d_tiles = nullptr; pl.d_repl = nullptr; pl.d_err = nullptr; pl.d_bcount = nullptr;
   if (e != hipSuccess) return set_err(ctx, SFS2D_E_HIP, std::string("bg_hist: ") + hipGetErrorString(e));
   if (rc) return rc;
-  for (int k = 0; k < K.nh; ++k) {
+  for (int k = 0; k < K.h1b + K.n2 + 1; ++k) {
     int64_t s = 0;
     for (int r = 0; r < REPL; ++r) s += hist[(size_t)r * K.nh + k];
     if (k < K.nb2) h2d[k] = s;

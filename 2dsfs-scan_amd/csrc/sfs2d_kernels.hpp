@@ -78,7 +78,7 @@ constexpr uint32_t B_VAR = 1u << 30, B_LAST = 1u << 31;
 struct KParams {
   int n1p, n2p, n1, n2;  // diploid sizes and haploid sample sizes
   int nb2;               // (n1+1)*(n2+1) 2D bins
-  int nh;                // background histogram words per chromosome: nb2 + (n1+1) + (n2+1)
+  int nh;                // background histogram words per chromosome: nb2 + (n1+1) + (n2+1), rounded up to 4
   int h1a, h1b;          // offsets of the unfolded 1D histograms inside a background histogram
   int nt;                // table entries per background: nb2 + (n1p+1) + (n2p+1)
   int t1a, t1b;          // offsets of the folded 1D tables
@@ -300,16 +300,21 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
                                                  const uint32_t* __restrict__ pos, const uint16_t* __restrict__ ann,
                                                  const Tile* __restrict__ tiles, uint32_t* __restrict__ repl,
                                                  uint2* __restrict__ slots, uint32_t* __restrict__ bins,
-                                                 uint32_t* __restrict__ bcount, uint32_t* __restrict__ err_word) {
+                                                 uint32_t* __restrict__ bcount, uint32_t* __restrict__ err_word,
+                                                 int hr) {
+  // repl / bcount: this run's parity buffers.  LDS histogram: hr interleaved copies of every word
+  // (lane & (hr-1) picks one), which spreads the many same-bin atomics of a wavefront over banks.
   extern __shared__ uint32_t sh_hist[];
   __shared__ uint32_t sh_b2;
   STAMP(20);
   const Tile t = tiles[blockIdx.x];
   uint32_t* gh = repl + ((size_t)(blockIdx.x % REPL) * P.nchrom + t.chrom) * (size_t)P.nh;
-  uint32_t* H = LDS_HIST ? sh_hist : gh;
+  const int lane0 = threadIdx.x & (WAVE - 1);
+  const int hsh = LDS_HIST ? (hr == 4 ? 2 : 0) : 0;
+  uint32_t* H = LDS_HIST ? sh_hist + (lane0 & (hr - 1)) : gh;
   if (DO_BG) {
     if (LDS_HIST)
-      for (int k = threadIdx.x; k < P.nh; k += BLOCK1) sh_hist[k] = 0u;
+      for (int k = threadIdx.x; k < P.nh * hr; k += BLOCK1) sh_hist[k] = 0u;
     if (threadIdx.x == 0) sh_b2 = 0u;
     __syncthreads();
   }
@@ -345,9 +350,9 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
       int k2all, u1a, u1b;
       bw[k] = classify(P, cc[k], var_ok, pos_ok, err, k2all, u1a, u1b);
       if (DO_BG && in) {
-        if (k2all >= 0) atomicAdd(&H[k2all], 1u);
-        if (u1a >= 0) atomicAdd(&H[P.h1a + u1a], 1u);
-        if (u1b >= 0) atomicAdd(&H[P.h1b + u1b], 1u);
+        if (k2all >= 0) atomicAdd(&H[k2all << hsh], 1u);
+        if (u1a >= 0) atomicAdd(&H[(P.h1a + u1a) << hsh], 1u);
+        if (u1b >= 0) atomicAdd(&H[(P.h1b + u1b) << hsh], 1u);
         b2 += bin_k2(bw[k]) ? 1u : 0u;
       }
       if (DO_SEG && in) {
@@ -412,7 +417,13 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
     __syncthreads();
     if (LDS_HIST)
       for (int k = threadIdx.x; k < P.nh; k += BLOCK1) {
-        const uint32_t v = sh_hist[k];
+        uint32_t v;
+        if (hr == 4) {
+          const uint4 q = *reinterpret_cast<const uint4*>(sh_hist + 4 * k);
+          v = q.x + q.y + q.z + q.w;
+        } else {
+          v = sh_hist[k];
+        }
         if (v) atomicAdd(&gh[k], v);
       }
     if (threadIdx.x == 0 && sh_b2) atomicAdd(&bcount[t.chrom], sh_b2);
@@ -489,14 +500,14 @@ __device__ __forceinline__ uint32_t adjust_last(PL* T, double* LP, int klast, do
 // spectra; the last block of a background to finish combines the leaves and writes its head.
 // The replicas, the inner-sum counters and the completion counter are left zeroed.
 // slices[s] = {kb, ke, leaf_lo, leaf_hi}; leaves[j] = {offset into p[1:], n}; nodes: numpy's tree
-// (children ids into [leaves | nodes], ordered children-first).
+// (children ids into [leaves | nodes] and the node's level, ordered by height: children first).
 __global__ __launch_bounds__(KBLOCK) void k_bg_slice(KParams P, uint32_t* __restrict__ repl,
                                                      uint32_t* __restrict__ bcount, PL* __restrict__ tab,
                                                      double* __restrict__ LPg, BgHead* __restrict__ head,
                                                      double* __restrict__ leafsum, Bg1D* __restrict__ bg1d,
                                                      uint32_t* __restrict__ done, const int4* __restrict__ slices,
                                                      int nslices, const int2* __restrict__ leaves, int nleaves,
-                                                     const int2* __restrict__ nodes, int nnodes) {
+                                                     const int4* __restrict__ nodes, int nnodes) {
   __shared__ double pv[4 * 128 + 8];
   __shared__ double acc8[KBLOCK];
   __shared__ uint32_t u1[2 * 256 + 2];
@@ -626,7 +637,7 @@ __global__ __launch_bounds__(KBLOCK) void k_bg_slice(KParams P, uint32_t* __rest
       double* node = acc8;   // leaves then internal nodes (<= 2 * PW_MAX_LEAVES entries)
       for (int j = 0; j < nleaves; ++j) node[j] = leafsum[(size_t)b * nleaves + j];
       for (int i = 0; i < nnodes; ++i) {
-        const int2 ab = nodes[i];
+        const int4 ab = nodes[i];
         node[nleaves + i] = node[ab.x] + node[ab.y];
       }
       const double S = (nleaves + nnodes) ? node[nleaves + nnodes - 1] : 0.0;
@@ -647,7 +658,7 @@ __global__ __launch_bounds__(FBLOCK) void k_bg_finalize(KParams P, int integer_v
                                                         double* __restrict__ scratch, PL* __restrict__ tab,
                                                         double* __restrict__ LPg, BgHead* __restrict__ head,
                                                         const int2* __restrict__ pw_leaves, int pw_nleaves,
-                                                        const int2* __restrict__ pw_nodes, int pw_nnodes) {
+                                                        const int4* __restrict__ pw_nodes, int pw_nnodes) {
   extern __shared__ double v_lds[];
   __shared__ double red[FBLOCK / WAVE];
   __shared__ double node[2 * PW_MAX_LEAVES];
@@ -706,7 +717,7 @@ __global__ __launch_bounds__(FBLOCK) void k_bg_finalize(KParams P, int integer_v
   __syncthreads();
   if (tid == 0) {
     for (int i = 0; i < pw_nnodes; ++i) {
-      const int2 ab = pw_nodes[i];
+      const int4 ab = pw_nodes[i];
       node[pw_nleaves + i] = node[ab.x] + node[ab.y];
     }
     uint32_t flags = integer_values ? 0u : BGF_FLOATV;
@@ -790,9 +801,42 @@ __device__ __forceinline__ uint32_t h2_take(uint32_t* h, uint32_t k) {  // read-
 // bin-by-bin proportionality test.  Used for large grids, for windows whose fast-path |T| is ~0
 // (possibly exactly proportional), for windows of >= LNX_N SNPs, and for the Q9 helper.
 // S1: word stride of the 1D histograms (k_scan_w keeps R1 replicas per bin; this uses the first).
-template <int G, bool P16, int S1>
+// Background table views for eval_exact: lp(k) and v(k) (the count, or p for normalised backgrounds)
+struct TabGlobal {   // the PL table written by k_bg_slice / k_bg_finalize
+  const PL* T;
+  __device__ __forceinline__ PL at(int k) const { return T[k]; }
+};
+
+struct TabFused {    // k_scan_w's own table: lp in LDS, counts summed from this run's replicas
+  const double* LPl;
+  const uint32_t* R;   // this chromosome's replica 0; replica r at R + r * rs
+  size_t rs;
+  int nb2, n1, n2, n1p, h1a, h1b, t1a, t1b;
+  __device__ __forceinline__ uint32_t u(int k) const {
+    uint32_t s = 0;
+#pragma unroll
+    for (int r = 0; r < REPL; ++r) s += R[k + r * rs];
+    return s;
+  }
+  __device__ __forceinline__ PL at(int k) const {
+    PL e;
+    e.lp = LPl[k];
+    if (k < nb2) {
+      e.v = (double)u(k);
+    } else if (k < t1b) {
+      const int f = k - t1a;   // fold_1d_sfs: u[f] + u[2n - f] (f < n)
+      e.v = (double)u(h1a + f) + (f < n1p ? (double)u(h1a + n1 - f) : 0.0);
+    } else {
+      const int f = k - t1b, n2p = n2 / 2;
+      e.v = (double)u(h1b + f) + (f < n2p ? (double)u(h1b + n2 - f) : 0.0);
+    }
+    return e;
+  }
+};
+
+template <int G, bool P16, int S1, class Tab>
 __device__ __forceinline__ WinOut eval_exact(const KParams& P, const uint32_t* __restrict__ bins, uint32_t b,
-                                             uint32_t e, const PL* __restrict__ T, const BgHead& hb,
+                                             uint32_t e, const Tab& T, const BgHead& hb,
                                              const double* __restrict__ lnx, uint32_t* H2, uint32_t* H1a,
                                              uint32_t* H1b, double* redd, unsigned long long* redu) {
   const int lane = threadIdx.x & (G - 1);
@@ -826,7 +870,7 @@ __device__ __forceinline__ WinOut eval_exact(const KParams& P, const uint32_t* _
     if (k2) {
       const uint32_t x = h2_take<P16>(H2, k2);
       if (x) {
-        const PL t = T[k2];
+        const PL t = T.at(k2);
         s2 += (double)x * (lnx_of(lnx, x) - t.lp);
         q2 &= prop_ok(x, N2, t.v, hb.B2, floatv);
       }
@@ -834,7 +878,7 @@ __device__ __forceinline__ WinOut eval_exact(const KParams& P, const uint32_t* _
     if (g1) {
       const uint32_t x = atomicExch(&H1a[g1 * S1], 0u);
       if (x) {
-        const PL t = T[P.t1a + g1];
+        const PL t = T.at(P.t1a + g1);
         sa += (double)x * (lnx_of(lnx, x) - t.lp);
         qa &= prop_ok(x, N1a, t.v, hb.B1a, floatv);
       }
@@ -842,7 +886,7 @@ __device__ __forceinline__ WinOut eval_exact(const KParams& P, const uint32_t* _
     if (g2) {
       const uint32_t x = atomicExch(&H1b[g2 * S1], 0u);
       if (x) {
-        const PL t = T[P.t1b + g2];
+        const PL t = T.at(P.t1b + g2);
         sb += (double)x * (lnx_of(lnx, x) - t.lp);
         qb &= prop_ok(x, N1b, t.v, hb.B1b, floatv);
       }
@@ -876,57 +920,242 @@ __device__ __forceinline__ double xlnx(uint32_t x, const double* Ft, const doubl
   return x < (uint32_t)LNT ? Ft[x] : (double)x * lnx[x];
 }
 
-// K3 for small grids.  Workgroup LDS: [lp table of the chunk's background (nb2 doubles) | D | F |
-// per wave: 2D bins (u16-packed when P16) | R1 x folded pop1 1D | R1 x pop2 1D | 64 trash words].
+// The fused prologue of k_scan_w (kept out of line: it runs once per workgroup and its registers
+// must not count against the window loop's).  Builds the chromosome's background table from this
+// run's replicas -- the k_bg_slice computation -- in LDS (LPl), using the histogram area HB as
+// scratch; clears this workgroup's share of the other parity's replicas; the chromosome's first
+// workgroup (writer) also writes the global tables.  The head lands in *hb_out (LDS).
+__device__ __attribute__((noinline)) void fused_table(int nb2, int nh, int nt, int n1p, int n2p, int n1, int n2,
+                                                      int t1a, int t1b, int nchrom, uint32_t chrom, bool writer,
+                                                      int bg, const uint32_t* __restrict__ Rc, size_t rs,
+                                                      uint32_t* __restrict__ repl, uint32_t* __restrict__ bcount,
+                                                      int par, PL* __restrict__ tab, double* __restrict__ LPg,
+                                                      BgHead* __restrict__ head, double* LPl, uint32_t* HB,
+                                                      const int2* __restrict__ leaves, int nleaves,
+                                                      const int4* __restrict__ nodes, int nnodes, int nlevels,
+                                                      BgHead* hb_out) {
+  __shared__ double sh_misc[8];
+  __shared__ uint32_t sh_flags;
+  const int tid = threadIdx.x;
+  const int lane = tid & (WAVE - 1);
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  BgHead hb;
+  PL* T = tab + (size_t)bg * nt;
+  double* LP = LPg + (size_t)bg * nt;
+  // the other parity's replicas and inner sums: zeroed for the next run, a slice per workgroup
+  {
+    uint32_t* Ro = repl + (size_t)(1 - par) * REPL * rs;
+    const size_t tot = (size_t)REPL * rs, share = (tot + gridDim.x - 1) / gridDim.x;
+    const size_t lo = (size_t)blockIdx.x * share, hi = lo + share < tot ? lo + share : tot;
+    for (size_t k = lo + tid; k < hi; k += SBLOCK) Ro[k] = 0u;
+    if (blockIdx.x == 0)
+      for (int c = tid; c < nchrom; c += SBLOCK) bcount[(size_t)(1 - par) * nchrom + c] = 0u;
+  }
+  // scratch in the histogram area: u1 words, 1D p, leaf accumulators, leaf sums
+  double* scr = reinterpret_cast<double*>(HB);
+  uint32_t* u1 = HB;                 // [0, 512) words
+  double* p1a = scr + 264;           // 128
+  double* p1b = scr + 392;           // 128
+  double* acc8 = scr + 512;          // 8 per leaf (<= 128 leaves)
+  double* lsum = scr + 1536;         // <= 128 leaves + 127 nodes
+  const double B2 = (double)bcount[(size_t)par * nchrom + chrom];
+  const int4 my_node = tid < nnodes ? nodes[tid] : make_int4(0, 0, -1, 0);
+  // replica sums, four words per 16-B load, every load of a round in flight; 2D words become
+  // proportions (LPl holds p until the log pass), 1D words go to u1
+  constexpr int QJ = 1;   // 16-B rows per thread per round
+  for (int q0 = tid; q0 < nh / 4; q0 += QJ * SBLOCK) {
+    uint4 x[QJ][REPL];
+#pragma unroll
+    for (int j = 0; j < QJ; ++j)
+#pragma unroll
+      for (int r = 0; r < REPL; ++r) {
+        const int q = q0 + j * SBLOCK;
+        x[j][r] = q < nh / 4 ? *reinterpret_cast<const uint4*>(Rc + r * rs + 4 * q) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+    for (int j = 0; j < QJ; ++j) {
+      const int q = q0 + j * SBLOCK;
+      if (q >= nh / 4) continue;
+      uint32_t sm[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int r = 0; r < REPL; ++r) {
+        sm[0] += x[j][r].x; sm[1] += x[j][r].y; sm[2] += x[j][r].z; sm[3] += x[j][r].w;
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int k = 4 * q + c;
+        if (k < nb2) {
+          const double v = (double)sm[c];
+          LPl[k] = (B2 != 0.0) ? v / B2 : 0.0;
+          if (writer) T[k].v = v;
+        } else {
+          u1[k - nb2] = sm[c];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  STAMP(16);
+  // 1D spectra (wave 0: pop1, wave 1: pop2): fold_1d_sfs (:446-463), inner sums, proportions
+  if (wv < 2) {
+    const int np_ = wv ? n2p : n1p, n_ = wv ? n2 : n1, off = wv ? n1 + 1 : 0, t0 = wv ? t1b : t1a;
+    double f[2], sf = 0.0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = lane + WAVE * j;
+      f[j] = 0.0;
+      if (k <= np_) f[j] = (double)u1[off + k] + (k < np_ ? (double)u1[off + n_ - k] : 0.0);
+      if (k >= 1 && k <= np_ - 1) sf += f[j];
+    }
+    const double B1 = wave_sum_d(sf);
+    double* p1 = wv ? p1b : p1a;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = lane + WAVE * j;
+      if (k <= np_) {
+        const double p = (B1 != 0.0) ? f[j] / B1 : 0.0;
+        p1[k] = p;
+        LPl[t0 + k] = p;
+        if (writer) T[t0 + k].v = f[j];
+      }
+    }
+    if (lane == 0) sh_misc[1 + wv] = B1;
+  } else {
+    // 2D numpy pairwise leaves over p[1 : nb2-2], eight lanes per leaf
+    for (int g = (tid - 2 * WAVE) >> 3; g < nleaves; g += (SBLOCK - 2 * WAVE) / 8) {
+      const int r = tid & 7;
+      const int2 lf = leaves[g];
+      if (lf.y >= 8) {
+        const double* a = LPl + 1 + lf.x;
+        double x = a[r];
+        for (int i = 8 + r; i < lf.y - (lf.y % 8); i += 8) x += a[i];
+        acc8[g * 8 + r] = x;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < nleaves) {
+    const int2 lf = leaves[tid];
+    const double* a = LPl + 1 + lf.x;
+    const double* q = acc8 + tid * 8;
+    double res = 0.0;
+    if (lf.y < 8) {
+      for (int i = 0; i < lf.y; ++i) res += a[i];
+    } else {
+      res = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+      for (int i = lf.y - (lf.y % 8); i < lf.y; ++i) res += a[i];
+    }
+    lsum[tid] = res;
+  }
+  if (tid == 4 * WAVE && n1p >= 2) sh_misc[3] = 1.0 - np_leaf_sum(p1a + 1, n1p - 2);
+  if (tid == 5 * WAVE && n2p >= 2) sh_misc[4] = 1.0 - np_leaf_sum(p1b + 1, n2p - 2);
+  __syncthreads();
+  STAMP(17);
+  // numpy's tree over the leaves, one level of equal-height nodes at a time (lsum holds the
+  // leaves, then the nodes; children always precede parents)
+  for (int l = 0; l < nlevels; ++l) {
+    if (my_node.z == l) lsum[nleaves + tid] = lsum[my_node.x] + lsum[my_node.y];
+    __syncthreads();
+  }
+  STAMP(18);
+  if (tid == 0) {
+    const double S = (nleaves + nnodes) ? lsum[nleaves + nnodes - 1] : 0.0;
+    const double B1a = sh_misc[1], B1b = sh_misc[2];
+    uint32_t flags = 0;
+    if (B2 == 0.0) flags |= BGF_B2_ZERO;
+    if (B1a == 0.0) flags |= BGF_B1A_ZERO;
+    if (B1b == 0.0) flags |= BGF_B1B_ZERO;
+    // bit 8/9/10: replace the last inner lp of 2D / pop1 / pop2 with log(padj)
+    const double pa[3] = {1.0 - S, sh_misc[3], sh_misc[4]};
+    const bool on[3] = {nb2 - 2 >= 1 && B2 != 0.0, n1p - 1 >= 1 && B1a != 0.0, n2p - 1 >= 1 && B1b != 0.0};
+    const uint32_t nanf[3] = {BGF_NAN2, BGF_NAN1A, BGF_NAN1B};
+    for (int q = 0; q < 3; ++q) {
+      if (!on[q]) continue;
+      if (pa[q] < -1e-15) flags |= nanf[q];
+      else if (fabs(pa[q]) > 1e-15) flags |= 256u << q;
+    }
+    sh_misc[0] = 1.0 - S;
+    sh_flags = flags;
+  }
+  __syncthreads();
+  const uint32_t flags = sh_flags;
+  const int kl[3] = {nb2 - 2, t1a + n1p - 1, t1b + n2p - 1};
+  const double pad[3] = {sh_misc[0], sh_misc[3], sh_misc[4]};
+  // logs, LG independent ones per thread per round
+  constexpr int LG = 2;
+  for (int k0 = tid; k0 < nt; k0 += LG * SBLOCK) {
+    double pv[LG], lv[LG];
+#pragma unroll
+    for (int j = 0; j < LG; ++j) {
+      const int k = k0 + j * SBLOCK;
+      pv[j] = k < nt ? LPl[k] : 1.0;
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        if (k == kl[q] && (flags & (256u << q))) pv[j] = pad[q];
+    }
+#pragma unroll
+    for (int j = 0; j < LG; ++j) lv[j] = log(pv[j]);
+#pragma unroll
+    for (int j = 0; j < LG; ++j) {
+      const int k = k0 + j * SBLOCK;
+      if (k < nt) {
+        LPl[k] = lv[j];
+        if (writer) { T[k].lp = lv[j]; LP[k] = lv[j]; }
+      }
+    }
+  }
+  hb.B2 = B2; hb.B1a = sh_misc[1]; hb.B1b = sh_misc[2]; hb.flags = flags & 0xffu; hb.pad = 0;
+  if (writer && tid == 0) head[bg] = hb;
+  if (tid == 0) *hb_out = hb;
+  __syncthreads();   // scratch reads done before the histogram area is zeroed
+}
+
+// K3 for small grids.  Workgroup LDS: [lp table of the chunk's background (nt doubles, rounded up
+// to even) | D | F | per wave: 2D bins (u16-packed when P16) | R1 x folded pop1 1D | R1 x pop2 1D |
+// 64 trash words].
+// FUSED (per-chromosome backgrounds): the workgroup builds its chromosome's table in the prologue
+// from this run's k_prep replicas (the k_bg_slice computation, in the histogram area as scratch),
+// clears its share of the other parity's replicas for the next run, and the first workgroup of a
+// chromosome also writes the global tables (k_scan_extra and callers read them).  Otherwise the
+// table comes from k_bg_finalize's output.
 // Per window (one wavefront): pass over its bins (first 512 prefetched with the previous window):
-// ballots give every count, the 2D atomic returns the SNP's rank r in its bin and the SNP adds
-// D(r) - lp_k; the 1D atomics land in lane-&3 replicas; then one lane per 1D bin adds
-// x ln x - x lp; the touched 2D words are cleared; three DPP sums; one record.
-template <bool P16>
-__global__ __launch_bounds__(SBLOCK) void k_scan_w(KParams P, const uint32_t* __restrict__ bins,
+// per-lane counters give every count, the 2D atomic returns the SNP's rank r in its bin and the
+// SNP adds D(r) - lp_k; the 1D atomics land in lane-&3 replicas; then one lane per 1D bin adds
+// x ln x - x lp; the touched 2D words are cleared; DPP sums; one record.
+template <bool P16, bool FUSED>
+__global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 4 : 1))) void k_scan_w(KParams P, const uint32_t* __restrict__ bins,
                                                    const Chunk* __restrict__ chunks, uint2* __restrict__ slots,
-                                                   const PL* __restrict__ tab, const double* __restrict__ LPg,
-                                                   const BgHead* __restrict__ head, int bg_per_chrom,
+                                                   PL* __restrict__ tab, double* __restrict__ LPg,
+                                                   BgHead* __restrict__ head, int bg_per_chrom,
                                                    const double* __restrict__ lnx, const double* __restrict__ dfg,
                                                    sfs2d_window* __restrict__ out, uint32_t* __restrict__ err_word,
-                                                   int mode_bp) {
+                                                   int mode_bp, uint32_t* __restrict__ repl,
+                                                   uint32_t* __restrict__ bcount, int par,
+                                                   const int2* __restrict__ leaves, int nleaves,
+                                                   const int4* __restrict__ nodes, int nnodes, int nlevels) {
   extern __shared__ double ldsd[];
+  __shared__ BgHead sh_hb;
   STAMP(10);
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & (WAVE - 1);
+  const int tid = threadIdx.x;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & (WAVE - 1);
   const Chunk ch = chunks[blockIdx.x];
   const int bg = bg_per_chrom ? (int)ch.chrom : 0;
-  const PL* T = tab + (size_t)bg * P.nt;
-  const double* LP = LPg + (size_t)bg * P.nt;
-  const BgHead hb = head[bg];
 
-  double* LPl = ldsd;                 // nb2 (rounded up to even: the histograms are 16-B aligned)
-  double* Dt = LPl + ((P.nb2 + 1) & ~1);   // LNT
-  double* Ft = Dt + LNT;              // LNT
+  double* LPl = ldsd;                            // nt (rounded up to even: the histograms are 16-B aligned)
+  double* Dt = LPl + ((P.nt + 1) & ~1);          // LNT
+  double* Ft = Dt + LNT;                         // LNT
+  uint32_t* HB = reinterpret_cast<uint32_t*>(Ft + LNT);
   const int h2w = P16 ? ((P.nb2 + 1) / 2 + 3) & ~3 : (P.nb2 + 3) & ~3;
   const int h1w = R1 * (P.n1p + 1), h1wb = R1 * (P.n2p + 1);
   const int per = h2w + h1w + h1wb + TRASH;
-  uint32_t* W = reinterpret_cast<uint32_t*>(Ft + LNT) + wv * per;
+  uint32_t* W = HB + wv * per;
   uint32_t* H1a = W + h2w;
   uint32_t* H1b = H1a + h1w;
   const uint32_t trash = (uint32_t)(h2w + h1w + h1wb + lane);   // word offset from W
   const uint32_t rep = lane & (R1 - 1);
 
-  for (int k = threadIdx.x; k < P.nb2; k += SBLOCK) LPl[k] = LP[k];
-  for (int k = threadIdx.x; k < 2 * LNT; k += SBLOCK) Dt[k] = dfg[k];
-  for (int k = lane; k < per; k += WAVE) W[k] = 0u;
-  // lp of the 1D bins owned by this lane in the per-bin pass (bins 1+lane, 65+lane)
-  double lpa[2], lpb[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int k = 1 + lane + WAVE * j;
-    lpa[j] = k <= P.n1p - 1 ? LP[P.t1a + k] : 0.0;
-    lpb[j] = k <= P.n2p - 1 ? LP[P.t1b + k] : 0.0;
-  }
-  const bool filt = P.ann_want >= 0;
-  const uint32_t zflags = bg_zero_flags(hb);
-  const bool nan2 = hb.flags & BGF_NAN2, nan1a = hb.flags & BGF_NAN1A, nan1b = hb.flags & BGF_NAN1B;
-
+  // the first window's slot record is fetched before the table work
   auto bounds = [&](uint32_t s, uint2 sr, Win& w) {
     if (mode_bp) {
       w.has = sr.x != 0u;
@@ -943,13 +1172,40 @@ __global__ __launch_bounds__(SBLOCK) void k_scan_w(KParams P, const uint32_t* __
       w.v1 = ld4(bins, i0 + 4 * WAVE, w.e);
     }
   };
-
   uint32_t s = ch.slot_lo + wv;
-  Win cur;
-  cur.has = false;
-  if (s < ch.slot_hi) bounds(s, mode_bp ? slots[s] : make_uint2(0, 0), cur);
+  const bool active = s < ch.slot_hi;
+  const uint2 sr0 = (active && mode_bp) ? slots[s] : make_uint2(0, 0);   // in flight during the table work
+
+  for (int k = tid; k < 2 * LNT; k += SBLOCK) Dt[k] = dfg[k];
+  BgHead hb;
+  const size_t rs = (size_t)P.nchrom * P.nh;     // replica stride
+  const uint32_t* Rc = repl + (size_t)par * REPL * rs + (size_t)ch.chrom * P.nh;
+  if (!FUSED) {
+    const double* LP = LPg + (size_t)bg * P.nt;
+    for (int k = tid; k < P.nt; k += SBLOCK) LPl[k] = LP[k];
+    hb = head[bg];
+  } else {
+    fused_table(P.nb2, P.nh, P.nt, P.n1p, P.n2p, P.n1, P.n2, P.t1a, P.t1b, P.nchrom, ch.chrom, ch.wid_lo == 0, bg,
+                Rc, rs, repl, bcount, par, tab, LPg, head, LPl, HB, leaves, nleaves, nodes, nnodes, nlevels, &sh_hb);
+    hb = sh_hb;
+  }
+  for (int k = lane; k < per / 4; k += WAVE) reinterpret_cast<uint4*>(W)[k] = make_uint4(0, 0, 0, 0);
+  // lp of the 1D bins owned by this lane in the per-bin pass (bins 1+lane, 65+lane)
   __syncthreads();
-  if (s >= ch.slot_hi) return;
+  double lpa[2], lpb[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int k = 1 + lane + WAVE * j;
+    lpa[j] = k <= P.n1p - 1 ? LPl[P.t1a + k] : 0.0;
+    lpb[j] = k <= P.n2p - 1 ? LPl[P.t1b + k] : 0.0;
+  }
+  const bool filt = P.ann_want >= 0;
+  const uint32_t zflags = bg_zero_flags(hb);
+  const bool nan2 = hb.flags & BGF_NAN2, nan1a = hb.flags & BGF_NAN1A, nan1b = hb.flags & BGF_NAN1B;
+
+  if (!active) return;
+  Win cur;
+  bounds(s, sr0, cur);
   STAMP(11);
   int it = 0;
   for (; s < ch.slot_hi; s += SBLOCK / WAVE, ++it) {
@@ -1073,7 +1329,13 @@ __global__ __launch_bounds__(SBLOCK) void k_scan_w(KParams P, const uint32_t* __
         suspect_zero(w.t1b, n1b)) {
       // rare: exact re-evaluation with the bin-by-bin proportionality test (histograms are clean)
       group_sync<WAVE>();
-      w = eval_exact<WAVE, P16, R1>(P, bins, cur.b, cur.e, T, hb, lnx, W, H1a, H1b, nullptr, nullptr);
+      if (FUSED)
+        w = eval_exact<WAVE, P16, R1>(P, bins, cur.b, cur.e,
+                                      TabFused{LPl, Rc, rs, P.nb2, P.n1, P.n2, P.n1p, P.h1a, P.h1b, P.t1a, P.t1b}, hb,
+                                      lnx, W, H1a, H1b, nullptr, nullptr);
+      else
+        w = eval_exact<WAVE, P16, R1>(P, bins, cur.b, cur.e, TabGlobal{tab + (size_t)bg * P.nt}, hb, lnx, W, H1a,
+                                      H1b, nullptr, nullptr);
       if (lane == 0) atomicAdd(err_word + 1, 1u);   // statistics: windows that took the exact path
     } else {
       if (nan2) w.t2d = __builtin_nan("");
@@ -1128,7 +1390,7 @@ __global__ __launch_bounds__(BLOCK) void k_scan_g(KParams P, const uint32_t* __r
       b = ch.cb + wid * P.ws;
       e = b + P.ws;
     }
-    const WinOut w = eval_exact<BLOCK, P16, 1>(P, bins, b, e, T, hb, lnx, H2, H1a, H1b, redd, redu);
+    const WinOut w = eval_exact<BLOCK, P16, 1>(P, bins, b, e, TabGlobal{T}, hb, lnx, H2, H1a, H1b, redd, redu);
     if (threadIdx.x == 0) {
       write_rec(out + s, ch.chrom, wid, b, e, w, bg_zero_flags(hb));
       if (mode_bp) slots[s] = make_uint2(0u, 0u);
@@ -1182,7 +1444,7 @@ __global__ __launch_bounds__(WAVE) void k_scan_extra(KParams P, const uint32_t* 
     while (c2 > 0 && chrom_off[c2] >= (long long)pe) --c2;
     pc = (uint32_t)c2;
     pb = window_begin_back(pos, chrom_off[c2], pe, P.ws);
-    w = eval_exact<WAVE, P16, 1>(P, bins, pb, pe, T, hb, lnx, H2, H1a, H1b, nullptr, nullptr);
+    w = eval_exact<WAVE, P16, 1>(P, bins, pb, pe, TabGlobal{T}, hb, lnx, H2, H1a, H1b, nullptr, nullptr);
   } else {
     flags |= SFS2D_W_EMPTY;
   }

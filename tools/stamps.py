@@ -28,4 +28,6 @@ print(which, "K1 blk0: zero %.2f  loop %.2f  flush %.2f us" % (d(20, 21), d(21, 
 print(which, "K2 slice0: repl+p/lp %.2f  leaves %.2f us; tail block: %.2f us" % (d(0, 1), d(1, 2), d(3, 4)))
 print(which, "K3 blk0: prologue %.2f  2D pass(1st) %.2f  1D+clear %.2f  reduce+store %.2f  rest %.2f us" % (
     d(10, 11), d(11, 12), d(12, 13), d(13, 14), d(14, 15)))
+print(which, "K3 fused prologue: replicas %.2f  1D+leaves %.2f  tree %.2f  logs %.2f  zero %.2f us" % (
+    d(10, 16), d(16, 17), d(17, 18), d(18, 19), d(19, 11)))
 print(which, "gaps: K1end->K2start %.2f  K2end->K3start %.2f us" % (d(23, 0), d(4, 10)))
