@@ -150,8 +150,10 @@ struct sfs2d_plan {
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   // live timing ring: events around each kernel of every run while timing is on
   bool timing = false;
-  std::vector<hipEvent_t> tev;   // 4 per run
+  std::vector<hipEvent_t> tev;   // 4 per sampled run
   int tcount = 0;
+  int tevery = 1;                // sample every tevery-th run
+  int64_t tseen = 0;             // runs since timing was set
 };
 
 namespace {
@@ -681,7 +683,8 @@ int sfs2d_plan_run_phase(sfs2d_plan* pl, int phase, sfs2d_window* out_dev) {
   sfs2d_ctx* ctx = pl->ctx;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   hipEvent_t* te = nullptr;
-  if (pl->timing && phase == 0 && pl->tcount * 4 < (int)pl->tev.size()) te = &pl->tev[(size_t)pl->tcount * 4];
+  if (pl->timing && phase == 0 && (pl->tseen++ % pl->tevery) == 0 && pl->tcount * 4 < (int)pl->tev.size())
+    te = &pl->tev[(size_t)pl->tcount * 4];
   if (!pl->do_bg && !pl->bg_ready && phase != 1)
     return set_err(ctx, SFS2D_E_ARG, "supplied-background plan run before sfs2d_plan_set_background");
   if (te) HIPCHK(ctx, hipEventRecord(te[0], ctx->stream));
@@ -704,8 +707,12 @@ int sfs2d_plan_run_phase(sfs2d_plan* pl, int phase, sfs2d_window* out_dev) {
   return 0;
 }
 
-int sfs2d_plan_set_timing(sfs2d_plan* pl, int max_runs) {
-  if (!pl || max_runs < 0) return SFS2D_E_ARG;
+int sfs2d_plan_set_timing(sfs2d_plan* pl, int max_runs) { return sfs2d_plan_set_timing_sampled(pl, max_runs, 1); }
+
+int sfs2d_plan_set_timing_sampled(sfs2d_plan* pl, int max_runs, int every) {
+  if (!pl || max_runs < 0 || every < 1) return SFS2D_E_ARG;
+  pl->tevery = every;
+  pl->tseen = 0;
   sfs2d_ctx* ctx = pl->ctx;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   for (auto& e : pl->tev) if (e) hipEventDestroy(e);
@@ -738,6 +745,15 @@ int sfs2d_plan_timing_read(sfs2d_plan* pl, int* nruns, double* ms_k1, double* ms
 }
 
 int sfs2d_plan_run(sfs2d_plan* pl, sfs2d_window* out_dev) { return sfs2d_plan_run_phase(pl, 0, out_dev); }
+
+int sfs2d_plan_run_many(sfs2d_plan* pl, int nruns, sfs2d_window* out_dev) {
+  if (!pl || nruns < 0) return SFS2D_E_ARG;
+  for (int i = 0; i < nruns; ++i) {
+    const int rc = sfs2d_plan_run_phase(pl, 0, out_dev);
+    if (rc) return rc;
+  }
+  return 0;
+}
 
 int sfs2d_plan_bg_buffer(sfs2d_plan* pl, void** dev_ptr, int64_t* nbytes) {
   if (!pl || !dev_ptr || !nbytes) return SFS2D_E_ARG;

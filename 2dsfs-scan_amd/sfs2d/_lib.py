@@ -27,7 +27,7 @@ W_EXTRA = 0x40000000
 EXPORTS = [
     "sfs2d_abi_version", "sfs2d_ctx_create", "sfs2d_ctx_destroy", "sfs2d_last_error", "sfs2d_ctx_set_stream",
     "sfs2d_data_upload", "sfs2d_data_wrap_device", "sfs2d_data_free", "sfs2d_bg_hist", "sfs2d_plan_create",
-    "sfs2d_plan_num_records", "sfs2d_plan_set_background", "sfs2d_plan_run", "sfs2d_plan_read",
+    "sfs2d_plan_num_records", "sfs2d_plan_set_background", "sfs2d_plan_run", "sfs2d_plan_run_many", "sfs2d_plan_set_timing_sampled", "sfs2d_plan_read",
     "sfs2d_plan_bg_buffer", "sfs2d_plan_run_phase", "sfs2d_plan_check", "sfs2d_plan_time",
     "sfs2d_plan_destroy", "sfs2d_scan", "sfs2d_plan_set_timing", "sfs2d_plan_timing_read",
     "sfs2d_plan_stats",
@@ -83,6 +83,8 @@ def lib():
     L.sfs2d_plan_num_records.restype = i64
     L.sfs2d_plan_set_background.argtypes = [vp, vp, vp, vp]
     L.sfs2d_plan_run.argtypes = [vp, vp]
+    L.sfs2d_plan_run_many.argtypes = [vp, C.c_int, vp]
+    L.sfs2d_plan_set_timing_sampled.argtypes = [vp, C.c_int, C.c_int]
     L.sfs2d_plan_run_phase.argtypes = [vp, C.c_int, vp]
     L.sfs2d_plan_read.argtypes = [vp, vp, i64, C.POINTER(i64)]
     L.sfs2d_plan_bg_buffer.argtypes = [vp, C.POINTER(vp), C.POINTER(i64)]

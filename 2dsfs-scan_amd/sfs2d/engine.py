@@ -158,6 +158,11 @@ class Plan:
         self.eng.check(self.eng.lib.sfs2d_plan_run_phase(self.h, phase,
                                                          C.c_void_p(out_dev_ptr) if out_dev_ptr else None))
 
+    def run_many(self, nruns: int, out_dev_ptr: Optional[int] = None):
+        """Enqueue `nruns` back-to-back runs from C (no Python between runs)."""
+        self.eng.check(self.eng.lib.sfs2d_plan_run_many(self.h, int(nruns),
+                                                        C.c_void_p(out_dev_ptr) if out_dev_ptr else None))
+
     def check(self):
         self.eng.check(self.eng.lib.sfs2d_plan_check(self.h))
 
@@ -183,8 +188,9 @@ class Plan:
         self.eng.check(self.eng.lib.sfs2d_plan_stats(self.h, C.byref(v)))
         return int(v.value)
 
-    def set_timing(self, max_runs: int):
-        self.eng.check(self.eng.lib.sfs2d_plan_set_timing(self.h, int(max_runs)))
+    def set_timing(self, max_runs: int, every: int = 1):
+        """Record HIP events around each kernel of every `every`-th following run (<= max_runs samples)."""
+        self.eng.check(self.eng.lib.sfs2d_plan_set_timing_sampled(self.h, int(max_runs), int(every)))
 
     def timing_read(self):
         n = C.c_int()

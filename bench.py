@@ -35,29 +35,28 @@ WS = 20000
 
 
 def algorithmic_bytes(n_snp, n_slots, n_win, which):
-    """scan pass reads the packed counts (4 B/SNP) + slot table (8 B/slot) and writes one
-    64-B record per slot; the bg/segmentation pass reads counts + positions (8 B/SNP)."""
+    """Bytes each kernel must move (DESIGN.md "Kernels"): k_prep reads counts + positions (8 B/SNP),
+    writes the packed bins (4 B/SNP) and the window slot table (8 B/window); k_scan_w reads the bins
+    (4 B/SNP) and the slot table (8 B/slot) and writes one 64-B record per slot."""
     if which == "k3":
         return 4 * n_snp + 8 * n_slots + 64 * n_slots
     if which == "k1":
-        return 8 * n_snp + 8 * n_win
-    return 12 * n_snp + 72 * n_slots
+        return 12 * n_snp + 8 * n_win
+    return 16 * n_snp + 8 * n_win + 72 * n_slots
 
 
-def cpu_baseline(p, budget_s=12.0):
-    """Oracle (numpy/scipy restatement of the reference's dense algorithm) on a bounded prefix."""
+def cpu_baseline(p):
+    """Oracle (numpy/scipy restatement of the reference's dense per-window algorithm, test
+    infrastructure only) over the whole rank-0 config-2 stream, one host core."""
     from oracle import sfs_oracle as O
-    from sfs2d.pack import PackedSNPs
-    n = 60000
-    q = PackedSNPs(p.counts[:n], p.pos[:n], np.array([0, n]), ["chr0000"], p.ann_id[:n], p.ann_names, p.pop1, p.pop2)
     cfg = O.Cfg(POP, POP)
     t0 = time.perf_counter()
-    res = O.combined_scan(q, WS, cfg)
+    res = O.combined_scan(p, WS, cfg)
     dt = time.perf_counter() - t0
     return {"value": len(res) / dt, "unit": "windows/s", "cores": 1, "kind": "port",
-            "sample": f"first {n} SNPs of the rank-0 config-2 stream ({len(res)} windows, {dt:.1f} s), "
-                      "oracle/sfs_oracle.combined_scan: dense per-window grids + scipy multinomial.logpmf "
-                      "exactly as the reference, single thread"}
+            "sample": f"the full rank-0 config-2 stream ({p.n} SNPs, {len(res)} windows, {dt:.1f} s): "
+                      "oracle/sfs_oracle.combined_scan, dense per-window grids + scipy multinomial.logpmf "
+                      "as the reference computes them, single thread"}
 
 
 def hbm_stream_roofline(eng, steps=5):
@@ -69,9 +68,8 @@ def hbm_stream_roofline(eng, steps=5):
     pl = eng.plan(dev, ScanConfig(n1p=POP, n2p=POP, window=WS))
     pl.run()
     pl.check()
-    pl.set_timing(steps)
-    for _ in range(steps):
-        pl.run()
+    pl.set_timing(steps, every=2)
+    pl.run_many(2 * steps)
     nr, (k1, k2, k3) = pl.timing_read()
     recs = pl.read()
     nwin = int(((recs["flags"] & 0x80000000) == 0).sum())
@@ -91,8 +89,8 @@ def hbm_stream_roofline(eng, steps=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-hbm-stream", action="store_true")
     args = ap.parse_args()
@@ -138,13 +136,18 @@ def main():
     pl.check()
     for _ in range(args.warmup):
         step()
-    pl.set_timing(args.steps)
+    # HIP events around each kernel of every 8th timed run, on the stream the kernels run on (sampled:
+    # an event pair costs several microseconds of queue time, 1/8 of it is ~1 us per step)
+    pl.set_timing(args.steps, every=8)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    if world == 1:
+        pl.run_many(args.steps, out.data_ptr())   # enqueued from C: no host work between steps
+    else:
+        for _ in range(args.steps):
+            step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -164,7 +167,7 @@ def main():
         b3 = algorithmic_bytes(p.n, nrec, nwin_rank, "k3")
         achieved = b3 / (k3 * 1e-3) / 1e9
         line = {
-            "metric": "genomic windows/s (T2D+T1D_p1+T1D_p2) at 20 kb windows, n1=n2=50",
+            "metric": "genomic windows/s (T2D+T1D_p1+T1D_p2; Fst not computed yet) at 20 kb, n1=n2=50",
             "value": value, "unit": "windows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic (SURVEY 8d generator, seed 12345+rank)",
@@ -172,11 +175,13 @@ def main():
                                    "n1=n2=50 haploid (pop_size 25/25), per-chromosome background",
                        "snps_per_gpu": p.n, "windows_per_gpu": nwin_rank, "window_bp": WS,
                        "parallelism": f"windows sharded by chromosome over {world} GPU(s); RCCL all-gather"},
-            "kernels_ms": {"k1_bg_seg": k1, "k2_bg_finalize": k2, "k3_scan": k3, "timed_runs": nr,
+            "kernels_ms": {"k_prep": k1, "k_bg_slice_or_gap": k2, "k_scan_w": k3, "timed_runs": nr,
                            "exact_path_windows": pl.stats()},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "note": "k_scan, algorithmic bytes 4 B/SNP + 72 B/slot; 8 MB input is MALL-resident"},
+                         "kernel": "k_scan_w", "ms": k3,
+                         "note": "k_scan_w, algorithmic bytes 4 B/SNP + 72 B/slot per launch over its event-timed "
+                                 "duration; the 8 MB config-2 stream is MALL-resident (see roofline_hbm)"},
         }
         if not args.no_hbm_stream and world == 1:
             line["roofline_hbm"] = hbm_stream_roofline(eng)

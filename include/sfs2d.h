@@ -127,6 +127,8 @@ int64_t sfs2d_plan_num_records(const sfs2d_plan* plan);
 int sfs2d_plan_set_background(sfs2d_plan* plan, const double* bg2d, const double* bg1a, const double* bg1b);
 /* enqueue the scan; out_dev: device buffer of sfs2d_plan_num_records records (NULL = plan-owned) */
 int sfs2d_plan_run(sfs2d_plan* plan, sfs2d_window* out_dev);
+/* enqueue `nruns` back-to-back runs (no host work in between; benchmarks and batch replays) */
+int sfs2d_plan_run_many(sfs2d_plan* plan, int nruns, sfs2d_window* out_dev);
 /* copy the last run's records to host (synchronises the stream) */
 int sfs2d_plan_read(sfs2d_plan* plan, sfs2d_window* out_host, int64_t cap, int64_t* nrec_out);
 /* device pointers of the plan's per-chromosome background histogram replicas (uint32), for a
@@ -137,10 +139,14 @@ int sfs2d_plan_run_phase(sfs2d_plan* plan, int phase, sfs2d_window* out_dev);
 int sfs2d_plan_stats(sfs2d_plan* plan, uint32_t* exact_windows);
 /* last run's error word (0 = ok, else SFS2D_E_KEY / SFS2D_E_GRID); synchronises */
 int sfs2d_plan_check(sfs2d_plan* plan);
-/* live timing: record HIP events around each kernel of the next `max_runs` sfs2d_plan_run calls
- * (0 = off), then read the average device time per kernel (k1 = bg+segmentation, k2 = background
- * tables, k3 = window scan) over those runs (synchronises). */
-int sfs2d_plan_set_timing(sfs2d_plan* plan, int max_runs);
+/* live timing: record HIP events around each kernel of every `every`-th of the following runs,
+ * for up to `max_samples` runs (sampling keeps the events' own cost out of the other runs);
+ * sfs2d_plan_timing_read averages the sampled runs' per-kernel durations */
+int sfs2d_plan_set_timing(sfs2d_plan* plan, int max_runs);   /* = sampled(plan, max_runs, 1) */
+int sfs2d_plan_set_timing_sampled(sfs2d_plan* plan, int max_samples, int every);
+/* average device time per kernel over the sampled runs (synchronises): k1 = k_prep, k2 = background
+ * tables (k_bg_slice; for plans whose scan kernel builds the tables itself, the gap between the two
+ * kernels), k3 = the window scan (+ the final-window helper when SFS2D_F_PREV_EXTRA is set) */
 int sfs2d_plan_timing_read(sfs2d_plan* plan, int* nruns, double* ms_k1, double* ms_k2, double* ms_k3);
 /* standalone timing loop: average device time per kernel over `iters` runs */
 int sfs2d_plan_time(sfs2d_plan* plan, int iters, double* ms_per_run, double* ms_k1, double* ms_k2, double* ms_k3);
