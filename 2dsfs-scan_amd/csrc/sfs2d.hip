@@ -195,7 +195,8 @@ void launch_scan_w(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
   hipLaunchKernelGGL((k_scan_w<P16, FUSED>), dim3((unsigned)pl->chunks.size()), dim3(SBLOCK), pl->scan_lds,
                      pl->ctx->stream, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
                      per_chrom, pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, bp, pl->d_repl, pl->d_bcount,
-                     plan_par(pl), pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels);
+                     plan_par(pl), pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels,
+                     pl->extra_rec >= 0 ? (int)pl->last_chrom : -1);
 }
 
 template <bool P16>
@@ -212,15 +213,21 @@ hipError_t launch_scan(sfs2d_plan* pl, sfs2d_window* out) {
   return hipGetLastError();
 }
 
-template <bool B, bool S, bool L, bool N>
-hipError_t launch_prep1(sfs2d_plan* pl) {
+template <bool B, bool S, bool L, bool N, bool F>
+hipError_t launch_prep2(sfs2d_plan* pl) {
   const sfs2d_data* d = pl->data;
   const int par = plan_par(pl);
-  hipLaunchKernelGGL((k_prep<B, S, L, N>), dim3((unsigned)pl->tiles.size()), dim3(BLOCK1), (B && L) ? pl->bg_lds : 0,
+  hipLaunchKernelGGL((k_prep<B, S, L, N, F>), dim3((unsigned)pl->tiles.size()), dim3(BLOCK1), (B && L) ? pl->bg_lds : 0,
                      pl->ctx->stream, pl->K, d->counts, d->pos, d->ann, pl->d_tiles,
                      pl->d_repl + (size_t)par * REPL * pl->K.nchrom * pl->K.nh, pl->d_slots, pl->d_bins,
                      pl->d_bcount + (size_t)par * pl->K.nchrom, pl->d_err, L ? pl->hr : 1);
   return hipGetLastError();
+}
+
+template <bool B, bool S, bool L, bool N>
+hipError_t launch_prep1(sfs2d_plan* pl) {
+  const bool f = pl->K.ann_want >= 0 || pl->K.has_start || pl->K.has_end;
+  return f ? launch_prep2<B, S, L, N, true>(pl) : launch_prep2<B, S, L, N, false>(pl);
 }
 
 hipError_t launch_prep(sfs2d_plan* pl, bool bins) {
@@ -434,6 +441,7 @@ static int make_kparams(sfs2d_ctx* ctx, const sfs2d_params* prm, int nchrom, KPa
   K->h1a = K->nb2; K->h1b = K->nb2 + K->n1 + 1; K->nh = (K->h1b + K->n2 + 1 + 3) & ~3;   // 16-B rows
   K->t1a = K->nb2; K->t1b = K->nb2 + K->n1p + 1; K->nt = K->t1b + K->n2p + 1;
   K->fold = prm->fold ? 1 : 0;
+  K->fold_thr = prm->fold ? K->n1p + K->n2p : 0x7fffffff;
   K->ann_want = prm->ann_want;
   K->has_start = prm->has_start ? 1 : 0; K->has_end = prm->has_end ? 1 : 0;
   K->start_pos = prm->start_pos; K->end_pos = prm->end_pos;
@@ -513,7 +521,7 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
       // fused prologue's scratch: u1 words, 1D proportions, leaf accumulators and sums)
       const int h2w = pl->p16 ? (((K.nb2 + 1) / 2 + 3) & ~3) : ((K.nb2 + 3) & ~3);
       const int per = h2w + R1 * (K.n1p + 1) + R1 * (K.n2p + 1) + TRASH;
-      const size_t hist_words = std::max<size_t>((size_t)(SBLOCK / WAVE) * per, 2 * (1536 + 256) + 16);
+      const size_t hist_words = std::max<size_t>((size_t)(SBLOCK / WAVE) * per, (size_t)FUSED_VCNT + K.nt + 16);
       pl->scan_lds = sizeof(double) * (size_t)(((K.nt + 1) & ~1) + 2 * LNT) + hist_words * 4;
     } else {
       pl->scan_lds = (size_t)(core + TRASH + 2) * 4 + 32 * 8 + 32 * 8;
@@ -583,11 +591,13 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
       }
   }
   pl->hr = (size_t)K.nh * 4 * 4 <= 64 * 1024 ? 4 : 1;
-  pl->bg_lds = (size_t)K.nh * 4 * pl->hr;
+  pl->bg_lds = ((size_t)K.nh * pl->hr + WAVE) * 4;   // + 64 lane trash words
   pl->lds_hist = pl->bg_lds <= 150 * 1024;
   if (pl->lds_hist && pl->bg_lds > 64 * 1024) {
-    hipFuncSetAttribute((const void*)k_prep<true, true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->bg_lds);
-    hipFuncSetAttribute((const void*)k_prep<true, false, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->bg_lds);
+    hipFuncSetAttribute((const void*)k_prep<true, true, true, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->bg_lds);
+    hipFuncSetAttribute((const void*)k_prep<true, false, true, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->bg_lds);
+    hipFuncSetAttribute((const void*)k_prep<true, true, true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->bg_lds);
+    hipFuncSetAttribute((const void*)k_prep<true, false, true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->bg_lds);
   }
   hipFuncSetAttribute((const void*)k_bg_finalize, hipFuncAttributeMaxDynamicSharedMemorySize,
                       (int)(sizeof(double) * FIN_LDS_BINS));
@@ -861,7 +871,7 @@ int sfs2d_bg_hist(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* pr
   sfs2d_plan pl;
   pl.ctx = ctx; pl.data = data; pl.prm = *prm; pl.K = K; pl.K.nchrom = 1;
   pl.do_bg = true; pl.do_seg = false;
-  pl.bg_lds = (size_t)K.nh * 4;
+  pl.bg_lds = ((size_t)K.nh + WAVE) * 4;
   pl.lds_hist = pl.bg_lds <= 150 * 1024;
   const int c0 = chrom < 0 ? 0 : chrom, c1 = chrom < 0 ? data->nchrom : chrom + 1;
   const int64_t T = 16384;
@@ -885,7 +895,8 @@ int sfs2d_bg_hist(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* pr
     if (e == hipSuccess) e = hipMemsetAsync(pl.d_err, 0, 4, ctx->stream);
     if (e == hipSuccess) e = hipMemsetAsync(pl.d_bcount, 0, 4, ctx->stream);
     if (e == hipSuccess && pl.lds_hist && pl.bg_lds > 64 * 1024)
-      hipFuncSetAttribute((const void*)k_prep<true, false, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.bg_lds);
+      hipFuncSetAttribute((const void*)k_prep<true, false, true, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.bg_lds),
+      hipFuncSetAttribute((const void*)k_prep<true, false, true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.bg_lds);
     if (e == hipSuccess) e = launch_prep(&pl, false);
     if (e == hipSuccess) e = hipMemcpyAsync(hist.data(), pl.d_repl, sizeof(uint32_t) * REPL * K.nh, hipMemcpyDeviceToHost, ctx->stream);
     uint32_t err = 0;

@@ -54,12 +54,13 @@ constexpr int FBLOCK = 1024;      // k_bg_finalize workgroup
 constexpr int KBLOCK = 512;       // k_bg_slice workgroup
 constexpr int LNX_N = 1 << 20;    // ln(k) table for k < LNX_N (bin counts / window totals)
 constexpr int LNT = 512;          // D(r) and x ln x tables staged in LDS by k_scan_w
-constexpr int REPL = 8;           // replicas of the per-chromosome background histograms
+constexpr int REPL = 4;           // replicas of the per-chromosome background histograms
 constexpr int PW_MAX_LEAVES = 256;
 constexpr int LEAVES_PER_SLICE = 4;
 constexpr int FIN_LDS_BINS = 12288;  // backgrounds with nt <= this keep values / proportions in LDS
 constexpr int TRASH = WAVE;       // lane-private scratch words after each wave's histograms
 constexpr int R1 = 4;             // replicas of the folded 1D window histograms (lane & 3)
+constexpr int FUSED_VCNT = 2 * (1536 + 256) + 16;   // k_scan_w fused prologue: word offset of the counts
 
 enum : uint32_t { ERR_KEY = 1u, ERR_GRID = 2u };
 enum : uint32_t {
@@ -86,6 +87,7 @@ struct KParams {
   int ann_want;          // -1: no variant_type filter
   int has_start, has_end;
   long long start_pos, end_pos;
+  int fold_thr;          // joint fold when alt1 + alt2 > fold_thr (n1p + n2p; INT_MAX without folding)
   unsigned int ws;       // bp window size (fixed-bp) or SNPs per window
   unsigned int wmag;     // (p-1)/ws as a multiply-high: q = (t + ((n - t) >> wsh1)) >> wsh2, t = mulhi(n, wmag)
   int wsh1, wsh2;
@@ -143,9 +145,9 @@ __device__ __forceinline__ uint32_t wid_of(uint32_t p, uint32_t ws) { return p ?
 
 // the same window id with the division replaced by a multiply-high (host-side magic numbers)
 __device__ __forceinline__ uint32_t wid_fast(const KParams& P, uint32_t p) {
-  const uint32_t n = p - 1u;
+  const uint32_t n = p - min(p, 1u);   // p - 1, and 0 for p = 0 (wid_of(0) = 0), without a branch
   const uint32_t t = __umulhi(n, P.wmag);
-  return p ? (t + ((n - t) >> P.wsh1)) >> P.wsh2 : 0u;
+  return (t + ((n - t) >> P.wsh1)) >> P.wsh2;
 }
 
 __device__ __forceinline__ double lnx_of(const double* lnx, uint32_t x) {
@@ -254,7 +256,7 @@ __device__ __forceinline__ uint32_t classify(const KParams& P, uint32_t c, bool 
                                             int& k2all, int& u1a, int& u1b) {
   const int r1 = c & 0xff, a1 = (c >> 8) & 0xff, r2 = (c >> 16) & 0xff, a2 = c >> 24;
   const bool pass = var_ok & pos_ok;
-  const bool sw = P.fold & (a1 + a2 > P.n1p + P.n2p);
+  const bool sw = a1 + a2 > P.fold_thr;
   const int x1 = sw ? r1 : a1, x2 = sw ? r2 : a2;
   const bool nz = (x1 | x2) != 0;
   const bool oob = (x1 > P.n1) | (x2 > P.n2);
@@ -295,7 +297,7 @@ __global__ void k_init_lnx(double* lnx, double* dtab, double* ftab) {
 
 // ------------------------------------------------------------------------------------------ K1
 
-template <bool DO_BG, bool DO_SEG, bool LDS_HIST, bool DO_BINS>
+template <bool DO_BG, bool DO_SEG, bool LDS_HIST, bool DO_BINS, bool FILT>
 __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __restrict__ counts,
                                                  const uint32_t* __restrict__ pos, const uint16_t* __restrict__ ann,
                                                  const Tile* __restrict__ tiles, uint32_t* __restrict__ repl,
@@ -311,16 +313,19 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
   uint32_t* gh = repl + ((size_t)(blockIdx.x % REPL) * P.nchrom + t.chrom) * (size_t)P.nh;
   const int lane0 = threadIdx.x & (WAVE - 1);
   const int hsh = LDS_HIST ? (hr == 4 ? 2 : 0) : 0;
-  uint32_t* H = LDS_HIST ? sh_hist + (lane0 & (hr - 1)) : gh;
+  const int rep = lane0 & (hr - 1);
+  const int trash = P.nh * hr + lane0;   // LDS word after the histogram (64 of them)
   if (DO_BG) {
     if (LDS_HIST)
-      for (int k = threadIdx.x; k < P.nh * hr; k += BLOCK1) sh_hist[k] = 0u;
+      for (int k = threadIdx.x; k < P.nh * hr + WAVE; k += BLOCK1) sh_hist[k] = 0u;
     if (threadIdx.x == 0) sh_b2 = 0u;
     __syncthreads();
   }
-  const bool pos_filter = P.has_start || P.has_end;
+  // FILT: a position or variant_type filter is set (kept out of the common kernel: its uniform
+  // flags would otherwise occupy scalar registers throughout the loop)
+  const bool pos_filter = FILT && (P.has_start || P.has_end);
   const bool need_pos = DO_SEG || pos_filter;
-  const bool filt = P.ann_want >= 0;
+  const bool filt = FILT && P.ann_want >= 0;
   const int lane = threadIdx.x & (WAVE - 1);
   uint32_t err = 0, b2 = 0;
   STAMP(21);
@@ -337,6 +342,7 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
       for (int k = 0; k < 4; ++k) w[k] = wid_fast(P, pp[k]);
     }
     uint32_t bw[4];
+    uint32_t segcode = 0;   // bit 2k: SNP k opens a window, bit 2k+1: it closes one
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint32_t i = i0 + k;
@@ -349,21 +355,37 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
       }
       int k2all, u1a, u1b;
       bw[k] = classify(P, cc[k], var_ok, pos_ok, err, k2all, u1a, u1b);
-      if (DO_BG && in) {
-        if (k2all >= 0) atomicAdd(&H[k2all << hsh], 1u);
-        if (u1a >= 0) atomicAdd(&H[(P.h1a + u1a) << hsh], 1u);
-        if (u1b >= 0) atomicAdd(&H[(P.h1b + u1b) << hsh], 1u);
-        b2 += bin_k2(bw[k]) ? 1u : 0u;
+      if (DO_BG) {
+        if (LDS_HIST) {
+          // no branches: skipped SNPs add to the lane's trash word (keeps exec masks, and the
+          // scalar registers they take, out of the unrolled loop)
+          atomicAdd(&sh_hist[(in & (k2all >= 0)) ? (k2all << hsh) + rep : trash], 1u);
+          atomicAdd(&sh_hist[(in & (u1a >= 0)) ? ((P.h1a + u1a) << hsh) + rep : trash], 1u);
+          atomicAdd(&sh_hist[(in & (u1b >= 0)) ? ((P.h1b + u1b) << hsh) + rep : trash], 1u);
+        } else if (in) {
+          if (k2all >= 0) atomicAdd(&gh[k2all], 1u);
+          if (u1a >= 0) atomicAdd(&gh[P.h1a + u1a], 1u);
+          if (u1b >= 0) atomicAdd(&gh[P.h1b + u1b], 1u);
+        }
+        b2 += (in & (bin_k2(bw[k]) != 0)) ? 1u : 0u;
       }
-      if (DO_SEG && in) {
+      if (DO_SEG) {
         // window id (pos-1)//ws: the reference's start += ws*((pos-start)//ws) from start=1 (:894, :948)
         const uint32_t qp = k ? w[k - 1] : wprev;
         const uint32_t qn = k < 3 ? w[k + 1] : wnext;
-        const bool first = (i == t.cb) || (qp != w[k]);
-        const bool last = (i + 1 == t.ce) || (qn != w[k]);
-        const size_t s = (size_t)t.sbase + w[k];
-        if (first) slots[s].x = i + 1u;  // 0 = unset; the scan kernel clears what it consumed
-        if (last) slots[s].y = i + 1u;
+        const bool first = in & ((i == t.cb) | (qp != w[k]));
+        const bool last = in & ((i + 1 == t.ce) | (qn != w[k]));
+        segcode |= (first ? 1u : 0u) << (2 * k) | (last ? 2u : 0u) << (2 * k);
+      }
+      __builtin_amdgcn_sched_barrier(0);   // one SNP at a time: its lane masks die before the next
+    }
+    // window boundaries are rare: one divergent pass over the set bits
+    if (DO_SEG && segcode) {
+      for (uint32_t c = segcode; c; c &= c - 1) {
+        const int bit = __builtin_ctz(c), k = bit >> 1;
+        const uint32_t wk = k == 0 ? w[0] : k == 1 ? w[1] : k == 2 ? w[2] : w[3];
+        uint32_t* sl = reinterpret_cast<uint32_t*>(slots + ((size_t)t.sbase + wk));
+        sl[bit & 1] = i0 + k + 1u;   // .x = first + 1, .y = last + 1 (0 = unset; the scan kernel clears them)
       }
     }
     if (DO_BINS) {
@@ -377,37 +399,30 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
     }
   };
 
-  // two vectors per thread in flight per step (8 SNPs, 32 B of counts + positions); the lanes at
-  // the wave edges fetch their neighbour positions in the same batch
-  constexpr uint32_t STEP = 8 * BLOCK1;
-  const uint32_t ab = t.begin & ~3u;
+  // one 16-B vector of counts (+ positions) per thread per step; loads are clamped into the tile
+  // (lanes past its end re-read its last vector, masked) so that no load sits behind a branch; the
+  // lanes at the wave edges fetch their neighbour positions in the same batch
+  constexpr uint32_t STEP = 4 * BLOCK1;
+  const uint32_t ab = t.begin & ~3u, alast = (t.end - 1u) & ~3u;
   for (uint32_t base = ab; base < t.end; base += STEP) {
-    const uint32_t ia = base + 4 * threadIdx.x, ib = ia + 4 * BLOCK1;
-    const bool la = ia < t.end, lb = ib < t.end;
-    const uint4 ca = la ? *reinterpret_cast<const uint4*>(counts + ia) : make_uint4(0, 0, 0, 0);
-    const uint4 cbv = lb ? *reinterpret_cast<const uint4*>(counts + ib) : make_uint4(0, 0, 0, 0);
-    const uint4 pa = (need_pos && la) ? *reinterpret_cast<const uint4*>(pos + ia) : make_uint4(0, 0, 0, 0);
-    const uint4 pb = (need_pos && lb) ? *reinterpret_cast<const uint4*>(pos + ib) : make_uint4(0, 0, 0, 0);
-    const uint2 aav = (filt && la) ? *reinterpret_cast<const uint2*>(ann + ia) : make_uint2(0, 0);
-    const uint2 abv = (filt && lb) ? *reinterpret_cast<const uint2*>(ann + ib) : make_uint2(0, 0);
-    uint32_t wpa = 0, wna = 0, wpb = 0, wnb = 0;
+    const uint32_t ia = base + 4 * threadIdx.x;
+    const uint32_t il = min(ia, alast);
+    const uint4 ca = *reinterpret_cast<const uint4*>(counts + il);
+    const uint4 pa = need_pos ? *reinterpret_cast<const uint4*>(pos + il) : make_uint4(0, 0, 0, 0);
+    const uint2 aav = filt ? *reinterpret_cast<const uint2*>(ann + il) : make_uint2(0, 0);
+    uint32_t wpa = 0, wna = 0;
     if (DO_SEG) {
       // neighbour positions at the wave edges and past the tile end, loaded with the vectors
-      uint32_t xa_prev = 0, xa_next = 0, xb_prev = 0, xb_next = 0;
-      if (lane == 0 && ia > 0) xa_prev = pos[ia - 1];
-      if ((lane == WAVE - 1 || ia + 4 >= t.end) && ia + 4 < t.ce) xa_next = pos[ia + 4];
-      if (lane == 0 && ib > 0) xb_prev = pos[ib - 1];
-      if ((lane == WAVE - 1 || ib + 4 >= t.end) && ib + 4 < t.ce) xb_next = pos[ib + 4];
+      uint32_t xa_prev = 0, xa_next = 0;
+      const bool edge_next = lane == WAVE - 1 || ia + 4 >= t.end;
+      if (lane == 0 && ia > 0) xa_prev = pos[min(ia, alast + 4u) - 1];
+      if (edge_next && ia + 4 < t.ce) xa_next = pos[ia + 4];
       wpa = __shfl_up(wid_fast(P, pa.w), 1, WAVE);
       wna = __shfl_down(wid_fast(P, pa.x), 1, WAVE);
-      wpb = __shfl_up(wid_fast(P, pb.w), 1, WAVE);
-      wnb = __shfl_down(wid_fast(P, pb.x), 1, WAVE);
-      if (lane == 0) { wpa = wid_fast(P, xa_prev); wpb = wid_fast(P, xb_prev); }
-      if (lane == WAVE - 1 || ia + 4 >= t.end) wna = wid_fast(P, xa_next);
-      if (lane == WAVE - 1 || ib + 4 >= t.end) wnb = wid_fast(P, xb_next);
+      if (lane == 0) wpa = wid_fast(P, xa_prev);
+      if (edge_next) wna = wid_fast(P, xa_next);
     }
     process(ia, ca, pa, aav, wpa, wna);
-    process(ib, cbv, pb, abv, wpb, wnb);
   }
   STAMP(22);
   if (err) atomicOr(err_word, err);
@@ -925,7 +940,7 @@ __device__ __forceinline__ double xlnx(uint32_t x, const double* Ft, const doubl
 // run's replicas -- the k_bg_slice computation -- in LDS (LPl), using the histogram area HB as
 // scratch; clears this workgroup's share of the other parity's replicas; the chromosome's first
 // workgroup (writer) also writes the global tables.  The head lands in *hb_out (LDS).
-__device__ __attribute__((noinline)) void fused_table(int nb2, int nh, int nt, int n1p, int n2p, int n1, int n2,
+__device__ __forceinline__ void fused_table(int nb2, int nh, int nt, int n1p, int n2p, int n1, int n2,
                                                       int t1a, int t1b, int nchrom, uint32_t chrom, bool writer,
                                                       int bg, const uint32_t* __restrict__ Rc, size_t rs,
                                                       uint32_t* __restrict__ repl, uint32_t* __restrict__ bcount,
@@ -933,7 +948,7 @@ __device__ __attribute__((noinline)) void fused_table(int nb2, int nh, int nt, i
                                                       BgHead* __restrict__ head, double* LPl, uint32_t* HB,
                                                       const int2* __restrict__ leaves, int nleaves,
                                                       const int4* __restrict__ nodes, int nnodes, int nlevels,
-                                                      BgHead* hb_out) {
+                                                      const double* __restrict__ lnx, BgHead* hb_out) {
   __shared__ double sh_misc[8];
   __shared__ uint32_t sh_flags;
   const int tid = threadIdx.x;
@@ -942,15 +957,6 @@ __device__ __attribute__((noinline)) void fused_table(int nb2, int nh, int nt, i
   BgHead hb;
   PL* T = tab + (size_t)bg * nt;
   double* LP = LPg + (size_t)bg * nt;
-  // the other parity's replicas and inner sums: zeroed for the next run, a slice per workgroup
-  {
-    uint32_t* Ro = repl + (size_t)(1 - par) * REPL * rs;
-    const size_t tot = (size_t)REPL * rs, share = (tot + gridDim.x - 1) / gridDim.x;
-    const size_t lo = (size_t)blockIdx.x * share, hi = lo + share < tot ? lo + share : tot;
-    for (size_t k = lo + tid; k < hi; k += SBLOCK) Ro[k] = 0u;
-    if (blockIdx.x == 0)
-      for (int c = tid; c < nchrom; c += SBLOCK) bcount[(size_t)(1 - par) * nchrom + c] = 0u;
-  }
   // scratch in the histogram area: u1 words, 1D p, leaf accumulators, leaf sums
   double* scr = reinterpret_cast<double*>(HB);
   uint32_t* u1 = HB;                 // [0, 512) words
@@ -958,11 +964,15 @@ __device__ __attribute__((noinline)) void fused_table(int nb2, int nh, int nt, i
   double* p1b = scr + 392;           // 128
   double* acc8 = scr + 512;          // 8 per leaf (<= 128 leaves)
   double* lsum = scr + 1536;         // <= 128 leaves + 127 nodes
+  uint32_t* vcnt = HB + FUSED_VCNT;  // the table's counts (2D, then folded 1D), nt words
   const double B2 = (double)bcount[(size_t)par * nchrom + chrom];
   const int4 my_node = tid < nnodes ? nodes[tid] : make_int4(0, 0, -1, 0);
+  const int2 my_leaf = tid < nleaves ? leaves[tid] : make_int2(0, 0);   // this thread's leaf to combine
+  const int gl = (tid - 2 * WAVE) >> 3;                                   // waves 2..7: accumulator group
+  const int2 acc_leaf = (tid >= 2 * WAVE && gl < nleaves) ? leaves[gl] : make_int2(0, 0);
   // replica sums, four words per 16-B load, every load of a round in flight; 2D words become
   // proportions (LPl holds p until the log pass), 1D words go to u1
-  constexpr int QJ = 1;   // 16-B rows per thread per round
+  constexpr int QJ = 2;   // 16-B rows per thread per round
   for (int q0 = tid; q0 < nh / 4; q0 += QJ * SBLOCK) {
     uint4 x[QJ][REPL];
 #pragma unroll
@@ -987,6 +997,7 @@ __device__ __attribute__((noinline)) void fused_table(int nb2, int nh, int nt, i
         if (k < nb2) {
           const double v = (double)sm[c];
           LPl[k] = (B2 != 0.0) ? v / B2 : 0.0;
+          vcnt[k] = sm[c];
           if (writer) T[k].v = v;
         } else {
           u1[k - nb2] = sm[c];
@@ -1016,6 +1027,7 @@ __device__ __attribute__((noinline)) void fused_table(int nb2, int nh, int nt, i
         const double p = (B1 != 0.0) ? f[j] / B1 : 0.0;
         p1[k] = p;
         LPl[t0 + k] = p;
+        vcnt[t0 + k] = (uint32_t)f[j];
         if (writer) T[t0 + k].v = f[j];
       }
     }
@@ -1024,7 +1036,7 @@ __device__ __attribute__((noinline)) void fused_table(int nb2, int nh, int nt, i
     // 2D numpy pairwise leaves over p[1 : nb2-2], eight lanes per leaf
     for (int g = (tid - 2 * WAVE) >> 3; g < nleaves; g += (SBLOCK - 2 * WAVE) / 8) {
       const int r = tid & 7;
-      const int2 lf = leaves[g];
+      const int2 lf = g == gl ? acc_leaf : leaves[g];
       if (lf.y >= 8) {
         const double* a = LPl + 1 + lf.x;
         double x = a[r];
@@ -1035,7 +1047,7 @@ __device__ __attribute__((noinline)) void fused_table(int nb2, int nh, int nt, i
   }
   __syncthreads();
   if (tid < nleaves) {
-    const int2 lf = leaves[tid];
+    const int2 lf = my_leaf;
     const double* a = LPl + 1 + lf.x;
     const double* q = acc8 + tid * 8;
     double res = 0.0;
@@ -1081,29 +1093,35 @@ __device__ __attribute__((noinline)) void fused_table(int nb2, int nh, int nt, i
   const uint32_t flags = sh_flags;
   const int kl[3] = {nb2 - 2, t1a + n1p - 1, t1b + n2p - 1};
   const double pad[3] = {sh_misc[0], sh_misc[3], sh_misc[4]};
-  // logs, LG independent ones per thread per round
-  constexpr int LG = 2;
-  for (int k0 = tid; k0 < nt; k0 += LG * SBLOCK) {
-    double pv[LG], lv[LG];
+  // lp = ln v - ln B, ln v from the ln table (p = v / B stayed in LPl only for numpy's sums above);
+  // the replaced last inner bins take log(padj).  Same value as log(v / B) to a few ulp.
+  const double lnB[3] = {log(B2), log(sh_misc[1]), log(sh_misc[2])};
+  const double ninf = -__builtin_inf();
+  constexpr int LB = 6;   // bins per thread per round, all table loads in flight together
+  for (int k0 = tid; k0 < nt; k0 += LB * SBLOCK) {
+    uint32_t v[LB];
+    double lv[LB];
 #pragma unroll
-    for (int j = 0; j < LG; ++j) {
+    for (int j = 0; j < LB; ++j) {
       const int k = k0 + j * SBLOCK;
-      pv[j] = k < nt ? LPl[k] : 1.0;
+      v[j] = k < nt ? vcnt[k] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < LB; ++j) lv[j] = lnx[v[j] < (uint32_t)LNX_N ? v[j] : 0u];
+#pragma unroll
+    for (int j = 0; j < LB; ++j) {
+      const int k = k0 + j * SBLOCK;
+      if (k >= nt) continue;
+      const int sp = k < nb2 ? 0 : (k < t1b ? 1 : 2);
+      double lp = v[j] == 0u ? ninf : (v[j] < (uint32_t)LNX_N ? lv[j] : log((double)v[j])) - lnB[sp];
 #pragma unroll
       for (int q = 0; q < 3; ++q)
-        if (k == kl[q] && (flags & (256u << q))) pv[j] = pad[q];
-    }
-#pragma unroll
-    for (int j = 0; j < LG; ++j) lv[j] = log(pv[j]);
-#pragma unroll
-    for (int j = 0; j < LG; ++j) {
-      const int k = k0 + j * SBLOCK;
-      if (k < nt) {
-        LPl[k] = lv[j];
-        if (writer) { T[k].lp = lv[j]; LP[k] = lv[j]; }
-      }
+        if (k == kl[q] && (flags & (256u << q))) lp = log(pad[q]);
+      LPl[k] = lp;
+      if (writer) { T[k].lp = lp; LP[k] = lp; }
     }
   }
+  STAMP(19);
   hb.B2 = B2; hb.B1a = sh_misc[1]; hb.B1b = sh_misc[2]; hb.flags = flags & 0xffu; hb.pad = 0;
   if (writer && tid == 0) head[bg] = hb;
   if (tid == 0) *hb_out = hb;
@@ -1132,7 +1150,8 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
                                                    int mode_bp, uint32_t* __restrict__ repl,
                                                    uint32_t* __restrict__ bcount, int par,
                                                    const int2* __restrict__ leaves, int nleaves,
-                                                   const int4* __restrict__ nodes, int nnodes, int nlevels) {
+                                                   const int4* __restrict__ nodes, int nnodes, int nlevels,
+                                                   int write_chrom) {
   extern __shared__ double ldsd[];
   __shared__ BgHead sh_hb;
   STAMP(10);
@@ -1185,8 +1204,10 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
     for (int k = tid; k < P.nt; k += SBLOCK) LPl[k] = LP[k];
     hb = head[bg];
   } else {
-    fused_table(P.nb2, P.nh, P.nt, P.n1p, P.n2p, P.n1, P.n2, P.t1a, P.t1b, P.nchrom, ch.chrom, ch.wid_lo == 0, bg,
-                Rc, rs, repl, bcount, par, tab, LPg, head, LPl, HB, leaves, nleaves, nodes, nnodes, nlevels, &sh_hb);
+    fused_table(P.nb2, P.nh, P.nt, P.n1p, P.n2p, P.n1, P.n2, P.t1a, P.t1b, P.nchrom, ch.chrom,
+                ch.wid_lo == 0 && (int)ch.chrom == write_chrom, bg,
+                Rc, rs, repl, bcount, par, tab, LPg, head, LPl, HB, leaves, nleaves, nodes, nnodes, nlevels, lnx,
+                &sh_hb);
     hb = sh_hb;
   }
   for (int k = lane; k < per / 4; k += WAVE) reinterpret_cast<uint4*>(W)[k] = make_uint4(0, 0, 0, 0);
@@ -1203,6 +1224,16 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
   const uint32_t zflags = bg_zero_flags(hb);
   const bool nan2 = hb.flags & BGF_NAN2, nan1a = hb.flags & BGF_NAN1A, nan1b = hb.flags & BGF_NAN1B;
 
+  if (FUSED) {
+    // the other parity's replicas and inner sums: zeroed for the next run, a slice per workgroup
+    // (after the last barrier: nothing waits for these stores)
+    uint32_t* Ro = repl + (size_t)(1 - par) * REPL * rs;
+    const size_t tot = (size_t)REPL * rs, share = (tot + gridDim.x - 1) / gridDim.x;
+    const size_t lo = (size_t)blockIdx.x * share, hi = lo + share < tot ? lo + share : tot;
+    for (size_t k = lo + tid; k < hi; k += SBLOCK) Ro[k] = 0u;
+    if (blockIdx.x == 0)
+      for (int c = tid; c < P.nchrom; c += SBLOCK) bcount[(size_t)(1 - par) * P.nchrom + c] = 0u;
+  }
   if (!active) return;
   Win cur;
   bounds(s, sr0, cur);
