@@ -1,0 +1,134 @@
+"""Multi-GPU scan: chromosome shards, one process per GPU, one gather of the window tables.
+
+Given per-chromosome backgrounds (combined_scan, scan_perChr_bySNPs; twoDSFS_class.py:809-825,
+1422-1541) every chromosome is independent, so a rank scans a contiguous range of whole
+chromosomes with no collective on the data path.  The only exchange is one all-gather
+of the fixed-stride 64-B window records (RCCL over xGMI with the "nccl" backend on MI355X, gloo
+on CPU), after which the tables are concatenated in chromosome order and the sequential rules of
+the drivers (sfs2d.post: stale carry Q6, final block Q9) run once on the whole table.
+
+The final-block helper record (Q9) needs the window before the last one of the whole scan, which
+may sit in the previous chromosome: the last rank therefore also scans the chromosome before its
+range (its records are dropped in the merge, the owner's are kept) and contributes the only
+helper record.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib as L
+
+
+def shard_chromosomes(chrom_off: Sequence[int], world: int) -> List[Tuple[int, int]]:
+    """Contiguous chromosome ranges [lo, hi) per rank, balanced by SNP count (greedy cuts at
+    k * total / world).  Ranks may get an empty range when there are fewer chromosomes than ranks."""
+    off = np.asarray(chrom_off, dtype=np.int64)
+    nchrom = len(off) - 1
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    total = int(off[-1]) if nchrom else 0
+    bounds = [0]
+    for k in range(1, world):
+        target = total * k / world
+        c = int(np.searchsorted(off[1:], target, side="left")) + 1   # first chromosome end >= target
+        c = max(bounds[-1], min(nchrom, c))
+        bounds.append(c)
+    bounds.append(nchrom)
+    return [(bounds[r], bounds[r + 1]) for r in range(world)]
+
+
+def scan_range(shards: List[Tuple[int, int]], rank: int, prev_extra: bool) -> Tuple[int, int]:
+    """Chromosomes rank `rank` actually scans: its shard, plus the preceding chromosome on the last
+    non-empty rank when the final-block helper (Q9) is wanted."""
+    lo, hi = shards[rank]
+    last = max((r for r, (a, b) in enumerate(shards) if b > a), default=-1)
+    if prev_extra and rank == last and lo > 0:
+        lo -= 1
+    return lo, hi
+
+
+def _globalise(t: np.ndarray, slo: int, snp0: int) -> np.ndarray:
+    """Local chromosome numbers and SNP indices of a rank's table -> global ones."""
+    t = t.copy()
+    t["chrom"] += slo
+    live = (t["flags"] & L.W_EMPTY) == 0
+    t["begin"][live] += snp0
+    t["end"][live] += snp0
+    return t
+
+
+def merge_tables(tables: List[np.ndarray], shards: List[Tuple[int, int]], prev_extra: bool,
+                 chrom_off: Sequence[int]) -> np.ndarray:
+    """Concatenate per-rank record tables (each in its own local chromosome numbering and SNP
+    indexing, as scanned over `scan_range`) into the global table a single-GPU plan over all
+    chromosomes would emit."""
+    off = np.asarray(chrom_off, dtype=np.int64)
+    parts, extra = [], None
+    last = max((r for r, (a, b) in enumerate(shards) if b > a), default=-1)
+    for r, t in enumerate(tables):
+        t = np.asarray(t, dtype=L.WINDOW_DTYPE)
+        lo, hi = shards[r]
+        slo, _ = scan_range(shards, r, prev_extra)
+        if hi <= lo:
+            continue
+        body = _globalise(t[(t["flags"] & L.W_EXTRA) == 0], slo, int(off[slo]))
+        body = body[body["chrom"] >= lo]          # the context chromosome belongs to its owner
+        parts.append(body)
+        if prev_extra and r == last:
+            e = t[(t["flags"] & L.W_EXTRA) != 0]
+            if len(e):
+                e = _globalise(e, slo, int(off[slo]))
+                e["wid"][(e["flags"] & L.W_EMPTY) == 0] += np.uint32(off[slo])   # helper: wid = SNP index
+                extra = e
+    out = np.concatenate(parts) if parts else np.zeros(0, dtype=L.WINDOW_DTYPE)
+    if extra is not None:
+        out = np.concatenate([out, extra])
+    return out
+
+
+def gather_tables(local: np.ndarray, world: int, device=None) -> List[np.ndarray]:
+    """All-gather variable-length record tables over the default process group.  `device` is the
+    torch device the exchange runs on (a GPU for RCCL, None / cpu for gloo)."""
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cpu") if device is None else torch.device(device)
+    raw = np.ascontiguousarray(local, dtype=L.WINDOW_DTYPE).view(np.uint8).reshape(-1, 64)
+    n = torch.tensor([raw.shape[0]], dtype=torch.int64, device=dev)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    ns = [int(x.item()) for x in ns]
+    m = max(ns) if ns else 0
+    buf = torch.zeros((m, 64), dtype=torch.uint8, device=dev)
+    if raw.shape[0]:
+        buf[: raw.shape[0]] = torch.from_numpy(raw).to(dev)
+    allb = torch.zeros((world * m, 64), dtype=torch.uint8, device=dev)
+    if m:
+        dist.all_gather_into_tensor(allb, buf)
+    allb = allb.cpu().numpy().reshape(world, m, 64)
+    return [allb[r, : ns[r]].copy().view(L.WINDOW_DTYPE).reshape(-1) for r in range(world)]
+
+
+def combined_scan_sharded(packed, window_size: int, n1p: int, n2p: int, rank: int, world: int,
+                          device: int = 0, comm_device=None, fold: bool = True) -> Optional[dict]:
+    """combined_scan (twoDSFS_class.py:787-991) over `world` GPUs: every rank holds the packed SNPs
+    on the host, uploads and scans its chromosome range; rank 0 returns the reference's result
+    dict, the other ranks None."""
+    from . import post
+    from .engine import Engine, ScanConfig
+    shards = shard_chromosomes(packed.chrom_off, world)
+    lo, hi = scan_range(shards, rank, True)
+    local = np.zeros(0, dtype=L.WINDOW_DTYPE)
+    if shards[rank][1] > shards[rank][0]:
+        sub = packed.subset_chroms(range(lo, hi))
+        eng = Engine.get(device)
+        dev = eng.upload(sub)
+        local = eng.scan(dev, ScanConfig(n1p=n1p, n2p=n2p, fold=fold, window=window_size,
+                                         prev_extra=(rank == max(r for r, (a, b) in enumerate(shards) if b > a))))
+        dev.close()
+    tables = gather_tables(local, world, comm_device)
+    if rank != 0:
+        return None
+    recs = merge_tables(tables, shards, True, packed.chrom_off)
+    return post.combined_scan(recs, packed, window_size, post.num_slots(recs))

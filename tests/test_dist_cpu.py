@@ -1,0 +1,112 @@
+"""Multi-GPU host logic on CPU: chromosome sharding, the per-rank scan ranges (with the Q9 context
+chromosome), the gloo all-gather of record tables across 2 processes, and the merge into the table a
+single plan over all chromosomes emits.  Per-rank records come from the oracle (tests/fake_records),
+so this runs without a GPU; the GPU path uses the same functions with the RCCL backend."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+
+import fake_records as FR
+from oracle import sfs_oracle as O
+from sfs2d import _lib as L
+from sfs2d import dist as D
+from sfs2d import post
+from sfs2d.synth import synth_genome
+
+
+def test_shard_chromosomes_balanced_and_contiguous():
+    off = np.cumsum([0, 100, 5, 300, 40, 40, 200, 10])
+    for world in (1, 2, 3, 4, 8, 16):
+        sh = D.shard_chromosomes(off, world)
+        assert len(sh) == world
+        assert sh[0][0] == 0 and sh[-1][1] == len(off) - 1
+        assert all(a[1] == b[0] for a, b in zip(sh, sh[1:]))
+        assert all(lo <= hi for lo, hi in sh)
+    sh = D.shard_chromosomes(off, 2)
+    sizes = [int(off[hi] - off[lo]) for lo, hi in sh]
+    assert max(sizes) <= 450   # 695 SNPs: a greedy cut near the half
+
+
+def test_scan_range_adds_context_chromosome_to_last_rank():
+    sh = [(0, 2), (2, 5), (5, 5)]
+    assert D.scan_range(sh, 0, True) == (0, 2)
+    assert D.scan_range(sh, 1, True) == (1, 5)     # last non-empty rank
+    assert D.scan_range(sh, 1, False) == (2, 5)
+    assert D.scan_range(sh, 2, True) == (5, 5)
+
+
+def _local_tables(p, shards, ws, ocfg, bgs):
+    tabs = []
+    last = max(r for r, (a, b) in enumerate(shards) if b > a)
+    for r in range(len(shards)):
+        lo, hi = D.scan_range(shards, r, True)
+        if shards[r][1] <= shards[r][0]:
+            tabs.append(np.zeros(0, dtype=L.WINDOW_DTYPE))
+            continue
+        sub = p.subset_chroms(range(lo, hi))
+        tabs.append(FR.bp_records(sub, ws, ocfg, lambda c, lo=lo: bgs[lo + c], prev_extra=(r == last)))
+    return tabs
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_merge_equals_single_plan(world):
+    p = synth_genome(4, [3000, 1500, 800, 1], 25, 25, seed=5)   # last chromosome: a single window
+    ocfg = O.Cfg(25, 25)
+    bgs = O.chrom_backgrounds(p, ocfg)
+    ws = 20000
+    full = FR.bp_records(p, ws, ocfg, lambda c: bgs[c], prev_extra=True)
+    shards = D.shard_chromosomes(p.chrom_off, world)
+    merged = D.merge_tables(_local_tables(p, shards, ws, ocfg, bgs), shards, True, p.chrom_off)
+    assert _same(merged, full)
+    ref = O.combined_scan(p, ws, ocfg)
+    got = post.combined_scan(merged, p, ws, post.num_slots(merged))
+    assert list(got) == list(ref)
+
+
+def _same(a, b):
+    """Tables equal, except the Q9 helper's window-id field (a SNP index on the GPU, unused)."""
+    a, b = a.copy(), b.copy()
+    for t in (a, b):
+        t["wid"][(t["flags"] & L.W_EXTRA) != 0] = 0
+    return a.tobytes() == b.tobytes()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, outdir):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    p = synth_genome(3, [2500, 1200, 700], 25, 25, seed=11)
+    ocfg = O.Cfg(25, 25)
+    bgs = O.chrom_backgrounds(p, ocfg)
+    shards = D.shard_chromosomes(p.chrom_off, world)
+    local = _local_tables(p, shards, 20000, ocfg, bgs)[rank]
+    tables = D.gather_tables(local, world)
+    if rank == 0:
+        merged = D.merge_tables(tables, shards, True, p.chrom_off)
+        np.save(os.path.join(outdir, "merged.npy"), merged.view(np.uint8))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_allgather_two_ranks():
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        merged = np.load(os.path.join(d, "merged.npy")).view(L.WINDOW_DTYPE)
+    p = synth_genome(3, [2500, 1200, 700], 25, 25, seed=11)
+    ocfg = O.Cfg(25, 25)
+    bgs = O.chrom_backgrounds(p, ocfg)
+    full = FR.bp_records(p, 20000, ocfg, lambda c: bgs[c], prev_extra=True)
+    assert _same(merged, full)

@@ -207,3 +207,24 @@ def test_dense_primitives_vs_oracle(golden):
     b1 = obj.fold_1d_sfs(obj.calculate_1d_sfs(d, "p1", 25, None, None, None))
     o1 = O.clr1d(O.fold1d(O.sfs1d(win, np.arange(win.n), 1, ocfg)), O.fold1d(O.sfs1d(d, np.arange(d.n), 1, ocfg)))
     assert gu.close(obj.calculate_likelihood_1D(f1, b1), o1)
+
+
+def test_sharded_combined_scan_world1_matches_class():
+    """sfs2d.dist end to end on one GPU (gloo group of one): shard, scan, gather, merge, post-pass."""
+    import os
+    import torch.distributed as dist
+    import twoDSFS_class as T
+    from sfs2d import dist as D
+    from sfs2d.synth import synth_genome
+    p = synth_genome(3, [6000, 2500, 1], 25, 25, seed=21)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        got = D.combined_scan_sharded(p, 20000, 25, 25, rank=0, world=1)
+    finally:
+        dist.destroy_process_group()
+    obj = T.LikelihoodInference_jointSFS(None, None, pop1="p1", pop2="p2", pop1_size=25, pop2_size=25)
+    ref = obj.combined_scan(p, 20000)
+    errs = gu.compare_results(got, ref)
+    assert not errs, errs[:10]
