@@ -15,6 +15,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -89,7 +90,7 @@ struct sfs2d_ctx {
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   double* d_lnx = nullptr;
-  double* d_df = nullptr;   // D(r) then F(x), LNT each
+  double* d_df = nullptr;   // D(r), F(x) (LNT each), then 1/k (RCPN)
   std::string err;
 };
 
@@ -117,6 +118,9 @@ struct sfs2d_plan {
   int nbg = 0;
   bool do_bg = false, do_seg = false, lds_hist = true, bg_ready = false;
   bool fused = false;       // per-chromosome tables built inside k_scan_w (parity-alternating replicas)
+  bool fst = false;         // SFS2D_F_FST: Fst per slot into d_fst
+  double* d_fst = nullptr;
+  unsigned long long* d_fsum = nullptr;   // k_prep's per-slot Fst sums (int64 fixed point), cleared by the scan
   int hr = 1;               // k_prep LDS histogram copies per word
   uint64_t runs = 0;        // completed runs (the replica parity of a fused plan)
   int G = 64;
@@ -183,20 +187,27 @@ void plan_free(sfs2d_plan* p) {
   hipFree(p->d_tiles); hipFree(p->d_chunks); hipFree(p->d_slots); hipFree(p->d_repl); hipFree(p->d_bcount);
   hipFree(p->d_done); hipFree(p->d_bgval); hipFree(p->d_tab); hipFree(p->d_lp); hipFree(p->d_head);
   hipFree(p->d_bg1d); hipFree(p->d_leafsum); hipFree(p->d_leaves); hipFree(p->d_nodes); hipFree(p->d_slices);
-  hipFree(p->d_out); hipFree(p->d_err); hipFree(p->d_bins);
+  hipFree(p->d_out); hipFree(p->d_err); hipFree(p->d_bins); hipFree(p->d_fst); hipFree(p->d_fsum);
   for (auto& e : p->ev) if (e) hipEventDestroy(e);
   for (auto& e : p->tev) if (e) hipEventDestroy(e);
 }
 
 int plan_par(const sfs2d_plan* pl) { return pl->fused ? (int)(pl->runs & 1) : 0; }
 
-template <bool P16, bool FUSED>
+template <bool P16, bool FUSED, bool FST>
 void launch_scan_w(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
-  hipLaunchKernelGGL((k_scan_w<P16, FUSED>), dim3((unsigned)pl->chunks.size()), dim3(SBLOCK), pl->scan_lds,
+  hipLaunchKernelGGL((k_scan_w<P16, FUSED, FST>), dim3((unsigned)pl->chunks.size()), dim3(SBLOCK), pl->scan_lds,
                      pl->ctx->stream, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
                      per_chrom, pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, bp, pl->d_repl, pl->d_bcount,
                      plan_par(pl), pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels,
-                     pl->extra_rec >= 0 ? (int)pl->last_chrom : -1);
+                     pl->extra_rec >= 0 ? (int)pl->last_chrom : -1, pl->d_fsum, pl->d_fst);
+}
+
+template <bool P16, bool FST>
+void launch_scan_g(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
+  hipLaunchKernelGGL((k_scan_g<P16, FST>), dim3((unsigned)pl->chunks.size()), dim3(BLOCK), pl->scan_lds,
+                     pl->ctx->stream, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_head, per_chrom,
+                     pl->ctx->d_lnx, out, bp, pl->d_fsum, pl->d_fst);
 }
 
 template <bool P16>
@@ -204,24 +215,36 @@ hipError_t launch_scan(sfs2d_plan* pl, sfs2d_window* out) {
   const int per_chrom = pl->prm.bg_mode == SFS2D_BG_PER_CHROM ? 1 : 0;
   const int bp = pl->prm.window_mode == SFS2D_WINDOW_BP ? 1 : 0;
   if (pl->G == WAVE) {
-    if (pl->fused) launch_scan_w<P16, true>(pl, out, per_chrom, bp);
-    else launch_scan_w<P16, false>(pl, out, per_chrom, bp);
-  } else
-    hipLaunchKernelGGL((k_scan_g<P16>), dim3((unsigned)pl->chunks.size()), dim3(BLOCK), pl->scan_lds, pl->ctx->stream,
-                       pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_head, per_chrom,
-                       pl->ctx->d_lnx, out, bp);
+    if (pl->fused) {
+      if (pl->fst) launch_scan_w<P16, true, true>(pl, out, per_chrom, bp);
+      else launch_scan_w<P16, true, false>(pl, out, per_chrom, bp);
+    } else {
+      if (pl->fst) launch_scan_w<P16, false, true>(pl, out, per_chrom, bp);
+      else launch_scan_w<P16, false, false>(pl, out, per_chrom, bp);
+    }
+  } else {
+    if (pl->fst) launch_scan_g<P16, true>(pl, out, per_chrom, bp);
+    else launch_scan_g<P16, false>(pl, out, per_chrom, bp);
+  }
+  return hipGetLastError();
+}
+
+template <bool B, bool S, bool L, bool N, bool F, bool FS>
+hipError_t launch_prep3(sfs2d_plan* pl) {
+  const sfs2d_data* d = pl->data;
+  const int par = plan_par(pl);
+  hipLaunchKernelGGL((k_prep<B, S, L, N, F, FS>), dim3((unsigned)pl->tiles.size()), dim3(BLOCK1),
+                     (B && L) ? pl->bg_lds : 0, pl->ctx->stream, pl->K, d->counts, d->pos, d->ann, pl->d_tiles,
+                     pl->d_repl + (size_t)par * REPL * pl->K.nchrom * pl->K.nh, pl->d_slots, pl->d_bins,
+                     pl->d_bcount + (size_t)par * pl->K.nchrom, pl->d_err, L ? pl->hr : 1,
+                     pl->ctx->d_df + 2 * LNT, pl->d_fsum);
   return hipGetLastError();
 }
 
 template <bool B, bool S, bool L, bool N, bool F>
 hipError_t launch_prep2(sfs2d_plan* pl) {
-  const sfs2d_data* d = pl->data;
-  const int par = plan_par(pl);
-  hipLaunchKernelGGL((k_prep<B, S, L, N, F>), dim3((unsigned)pl->tiles.size()), dim3(BLOCK1), (B && L) ? pl->bg_lds : 0,
-                     pl->ctx->stream, pl->K, d->counts, d->pos, d->ann, pl->d_tiles,
-                     pl->d_repl + (size_t)par * REPL * pl->K.nchrom * pl->K.nh, pl->d_slots, pl->d_bins,
-                     pl->d_bcount + (size_t)par * pl->K.nchrom, pl->d_err, L ? pl->hr : 1);
-  return hipGetLastError();
+  if (N && pl->fst) return launch_prep3<B, S, L, N, F, N>(pl);   // Fst only with the bins pass
+  return launch_prep3<B, S, L, N, F, false>(pl);
 }
 
 template <bool B, bool S, bool L, bool N>
@@ -300,10 +323,11 @@ int sfs2d_ctx_create(int device, sfs2d_ctx** out) {
   c->stream = c->own;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) c->ncu = prop.multiProcessorCount;
-  if (dalloc(c, &c->d_lnx, LNX_N) || dalloc(c, &c->d_df, 2 * LNT)) {
+  if (dalloc(c, &c->d_lnx, LNX_N) || dalloc(c, &c->d_df, 2 * LNT + RCPN)) {
     hipFree(c->d_lnx); hipStreamDestroy(c->own); delete c; return SFS2D_E_NOMEM;
   }
-  hipLaunchKernelGGL(k_init_lnx, dim3(LNX_N / 256), dim3(256), 0, c->stream, c->d_lnx, c->d_df, c->d_df + LNT);
+  hipLaunchKernelGGL(k_init_lnx, dim3(LNX_N / 256), dim3(256), 0, c->stream, c->d_lnx, c->d_df, c->d_df + LNT,
+                     c->d_df + 2 * LNT);
   if (hipStreamSynchronize(c->stream) != hipSuccess) {
     hipFree(c->d_lnx); hipFree(c->d_df); hipStreamDestroy(c->own); delete c; return SFS2D_E_HIP;
   }
@@ -532,13 +556,22 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
     return set_err(ctx, SFS2D_E_ARG, "2D grid too large for LDS with 32-bit bins (windows of >= 65536 SNPs)");
   }
   pl->fused = pl->do_bg && pl->G == WAVE;
+  pl->fst = (prm->flags & SFS2D_F_FST) != 0;
   if (pl->scan_lds > 64 * 1024) {
-    hipFuncSetAttribute((const void*)k_scan_w<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
-    hipFuncSetAttribute((const void*)k_scan_w<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
-    hipFuncSetAttribute((const void*)k_scan_w<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
-    hipFuncSetAttribute((const void*)k_scan_w<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
-    hipFuncSetAttribute((const void*)k_scan_g<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
-    hipFuncSetAttribute((const void*)k_scan_g<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->scan_lds);
+    const int lds = (int)pl->scan_lds;
+    const hipFuncAttribute A = hipFuncAttributeMaxDynamicSharedMemorySize;
+    hipFuncSetAttribute((const void*)k_scan_w<true, true, false>, A, lds);
+    hipFuncSetAttribute((const void*)k_scan_w<false, true, false>, A, lds);
+    hipFuncSetAttribute((const void*)k_scan_w<true, false, false>, A, lds);
+    hipFuncSetAttribute((const void*)k_scan_w<false, false, false>, A, lds);
+    hipFuncSetAttribute((const void*)k_scan_w<true, true, true>, A, lds);
+    hipFuncSetAttribute((const void*)k_scan_w<false, true, true>, A, lds);
+    hipFuncSetAttribute((const void*)k_scan_w<true, false, true>, A, lds);
+    hipFuncSetAttribute((const void*)k_scan_w<false, false, true>, A, lds);
+    hipFuncSetAttribute((const void*)k_scan_g<true, false>, A, lds);
+    hipFuncSetAttribute((const void*)k_scan_g<false, false>, A, lds);
+    hipFuncSetAttribute((const void*)k_scan_g<true, true>, A, lds);
+    hipFuncSetAttribute((const void*)k_scan_g<false, true>, A, lds);
   }
   if (pl->extra_lds > 64 * 1024) {
     hipFuncSetAttribute((const void*)k_scan_extra<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->extra_lds);
@@ -551,8 +584,8 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
   uint32_t CH = 2;
   if (pl->G == WAVE) {
     int occ = 0;
-    const hipError_t oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<true, true>, SBLOCK, pl->scan_lds)
-                                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<false, true>, SBLOCK, pl->scan_lds);
+    const hipError_t oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<true, true, false>, SBLOCK, pl->scan_lds)
+                                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<false, true, false>, SBLOCK, pl->scan_lds);
     if (oe != hipSuccess || occ < 1) occ = 1;
     const int64_t cap = (int64_t)occ * ctx->ncu;
     auto nchunks = [&](uint32_t L) {
@@ -561,6 +594,7 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
       return t;
     };
     CH = SBLOCK / WAVE;
+    if (const char* ev = std::getenv("SFS2D_CHUNK")) CH = std::max<uint32_t>(8, (uint32_t)std::atoi(ev) & ~7u);   // tuning
     while (nchunks(CH) > cap) CH += SBLOCK / WAVE;
   }
   for (int c = 0; c < nc; ++c) {
@@ -579,7 +613,10 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
   {
     const int64_t n = data->n;
     // ~1000+ tiles for big inputs (several workgroups per CU), >= 4096 SNPs each (flush amortised)
-    int64_t T = std::max<int64_t>(4096, std::min<int64_t>(65536, (n / 768 + 4095) / 4096 * 4096));
+    // (with Fst, <= 32k SNPs per tile keep a tile's windows in its LDS sums down to ~128-SNP windows)
+    const int64_t Tmax = (prm->flags & SFS2D_F_FST) ? 32768 : 65536;
+    int64_t T = std::max<int64_t>(4096, std::min<int64_t>(Tmax, (n / 768 + 4095) / 4096 * 4096));
+    if (const char* ev = std::getenv("SFS2D_TILE")) T = std::max<int64_t>(2048, std::atoll(ev) & ~int64_t(3));   // tuning
     for (int c = 0; c < nc; ++c)
       for (int64_t s = data->chrom_off[c]; s < data->chrom_off[c + 1]; s += T) {
         Tile t{};
@@ -587,6 +624,7 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
         t.end = (uint32_t)std::min<int64_t>(s + T, data->chrom_off[c + 1]);
         t.cb = (uint32_t)data->chrom_off[c]; t.ce = (uint32_t)data->chrom_off[c + 1];
         t.sbase = (uint32_t)slot_base[c];
+        t.nslots = (uint32_t)(slot_base[c + 1] - slot_base[c]);
         pl->tiles.push_back(t);
       }
   }
@@ -594,10 +632,16 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
   pl->bg_lds = ((size_t)K.nh * pl->hr + WAVE) * 4;   // + 64 lane trash words
   pl->lds_hist = pl->bg_lds <= 150 * 1024;
   if (pl->lds_hist && pl->bg_lds > 64 * 1024) {
-    hipFuncSetAttribute((const void*)k_prep<true, true, true, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->bg_lds);
-    hipFuncSetAttribute((const void*)k_prep<true, false, true, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->bg_lds);
-    hipFuncSetAttribute((const void*)k_prep<true, true, true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->bg_lds);
-    hipFuncSetAttribute((const void*)k_prep<true, false, true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->bg_lds);
+    const hipFuncAttribute A = hipFuncAttributeMaxDynamicSharedMemorySize;
+    const int lds = (int)pl->bg_lds;
+    hipFuncSetAttribute((const void*)k_prep<true, true, true, true, false, false>, A, lds);
+    hipFuncSetAttribute((const void*)k_prep<true, false, true, true, false, false>, A, lds);
+    hipFuncSetAttribute((const void*)k_prep<true, true, true, true, true, false>, A, lds);
+    hipFuncSetAttribute((const void*)k_prep<true, false, true, true, true, false>, A, lds);
+    hipFuncSetAttribute((const void*)k_prep<true, true, true, true, false, true>, A, lds);
+    hipFuncSetAttribute((const void*)k_prep<true, false, true, true, false, true>, A, lds);
+    hipFuncSetAttribute((const void*)k_prep<true, true, true, true, true, true>, A, lds);
+    hipFuncSetAttribute((const void*)k_prep<true, false, true, true, true, true>, A, lds);
   }
   hipFuncSetAttribute((const void*)k_bg_finalize, hipFuncAttributeMaxDynamicSharedMemorySize,
                       (int)(sizeof(double) * FIN_LDS_BINS));
@@ -639,6 +683,8 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
   rc = rc ? rc : dalloc(ctx, &pl->d_bins, nbins);
   rc = rc ? rc : dalloc(ctx, &pl->d_out, (size_t)pl->nrec);
   rc = rc ? rc : dalloc(ctx, &pl->d_err, 4);
+  if (pl->fst) rc = rc ? rc : dalloc(ctx, &pl->d_fst, (size_t)pl->nslots + 1);
+  if (pl->fst) rc = rc ? rc : dalloc(ctx, &pl->d_fsum, 2 * ((size_t)pl->nslots + 1));
   if (rc) { plan_free(pl); delete pl; return rc; }
   hipError_t e = hipSuccess;
 #define PCPY(dst, v) if (e == hipSuccess && !(v).empty()) e = hipMemcpyAsync(dst, (v).data(), sizeof((v)[0]) * (v).size(), hipMemcpyHostToDevice, st)
@@ -654,6 +700,7 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_done, 0, sizeof(uint32_t) * pl->nbg, st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_err, 0, 4 * sizeof(uint32_t), st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_bins, 0, sizeof(uint32_t) * nbins, st);
+  if (e == hipSuccess && pl->fst) e = hipMemsetAsync(pl->d_fsum, 0, sizeof(unsigned long long) * 2 * ((size_t)pl->nslots + 1), st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_out, 0, sizeof(sfs2d_window) * (size_t)pl->nrec, st);
   for (auto& ev : pl->ev) if (e == hipSuccess) e = hipEventCreate(&ev);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
@@ -773,6 +820,26 @@ int sfs2d_plan_bg_buffer(sfs2d_plan* pl, void** dev_ptr, int64_t* nbytes) {
   return 0;
 }
 
+int sfs2d_plan_fst_buffer(sfs2d_plan* pl, void** dev_ptr, int64_t* nslots) {
+  if (!pl || !dev_ptr || !nslots) return SFS2D_E_ARG;
+  if (!pl->fst) return set_err(pl->ctx, SFS2D_E_ARG, "plan was created without SFS2D_F_FST");
+  *dev_ptr = pl->d_fst;
+  *nslots = pl->nslots;
+  return 0;
+}
+
+int sfs2d_plan_fst_read(sfs2d_plan* pl, double* out_host, int64_t cap) {
+  if (!pl) return SFS2D_E_ARG;
+  sfs2d_ctx* ctx = pl->ctx;
+  if (!pl->fst) return set_err(ctx, SFS2D_E_ARG, "plan was created without SFS2D_F_FST");
+  if (cap < pl->nslots) return set_err(ctx, SFS2D_E_CAP, "output capacity too small");
+  if (pl->nslots && !out_host) return SFS2D_E_ARG;
+  if (pl->nslots)
+    HIPCHK(ctx, hipMemcpyAsync(out_host, pl->d_fst, sizeof(double) * pl->nslots, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
 int sfs2d_plan_check(sfs2d_plan* pl) {
   if (!pl) return SFS2D_E_ARG;
   sfs2d_ctx* ctx = pl->ctx;
@@ -791,7 +858,10 @@ int sfs2d_plan_check(sfs2d_plan* pl) {
 // diagnostic: stamps of a -DSFS2D_STAMPS build (returns SFS2D_E_ARG in the shipped build)
 int sfs2d__debug_stamps(unsigned long long* out64) {
 #ifdef SFS2D_STAMPS
+  // 64 phase stamps, then per-block (start, end) of k_prep and k_scan_w (2 x 4096 x 2)
   if (hipMemcpyFromSymbol(out64, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 64) != hipSuccess) return SFS2D_E_HIP;
+  if (hipMemcpyFromSymbol(out64 + 64, HIP_SYMBOL(g_blk), sizeof(unsigned long long) * 2 * 4096 * 2) != hipSuccess)
+    return SFS2D_E_HIP;
   return 0;
 #else
   (void)out64;
@@ -895,8 +965,8 @@ int sfs2d_bg_hist(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* pr
     if (e == hipSuccess) e = hipMemsetAsync(pl.d_err, 0, 4, ctx->stream);
     if (e == hipSuccess) e = hipMemsetAsync(pl.d_bcount, 0, 4, ctx->stream);
     if (e == hipSuccess && pl.lds_hist && pl.bg_lds > 64 * 1024)
-      hipFuncSetAttribute((const void*)k_prep<true, false, true, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.bg_lds),
-      hipFuncSetAttribute((const void*)k_prep<true, false, true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.bg_lds);
+      hipFuncSetAttribute((const void*)k_prep<true, false, true, false, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.bg_lds),
+      hipFuncSetAttribute((const void*)k_prep<true, false, true, false, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.bg_lds);
     if (e == hipSuccess) e = launch_prep(&pl, false);
     if (e == hipSuccess) e = hipMemcpyAsync(hist.data(), pl.d_repl, sizeof(uint32_t) * REPL * K.nh, hipMemcpyDeviceToHost, ctx->stream);
     uint32_t err = 0;

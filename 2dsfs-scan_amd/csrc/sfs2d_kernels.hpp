@@ -54,6 +54,7 @@ constexpr int FBLOCK = 1024;      // k_bg_finalize workgroup
 constexpr int KBLOCK = 512;       // k_bg_slice workgroup
 constexpr int LNX_N = 1 << 20;    // ln(k) table for k < LNX_N (bin counts / window totals)
 constexpr int LNT = 512;          // D(r) and x ln x tables staged in LDS by k_scan_w
+constexpr int RCPN = 512;         // 1/k for k < 512 (Fst: called allele counts ref + alt <= 510), after the LNT tables
 constexpr int REPL = 4;           // replicas of the per-chromosome background histograms
 constexpr int PW_MAX_LEAVES = 256;
 constexpr int LEAVES_PER_SLICE = 4;
@@ -95,8 +96,12 @@ struct KParams {
 };
 
 struct Tile {   // k_prep work item: SNPs [begin, end) of chromosome chrom = [cb, ce), slots from sbase
-  uint32_t chrom, begin, end, cb, ce, sbase, pad0, pad1;
+  uint32_t chrom, begin, end, cb, ce, sbase, nslots, pad1;   // nslots: the chromosome's window slots
 };
+
+constexpr int FST_LDS = 256;             // k_prep: windows per tile accumulated in LDS (others: global)
+constexpr int FST_R = 4;                 // ... in FST_R interleaved copies (lane & 3) to spread same-window atomics
+constexpr double FST_SCALE = 1099511627776.0;   // 2^40: Fst sums as int64 fixed point (deterministic atomics)
 
 struct Chunk {  // k_scan work item: window slots [slot_lo, slot_hi) of one chromosome
   uint32_t chrom, slot_lo, slot_hi, wid_lo, cb, pad0, pad1, pad2;
@@ -129,6 +134,11 @@ static_assert(sizeof(Tile) == 32 && sizeof(Chunk) == 32, "work items are 32 byte
 // phase boundaries, read back with sfs2d__debug_stamps.  The shipped library executes none.
 #ifdef SFS2D_STAMPS
 __device__ unsigned long long g_stamps[64];
+__device__ unsigned long long g_blk[2][4096][2];   // per-block start / end (k_prep, k_scan_w)
+#define BLK_STAMP(k, e)                                                                          \
+  do {                                                                                           \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_blk[k][blockIdx.x][e] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #define STAMP(i)                                                                                 \
   do {                                                                                           \
     if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[i] = __builtin_amdgcn_s_memrealtime();     \
@@ -136,6 +146,9 @@ __device__ unsigned long long g_stamps[64];
 #else
 #define STAMP(i) \
   do {           \
+  } while (0)
+#define BLK_STAMP(k, e) \
+  do {                  \
   } while (0)
 #endif
 
@@ -146,6 +159,12 @@ __device__ __forceinline__ uint32_t wid_of(uint32_t p, uint32_t ws) { return p ?
 // the same window id with the division replaced by a multiply-high (host-side magic numbers)
 __device__ __forceinline__ uint32_t wid_fast(const KParams& P, uint32_t p) {
   const uint32_t n = p - min(p, 1u);   // p - 1, and 0 for p = 0 (wid_of(0) = 0), without a branch
+  const uint32_t t = __umulhi(n, P.wmag);
+  return (t + ((n - t) >> P.wsh1)) >> P.wsh2;
+}
+
+// q = n / ws with the host-side magic numbers (fixed-SNP-count window ids)
+__device__ __forceinline__ uint32_t div_fast(const KParams& P, uint32_t n) {
   const uint32_t t = __umulhi(n, P.wmag);
   return (t + ((n - t) >> P.wsh1)) >> P.wsh2;
 }
@@ -284,9 +303,10 @@ __device__ __forceinline__ uint32_t bin_g2(uint32_t w) { return (w >> 23) & 0x7f
 
 // ln k for k < LNX_N; F(x) = x ln x for x < LNT; D(r) = F(r+1) - F(r) for r < LNT-1 and
 // D(LNT-1) = 0 (k_scan_w adds the ranks from LNT-1 on per bin, as F(x) - F(LNT-1))
-__global__ void k_init_lnx(double* lnx, double* dtab, double* ftab) {
+__global__ void k_init_lnx(double* lnx, double* dtab, double* ftab, double* rtab) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < LNX_N) lnx[i] = i ? log((double)i) : 0.0;
+  if (i < RCPN) rtab[i] = i ? 1.0 / (double)i : 0.0;
   if (i < LNT) {
     const double a = i ? (double)i * log((double)i) : 0.0;
     const double b = (double)(i + 1) * log((double)(i + 1));
@@ -297,30 +317,71 @@ __global__ void k_init_lnx(double* lnx, double* dtab, double* ftab) {
 
 // ------------------------------------------------------------------------------------------ K1
 
-template <bool DO_BG, bool DO_SEG, bool LDS_HIST, bool DO_BINS, bool FILT>
+// Per-SNP Fst terms (see fst_terms below for the definition) from the raw counts; 1/k from rcp.
+__device__ __forceinline__ bool fst_snp(uint32_t c, bool member, const double* rcp, double& num, double& den) {
+  const uint32_t r1 = c & 0xffu, a1 = (c >> 8) & 0xffu, r2 = (c >> 16) & 0xffu, a2 = c >> 24;
+  const uint32_t n1c = r1 + a1, n2c = r2 + a2;
+  const bool ok = member & (n1c >= 2u) & (n2c >= 2u);
+  const uint32_t m1 = ok ? n1c : 2u, m2 = ok ? n2c : 2u;   // u8 counts: n <= 510 < RCPN
+  const double i1 = rcp[m1], i2 = rcp[m2], j1 = rcp[m1 - 1], j2 = rcp[m2 - 1];
+  const double p1 = (double)a1 * i1, p2 = (double)a2 * i2;
+  const double d = p1 - p2;
+  num = ok ? d * d - p1 * (1.0 - p1) * j1 - p2 * (1.0 - p2) * j2 : 0.0;
+  den = ok ? p1 * (1.0 - p2) + p2 * (1.0 - p1) : 0.0;
+  return ok;
+}
+
+template <bool DO_BG, bool DO_SEG, bool LDS_HIST, bool DO_BINS, bool FILT, bool FST>
 __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __restrict__ counts,
                                                  const uint32_t* __restrict__ pos, const uint16_t* __restrict__ ann,
                                                  const Tile* __restrict__ tiles, uint32_t* __restrict__ repl,
                                                  uint2* __restrict__ slots, uint32_t* __restrict__ bins,
                                                  uint32_t* __restrict__ bcount, uint32_t* __restrict__ err_word,
-                                                 int hr) {
+                                                 int hr, const double* __restrict__ rcp_g,
+                                                 unsigned long long* __restrict__ fsum) {
   // repl / bcount: this run's parity buffers.  LDS histogram: hr interleaved copies of every word
   // (lane & (hr-1) picks one), which spreads the many same-bin atomics of a wavefront over banks.
   extern __shared__ uint32_t sh_hist[];
   __shared__ uint32_t sh_b2;
+  // FST: per-window sums of the Fst terms, int64 fixed point (num, den) for the tile's first
+  // FST_LDS windows (FST_R copies each), the rest straight to the global per-slot sums
+  __shared__ unsigned long long sh_fst[FST ? 2 * FST_R * FST_LDS : 1];
+  __shared__ double sh_rcp[FST ? RCPN : 1];
+  __shared__ uint32_t sh_wlo;
   STAMP(20);
+  BLK_STAMP(0, 0);
   const Tile t = tiles[blockIdx.x];
   uint32_t* gh = repl + ((size_t)(blockIdx.x % REPL) * P.nchrom + t.chrom) * (size_t)P.nh;
   const int lane0 = threadIdx.x & (WAVE - 1);
   const int hsh = LDS_HIST ? (hr == 4 ? 2 : 0) : 0;
   const int rep = lane0 & (hr - 1);
   const int trash = P.nh * hr + lane0;   // LDS word after the histogram (64 of them)
+  if (FST) {
+    for (int k = threadIdx.x; k < 2 * FST_R * FST_LDS; k += BLOCK1) sh_fst[k] = 0ull;
+    for (int k = threadIdx.x; k < RCPN; k += BLOCK1) sh_rcp[k] = rcp_g[k];
+    if (threadIdx.x == 0) sh_wlo = DO_SEG ? wid_fast(P, pos[t.begin]) : div_fast(P, t.begin - t.cb);
+  }
   if (DO_BG) {
     if (LDS_HIST)
       for (int k = threadIdx.x; k < P.nh * hr + WAVE; k += BLOCK1) sh_hist[k] = 0u;
     if (threadIdx.x == 0) sh_b2 = 0u;
-    __syncthreads();
   }
+  if (DO_BG || FST) __syncthreads();
+  const uint32_t wlo = FST ? sh_wlo : 0u;
+  // fixed-point add of one lane's (num, den) pair into window wid of this chromosome
+  const int frep = threadIdx.x & (FST_R - 1);
+  auto fst_add = [&](uint32_t wid, double num, double den) {
+    const unsigned long long qn = (unsigned long long)__double2ll_rn(num * FST_SCALE);
+    const unsigned long long qd = (unsigned long long)__double2ll_rn(den * FST_SCALE);
+    const uint32_t j = wid - wlo;
+    if (j < (uint32_t)FST_LDS) {
+      atomicAdd(&sh_fst[2 * (j * FST_R + frep)], qn);
+      atomicAdd(&sh_fst[2 * (j * FST_R + frep) + 1], qd);
+    } else {
+      atomicAdd(&fsum[2 * ((size_t)t.sbase + wid)], qn);
+      atomicAdd(&fsum[2 * ((size_t)t.sbase + wid) + 1], qd);
+    }
+  };
   // FILT: a position or variant_type filter is set (kept out of the common kernel: its uniform
   // flags would otherwise occupy scalar registers throughout the loop)
   const bool pos_filter = FILT && (P.has_start || P.has_end);
@@ -343,6 +404,10 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
     }
     uint32_t bw[4];
     uint32_t segcode = 0;   // bit 2k: SNP k opens a window, bit 2k+1: it closes one
+    // Fst: this lane's sums for the window of its first SNP (key); SNPs of a later window in the
+    // same vector (a boundary inside it: rare) are added on their own
+    uint32_t fkey = 0xffffffffu;
+    double fn = 0.0, fd = 0.0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint32_t i = i0 + k;
@@ -355,6 +420,20 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
       }
       int k2all, u1a, u1b;
       bw[k] = classify(P, cc[k], var_ok, pos_ok, err, k2all, u1a, u1b);
+      if (FST) {
+        const uint32_t wk = DO_SEG ? w[k] : div_fast(P, i - t.cb);
+        const bool in_slot = DO_SEG | (wk < t.nslots);   // fixed-SNP windows: the tail is dropped
+        double num, den;
+        if (fst_snp(cc[k], in & (k2all >= 0) & in_slot, sh_rcp, num, den)) {
+          if (fkey == 0xffffffffu) fkey = wk;
+          if (wk == fkey) {
+            fn += num;
+            fd += den;
+          } else {
+            fst_add(wk, num, den);
+          }
+        }
+      }
       if (DO_BG) {
         if (LDS_HIST) {
           // no branches: skipped SNPs add to the lane's trash word (keeps exec masks, and the
@@ -379,6 +458,7 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
       }
       __builtin_amdgcn_sched_barrier(0);   // one SNP at a time: its lane masks die before the next
     }
+    if (FST && fkey != 0xffffffffu) fst_add(fkey, fn, fd);
     // window boundaries are rare: one divergent pass over the set bits
     if (DO_SEG && segcode) {
       for (uint32_t c = segcode; c; c &= c - 1) {
@@ -429,7 +509,22 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
   if (DO_BG) {
     b2 = wave_sum_u(b2);
     if (lane == 0 && b2) atomicAdd(&sh_b2, b2);
-    __syncthreads();
+  }
+  if (DO_BG || FST) __syncthreads();
+  if (FST)
+    for (int j = threadIdx.x; j < FST_LDS; j += BLOCK1) {
+      unsigned long long qn = 0, qd = 0;
+#pragma unroll
+      for (int r = 0; r < FST_R; ++r) {
+        qn += sh_fst[2 * (j * FST_R + r)];
+        qd += sh_fst[2 * (j * FST_R + r) + 1];
+      }
+      if (qn | qd) {
+        atomicAdd(&fsum[2 * ((size_t)t.sbase + wlo + j)], qn);
+        atomicAdd(&fsum[2 * ((size_t)t.sbase + wlo + j) + 1], qd);
+      }
+    }
+  if (DO_BG) {
     if (LDS_HIST)
       for (int k = threadIdx.x; k < P.nh; k += BLOCK1) {
         uint32_t v;
@@ -444,6 +539,7 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
     if (threadIdx.x == 0 && sh_b2) atomicAdd(&bcount[t.chrom], sh_b2);
   }
   STAMP(23);
+  BLK_STAMP(0, 1);
 }
 
 // ------------------------------------------------------------------------------------------ K2
@@ -924,6 +1020,21 @@ __device__ __forceinline__ bool suspect_zero(double t, uint32_t N) {
   return N && fabs(t) <= 1e-9 * ((double)N + 1.0);
 }
 
+// Hudson's Fst (Bhatia et al. 2013, ratio of averages) over the SNPs entering the window's 2D SFS
+// (filters passed, (0,0) excluded, the (n1,n2) bin included) with >= 2 called alleles in each
+// population: p_i = alt_i / (ref_i + alt_i) on the raw counts,
+//   num = (p1 - p2)^2 - p1(1-p1)/(n1c-1) - p2(1-p2)/(n2c-1),  den = p1(1-p2) + p2(1-p1),
+// Fst = sum num / sum den (NaN when no SNP qualifies or sum den == 0).  Not in the reference (its
+// published Fst is pixy's Weir-Cockerham, joined in R): parity is pinned to oracle.window_fst.
+// k_prep sums the terms per window slot (fst_snp, int64 fixed point); the scan kernels turn the
+// sums into the value and clear them for the next run.
+__device__ __forceinline__ double fst_take(unsigned long long* fsum, size_t s) {
+  const long long qn = (long long)fsum[2 * s], qd = (long long)fsum[2 * s + 1];
+  fsum[2 * s] = 0ull;
+  fsum[2 * s + 1] = 0ull;
+  return qd != 0 ? (double)qn / (double)qd : __builtin_nan("");
+}
+
 struct Win {
   uint32_t b, e;
   uint4 v0, v1;   // bins of the first chunk (SNPs [b & ~3, +512))
@@ -950,6 +1061,7 @@ __device__ __forceinline__ void fused_table(int nb2, int nh, int nt, int n1p, in
                                                       const int4* __restrict__ nodes, int nnodes, int nlevels,
                                                       const double* __restrict__ lnx, BgHead* hb_out) {
   __shared__ double sh_misc[8];
+  __shared__ double sh_lnb[3];
   __shared__ uint32_t sh_flags;
   const int tid = threadIdx.x;
   const int lane = tid & (WAVE - 1);
@@ -1087,6 +1199,9 @@ __device__ __forceinline__ void fused_table(int nb2, int nh, int nt, int n1p, in
       else if (fabs(pa[q]) > 1e-15) flags |= 256u << q;
     }
     sh_misc[0] = 1.0 - S;
+    sh_lnb[0] = log(B2);
+    sh_lnb[1] = log(B1a);
+    sh_lnb[2] = log(B1b);
     sh_flags = flags;
   }
   __syncthreads();
@@ -1095,7 +1210,7 @@ __device__ __forceinline__ void fused_table(int nb2, int nh, int nt, int n1p, in
   const double pad[3] = {sh_misc[0], sh_misc[3], sh_misc[4]};
   // lp = ln v - ln B, ln v from the ln table (p = v / B stayed in LPl only for numpy's sums above);
   // the replaced last inner bins take log(padj).  Same value as log(v / B) to a few ulp.
-  const double lnB[3] = {log(B2), log(sh_misc[1]), log(sh_misc[2])};
+  const double lnB[3] = {sh_lnb[0], sh_lnb[1], sh_lnb[2]};
   const double ninf = -__builtin_inf();
   constexpr int LB = 6;   // bins per thread per round, all table loads in flight together
   for (int k0 = tid; k0 < nt; k0 += LB * SBLOCK) {
@@ -1140,7 +1255,7 @@ __device__ __forceinline__ void fused_table(int nb2, int nh, int nt, int n1p, in
 // per-lane counters give every count, the 2D atomic returns the SNP's rank r in its bin and the
 // SNP adds D(r) - lp_k; the 1D atomics land in lane-&3 replicas; then one lane per 1D bin adds
 // x ln x - x lp; the touched 2D words are cleared; DPP sums; one record.
-template <bool P16, bool FUSED>
+template <bool P16, bool FUSED, bool FST>
 __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 4 : 1))) void k_scan_w(KParams P, const uint32_t* __restrict__ bins,
                                                    const Chunk* __restrict__ chunks, uint2* __restrict__ slots,
                                                    PL* __restrict__ tab, double* __restrict__ LPg,
@@ -1151,10 +1266,12 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
                                                    uint32_t* __restrict__ bcount, int par,
                                                    const int2* __restrict__ leaves, int nleaves,
                                                    const int4* __restrict__ nodes, int nnodes, int nlevels,
-                                                   int write_chrom) {
+                                                   int write_chrom, unsigned long long* __restrict__ fsum,
+                                                   double* __restrict__ fst_out) {
   extern __shared__ double ldsd[];
   __shared__ BgHead sh_hb;
   STAMP(10);
+  BLK_STAMP(1, 0);
   const int tid = threadIdx.x;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & (WAVE - 1);
@@ -1246,6 +1363,7 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
     const uint32_t wid = ch.wid_lo + (s - ch.slot_lo);
     if (!cur.has) {
       if (lane == 0) write_empty(out + s, ch.chrom, wid);
+      if (FST && lane == 0) fst_out[s] = __builtin_nan("");
       Win nxt;
       nxt.has = false;
       if (more) bounds(sn, srn, nxt);
@@ -1373,6 +1491,7 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
       if (nan1a) w.t1a = __builtin_nan("");
       if (nan1b) w.t1b = __builtin_nan("");
     }
+    if (FST && lane == 0) fst_out[s] = fst_take(fsum, s);
     if (lane == 0) {
       write_rec(out + s, ch.chrom, wid, cur.b, cur.e, w, zflags);
       if (mode_bp) slots[s] = make_uint2(0u, 0u);   // leave the slot table clean for the next run
@@ -1382,15 +1501,20 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
     cur = nxt;
   }
   STAMP(15);
+#ifdef SFS2D_STAMPS
+  __builtin_amdgcn_s_barrier();   // diagnostic build only: the block's end is its last active wave's
+#endif
+  BLK_STAMP(1, 1);
 }
 
 // K3 for large grids: one workgroup per window, exact evaluation.
-template <bool P16>
+template <bool P16, bool FST>
 __global__ __launch_bounds__(BLOCK) void k_scan_g(KParams P, const uint32_t* __restrict__ bins,
                                                   const Chunk* __restrict__ chunks, uint2* __restrict__ slots,
                                                   const PL* __restrict__ tab, const BgHead* __restrict__ head,
                                                   int bg_per_chrom, const double* __restrict__ lnx,
-                                                  sfs2d_window* __restrict__ out, int mode_bp) {
+                                                  sfs2d_window* __restrict__ out, int mode_bp,
+                                                  unsigned long long* __restrict__ fsum, double* __restrict__ fst_out) {
   extern __shared__ uint32_t lds[];
   const int h2w = P16 ? (P.nb2 + 1) / 2 : P.nb2;
   const int core = h2w + (P.n1p + 1) + (P.n2p + 1);
@@ -1413,6 +1537,7 @@ __global__ __launch_bounds__(BLOCK) void k_scan_g(KParams P, const uint32_t* __r
       __syncthreads();
       if (sr.x == 0u) {
         if (threadIdx.x == 0) write_empty(out + s, ch.chrom, wid);
+        if (FST && threadIdx.x == 0) fst_out[s] = __builtin_nan("");
         continue;
       }
       b = sr.x - 1u;
@@ -1422,6 +1547,7 @@ __global__ __launch_bounds__(BLOCK) void k_scan_g(KParams P, const uint32_t* __r
       e = b + P.ws;
     }
     const WinOut w = eval_exact<BLOCK, P16, 1>(P, bins, b, e, TabGlobal{T}, hb, lnx, H2, H1a, H1b, redd, redu);
+    if (FST && threadIdx.x == 0) fst_out[s] = fst_take(fsum, s);
     if (threadIdx.x == 0) {
       write_rec(out + s, ch.chrom, wid, b, e, w, bg_zero_flags(hb));
       if (mode_bp) slots[s] = make_uint2(0u, 0u);

@@ -28,6 +28,7 @@ class ScanConfig:
     start_position: Optional[int] = None
     end_position: Optional[int] = None
     prev_extra: bool = False
+    fst: bool = False          # also compute Hudson's Fst per window slot (Plan.read_fst)
 
     def params(self) -> L.Params:
         p = L.Params()
@@ -40,7 +41,7 @@ class ScanConfig:
         p.start_pos = 0 if self.start_position is None else clamp(self.start_position)
         p.has_end = 0 if self.end_position is None else 1
         p.end_pos = 0 if self.end_position is None else clamp(self.end_position)
-        p.flags = L.F_PREV_EXTRA if self.prev_extra else 0
+        p.flags = (L.F_PREV_EXTRA if self.prev_extra else 0) | (L.F_FST if self.fst else 0)
         return p
 
 
@@ -157,6 +158,14 @@ class Plan:
     def run(self, out_dev_ptr: Optional[int] = None, phase: int = 0):
         self.eng.check(self.eng.lib.sfs2d_plan_run_phase(self.h, phase,
                                                          C.c_void_p(out_dev_ptr) if out_dev_ptr else None))
+
+    def read_fst(self) -> np.ndarray:
+        """Fst of the last run per window slot (NaN = no qualifying SNP / empty slot)."""
+        dptr, n = C.c_void_p(), C.c_int64()
+        self.eng.check(self.eng.lib.sfs2d_plan_fst_buffer(self.h, C.byref(dptr), C.byref(n)))
+        out = np.zeros(n.value, dtype=np.float64)
+        self.eng.check(self.eng.lib.sfs2d_plan_fst_read(self.h, out.ctypes.data if n.value else None, n.value))
+        return out
 
     def run_many(self, nruns: int, out_dev_ptr: Optional[int] = None):
         """Enqueue `nruns` back-to-back runs from C (no Python between runs)."""

@@ -37,12 +37,13 @@ WS = 20000
 def algorithmic_bytes(n_snp, n_slots, n_win, which):
     """Bytes each kernel must move (DESIGN.md "Kernels"): k_prep reads counts + positions (8 B/SNP),
     writes the packed bins (4 B/SNP) and the window slot table (8 B/window); k_scan_w reads the bins
-    (4 B/SNP) and the slot table (8 B/slot) and writes one 64-B record per slot."""
+    and, for Fst, the counts (8 B/SNP) and the slot table (8 B/slot) and writes one 64-B record and
+    one 8-B Fst per slot."""
     if which == "k3":
-        return 4 * n_snp + 8 * n_slots + 64 * n_slots
+        return 8 * n_snp + 8 * n_slots + 72 * n_slots
     if which == "k1":
         return 12 * n_snp + 8 * n_win
-    return 16 * n_snp + 8 * n_win + 72 * n_slots
+    return 20 * n_snp + 8 * n_win + 80 * n_slots
 
 
 def cpu_baseline(p):
@@ -65,7 +66,7 @@ def hbm_stream_roofline(eng, steps=5):
     from sfs2d.synth import synth_genome
     p = synth_genome(32, 1_562_500, POP, POP, seed=777)
     dev = eng.upload(p)
-    pl = eng.plan(dev, ScanConfig(n1p=POP, n2p=POP, window=WS))
+    pl = eng.plan(dev, ScanConfig(n1p=POP, n2p=POP, window=WS, fst=True))
     pl.run()
     pl.check()
     pl.set_timing(steps, every=2)
@@ -101,10 +102,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world)
-    torch.cuda.set_device(local)
 
     from sfs2d import _lib as L
     from sfs2d.engine import Engine, ScanConfig
@@ -112,30 +113,51 @@ def main():
 
     p = synth_genome(1, N_SNP, POP, POP, seed=12345 + rank)
     eng = Engine.get(local)
-    stream = torch.cuda.Stream(device=local)   # one stream shared by the HIP library and torch/RCCL
-    torch.cuda.set_stream(stream)
-    eng.set_stream(stream.cuda_stream)
+    scan_s = torch.cuda.Stream(device=local)    # the HIP library's stream
+    comm_s = torch.cuda.Stream(device=local)    # RCCL gathers of the window tables
+    torch.cuda.set_stream(scan_s)
+    eng.set_stream(scan_s.cuda_stream)
     dev = eng.upload(p)
-    pl = eng.plan(dev, ScanConfig(n1p=POP, n2p=POP, window=WS))
+    pl = eng.plan(dev, ScanConfig(n1p=POP, n2p=POP, window=WS, fst=True))
     nrec = pl.nrec
-    out = torch.empty((nrec, 64), dtype=torch.uint8, device=f"cuda:{local}")
-    gathered = None
+    cdev = f"cuda:{local}"
     if world > 1:
-        gathered = torch.empty((world, nrec, 64), dtype=torch.uint8, device=f"cuda:{local}")
-        counts = torch.tensor([nrec], device=f"cuda:{local}")
-        allc = [torch.zeros_like(counts) for _ in range(world)]
-        dist.all_gather(allc, counts)
-        assert all(int(c) == nrec for c in allc), "weak-scaling shards must have equal record counts"
+        # shards differ in window count: tables are padded to the largest (unused rows flagged empty)
+        c = torch.tensor([nrec], dtype=torch.int64, device=cdev)
+        dist.all_reduce(c, op=dist.ReduceOp.MAX)
+        rows = int(c.item())
+    else:
+        rows = nrec
+    outs = [torch.zeros((rows, 64), dtype=torch.uint8, device=cdev) for _ in range(2)]
+    for o in outs:
+        o[nrec:, 39] = 0x80   # padding rows: flags = SFS2D_W_EMPTY
+    gathered = [torch.empty((world * rows, 64), dtype=torch.uint8, device=cdev) for _ in range(2)] if world > 1 else None
+    ev_scan = [torch.cuda.Event() for _ in range(2)]
+    ev_comm = [torch.cuda.Event() for _ in range(2)]
+    for e in ev_comm:
+        e.record(comm_s)
+    torch.cuda.synchronize()
 
-    def step():
-        pl.run(out.data_ptr())
-        if world > 1:
-            dist.all_gather_into_tensor(gathered.view(world * nrec, 64), out)
+    def step(i):
+        # step i: scan into table i&1 on the scan stream; gather it on the comm stream while step
+        # i+1 scans into the other table (the scan of step i+2 waits for gather i to finish)
+        b = i & 1
+        scan_s.wait_event(ev_comm[b])
+        pl.run(outs[b].data_ptr())
+        ev_scan[b].record(scan_s)
+        comm_s.wait_event(ev_scan[b])
+        with torch.cuda.stream(comm_s):
+            dist.all_gather_into_tensor(gathered[b], outs[b])
+        ev_comm[b].record(comm_s)
 
+    out = outs[0]
     pl.run(out.data_ptr())
     pl.check()
-    for _ in range(args.warmup):
-        step()
+    if world > 1:
+        for i in range(args.warmup):
+            step(i)
+    else:
+        pl.run_many(args.warmup, out.data_ptr())
     # HIP events around each kernel of every 8th timed run, on the stream the kernels run on (sampled:
     # an event pair costs several microseconds of queue time, 1/8 of it is ~1 us per step)
     pl.set_timing(args.steps, every=8)
@@ -146,41 +168,47 @@ def main():
     if world == 1:
         pl.run_many(args.steps, out.data_ptr())   # enqueued from C: no host work between steps
     else:
-        for _ in range(args.steps):
-            step()
+        for i in range(args.steps):
+            step(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([dt], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     nr, (k1, k2, k3) = pl.timing_read()
     pl.check()
-    recs = np.frombuffer(out.cpu().numpy().tobytes(), dtype=L.WINDOW_DTYPE)
+    recs = np.frombuffer(out[:nrec].cpu().numpy().tobytes(), dtype=L.WINDOW_DTYPE)
     nwin_rank = int(((recs["flags"] & L.W_EMPTY) == 0).sum())
-    total_windows = nwin_rank * world
+    total_windows = nwin_rank
+    if world > 1:
+        tw = torch.tensor([nwin_rank], dtype=torch.int64, device=cdev)
+        dist.all_reduce(tw)
+        total_windows = int(tw.item())
     value = total_windows * args.steps / dt
 
     if rank == 0:
         b3 = algorithmic_bytes(p.n, nrec, nwin_rank, "k3")
         achieved = b3 / (k3 * 1e-3) / 1e9
         line = {
-            "metric": "genomic windows/s (T2D+T1D_p1+T1D_p2; Fst not computed yet) at 20 kb, n1=n2=50",
+            "metric": "genomic windows/s (T2D+T1D+Fst) at 20 kb, n1=n2=50; HBM GB/s fraction",
             "value": value, "unit": "windows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic (SURVEY 8d generator, seed 12345+rank)",
             "config": {"workload": "configs[1]: synthetic 1 chromosome x 1e6 SNPs per GPU, 20 kb windows, "
                                    "n1=n2=50 haploid (pop_size 25/25), per-chromosome background",
                        "snps_per_gpu": p.n, "windows_per_gpu": nwin_rank, "window_bp": WS,
+                       "stats": "T2D, T1D_p1, T1D_p2 (reference semantics) + Hudson Fst (DESIGN.md; not in the "
+                                "reference, parity vs its own oracle restatement)",
                        "parallelism": f"windows sharded by chromosome over {world} GPU(s); RCCL all-gather"},
             "kernels_ms": {"k_prep": k1, "k_bg_slice_or_gap": k2, "k_scan_w": k3, "timed_runs": nr,
                            "exact_path_windows": pl.stats()},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": "k_scan_w", "ms": k3,
-                         "note": "k_scan_w, algorithmic bytes 4 B/SNP + 72 B/slot per launch over its event-timed "
+                         "note": "k_scan_w, algorithmic bytes 8 B/SNP + 80 B/slot per launch over its event-timed "
                                  "duration; the 8 MB config-2 stream is MALL-resident (see roofline_hbm)"},
         }
         if not args.no_hbm_stream and world == 1:

@@ -57,6 +57,9 @@ extern "C" {
 #define SFS2D_F_PREV_EXTRA 1u  /* also evaluate the previous window's 1D SFSs against the LAST window's
                                   chromosome background (combined_scan final block, 951-989, quirk Q9) */
 
+#define SFS2D_F_FST 2u         /* also compute Hudson's Fst per window slot (not in the reference),
+                                  read with sfs2d_plan_fst_read / sfs2d_plan_fst_buffer */
+
 /* window record flags */
 #define SFS2D_W_EMPTY 0x80000000u  /* slot holds no SNP (fixed-bp slot between SNPs): not a window */
 #define SFS2D_W_BG2_ZERO 0x1u      /* background 2D inner sum == 0  -> None / ZeroDivisionError */
@@ -134,6 +137,9 @@ int sfs2d_plan_read(sfs2d_plan* plan, sfs2d_window* out_host, int64_t cap, int64
 /* device pointers of the plan's per-chromosome background histogram replicas (uint32), for a
  * multi-GPU all-reduce between sfs2d_plan_run_phase(plan, 1) and (plan, 2). */
 int sfs2d_plan_bg_buffer(sfs2d_plan* plan, void** dev_ptr, int64_t* nbytes);
+/* Fst of the last run per window slot (NaN: no qualifying SNP / empty slot); plans with SFS2D_F_FST */
+int sfs2d_plan_fst_read(sfs2d_plan* plan, double* out_host, int64_t cap);
+int sfs2d_plan_fst_buffer(sfs2d_plan* plan, void** dev_ptr, int64_t* nslots);
 int sfs2d_plan_run_phase(sfs2d_plan* plan, int phase, sfs2d_window* out_dev);
 /* cumulative number of windows re-evaluated on the exact path (|T| ~ 0: proportionality test) */
 int sfs2d_plan_stats(sfs2d_plan* plan, uint32_t* exact_windows);

@@ -387,3 +387,32 @@ def window_records(p, wins, cfg, bg_of_window, guards=True):
                         T2D=_num(clr2d(g, bg2, guards)), T1D_p1=_num(clr1d(f1, bg1a, guards)),
                         T1D_p2=_num(clr1d(f2, bg1b, guards))))
     return out
+
+
+def window_fst(p, idx, cfg) -> Optional[float]:
+    """Hudson's Fst (Bhatia et al. 2013, ratio of averages) of one window -- NOT part of the
+    reference (its published Fst is pixy's Weir-Cockerham, joined in R): parity is
+    unpinned, this restatement defines it.  SNPs: those entering the window's 2D SFS (filters
+    passed, (0,0) after the joint fold excluded; twoDSFS_class.py:179-217) with >= 2 called alleles
+    in each population; raw (unfolded) frequencies p = alt / (ref + alt):
+        num = (p1 - p2)^2 - p1(1-p1)/(n1c-1) - p2(1-p2)/(n2c-1),  den = p1(1-p2) + p2(1-p1),
+    Fst = sum(num) / sum(den); None when no SNP qualifies or sum(den) == 0."""
+    idx = np.asarray(idx, dtype=np.int64)
+    m = _sfs_mask(p, idx, cfg)
+    r1, a1, r2, a2 = p.ref1[idx], p.alt1[idx], p.ref2[idx], p.alt2[idx]
+    x1, x2 = a1, a2
+    if cfg.fold:
+        sw = (a1 + a2) > (cfg.n1p + cfg.n2p)
+        x1 = np.where(sw, r1, a1)
+        x2 = np.where(sw, r2, a2)
+    n1c, n2c = r1 + a1, r2 + a2
+    keep = m & ~((x1 == 0) & (x2 == 0)) & (n1c >= 2) & (n2c >= 2)
+    if not keep.any():
+        return None
+    n1c, n2c = n1c[keep].astype(np.float64), n2c[keep].astype(np.float64)
+    p1 = a1[keep] / n1c
+    p2 = a2[keep] / n2c
+    num = (p1 - p2) ** 2 - p1 * (1 - p1) / (n1c - 1) - p2 * (1 - p2) / (n2c - 1)
+    den = p1 * (1 - p2) + p2 * (1 - p1)
+    d = float(den.sum())
+    return None if d == 0.0 else float(num.sum()) / d

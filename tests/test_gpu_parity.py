@@ -228,3 +228,72 @@ def test_sharded_combined_scan_world1_matches_class():
     ref = obj.combined_scan(p, 20000)
     errs = gu.compare_results(got, ref)
     assert not errs, errs[:10]
+
+
+def test_rank_overflow_big_bins_bp():
+    """Bins holding more than the LDS D-table's 511 ranks (k_scan_w adds F(x) - F(511) per bin)."""
+    from sfs2d import _lib as L
+    from sfs2d.engine import ScanConfig
+    from sfs2d.pack import pack_counts
+    from sfs2d.synth import synth_genome
+    p = synth_genome(2, [4000, 2600], 25, 25, seed=77)
+    rng = np.random.default_rng(3)
+    hot = rng.random(p.n) < 0.6            # 60% of the SNPs share the bin (1, 0)
+    a1 = np.where(hot, 1, p.alt1); r1 = np.where(hot, 49, p.ref1)
+    a2 = np.where(hot, 0, p.alt2); r2 = np.where(hot, 50, p.ref2)
+    p.counts = pack_counts(r1, a1, r2, a2)
+    ocfg = O.Cfg(25, 25)
+    bgs = O.chrom_backgrounds(p, ocfg)
+    for ws in (10_000_000, 100_000):
+        _records_vs_oracle(p, ScanConfig(n1p=25, n2p=25, window=ws), ocfg, O.bp_windows(p, ws), lambda c: bgs[c])
+
+
+def test_snp_windows_of_65536_plus_take_exact_path():
+    """Windows of >= 65536 SNPs: 32-bit 2D bins and the exact evaluation (fused table view)."""
+    from sfs2d import _lib as L
+    from sfs2d.engine import ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(1, 150_000, 25, 25, seed=8)
+    ocfg = O.Cfg(25, 25)
+    bgs = O.chrom_backgrounds(p, ocfg)
+    wins, _ = O.snp_windows(p, 70000)
+    _records_vs_oracle(p, ScanConfig(n1p=25, n2p=25, window_mode=L.WINDOW_SNPS, window=70000), ocfg, wins,
+                       lambda c: bgs[c])
+
+
+def _fst_close(a, b):
+    if b is None:
+        return np.isnan(a)
+    return abs(a - b) <= 1e-12 + 1e-10 * abs(b)
+
+
+@pytest.mark.parametrize("n1p,n2p,mode,ws", [(25, 25, "bp", 20000), (18, 14, "bp", 7000), (25, 25, "snps", 500),
+                                             (100, 75, "snps", 500)])
+def test_fst_vs_oracle(n1p, n2p, mode, ws):
+    """Hudson Fst per window (k_scan_w fast path, k_scan_g for the 201x151 grid) against
+    oracle.window_fst (parity of Fst itself is unpinned: the reference has no Fst)."""
+    from sfs2d import _lib as L
+    from sfs2d.engine import Engine, ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(2, [6000, 2500], n1p, n2p, seed=n1p + ws)
+    ocfg = O.Cfg(n1p, n2p)
+    eng = Engine.get(0)
+    dev = eng.upload(p)
+    if mode == "bp":
+        cfg = ScanConfig(n1p=n1p, n2p=n2p, window=ws, fst=True)
+        wins = [(b, e) for (c, s, b, e) in O.bp_windows(p, ws)]
+    else:
+        cfg = ScanConfig(n1p=n1p, n2p=n2p, window_mode=L.WINDOW_SNPS, window=ws, fst=True)
+        wins = [(w[3], w[4]) for w in O.snp_windows(p, ws)[0]]
+    pl = eng.plan(dev, cfg)
+    pl.run()
+    pl.check()
+    recs = pl.read()
+    fst = pl.read_fst()
+    live = (recs["flags"][: len(fst)] & L.W_EMPTY) == 0
+    assert np.all(np.isnan(fst[~live]))
+    got = fst[live]
+    assert len(got) == len(wins)
+    for g, (b, e) in zip(got, wins):
+        assert _fst_close(float(g), O.window_fst(p, np.arange(b, e), ocfg)), (g, b, e)
+    pl.close()

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run one scan configuration a few times (no torch) -- the target of rocprofv3 kernel-trace / PMC runs.
 
-usage: python tools/profile_scan.py [config2|config3|config5] [iters]
+usage: python tools/profile_scan.py [config2|config3|config5] [iters] [fst]
 """
 import os
 import sys
@@ -16,6 +16,7 @@ from sfs2d.synth import synth_genome  # noqa: E402
 
 which = sys.argv[1] if len(sys.argv) > 1 else "config3"
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+fst = len(sys.argv) > 3 and sys.argv[3] == "fst"
 if which == "config2":
     p, cfg = synth_genome(1, 1_000_000, 25, 25, seed=12345), ScanConfig(n1p=25, n2p=25, window=20000)
 elif which == "config3":
@@ -23,6 +24,7 @@ elif which == "config3":
 else:
     p = synth_genome(1, 1_000_000, 100, 75, seed=55)
     cfg = ScanConfig(n1p=100, n2p=75, window_mode=L.WINDOW_SNPS, window=500)
+cfg.fst = fst
 eng = Engine.get(0)
 dev = eng.upload(p)
 pl = eng.plan(dev, cfg)
