@@ -137,6 +137,7 @@ struct sfs2d_plan {
   uint32_t* d_repl = nullptr;
   uint32_t* d_bcount = nullptr;   // per-chromosome inner 2D sums (k_prep -> k_bg_slice)
   uint32_t* d_done = nullptr;     // per-background completion counters of k_bg_slice
+  uint32_t* d_ctr = nullptr;      // k_scan_w window pool counters, 2 parities x nchrom x CTR_POOLS lines
   double* d_bgval = nullptr;
   PL* d_tab = nullptr;
   double* d_lp = nullptr;         // log proportions alone (k_scan_w stages them in LDS)
@@ -184,7 +185,7 @@ int dalloc(sfs2d_ctx* ctx, T** p, size_t count) {
 }
 
 void plan_free(sfs2d_plan* p) {
-  hipFree(p->d_tiles); hipFree(p->d_chunks); hipFree(p->d_slots); hipFree(p->d_repl); hipFree(p->d_bcount);
+  hipFree(p->d_tiles); hipFree(p->d_chunks); hipFree(p->d_slots); hipFree(p->d_repl); hipFree(p->d_bcount); hipFree(p->d_ctr);
   hipFree(p->d_done); hipFree(p->d_bgval); hipFree(p->d_tab); hipFree(p->d_lp); hipFree(p->d_head);
   hipFree(p->d_bg1d); hipFree(p->d_leafsum); hipFree(p->d_leaves); hipFree(p->d_nodes); hipFree(p->d_slices);
   hipFree(p->d_out); hipFree(p->d_err); hipFree(p->d_bins); hipFree(p->d_fst); hipFree(p->d_fsum);
@@ -200,7 +201,8 @@ void launch_scan_w(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
                      pl->ctx->stream, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
                      per_chrom, pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, bp, pl->d_repl, pl->d_bcount,
                      plan_par(pl), pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels,
-                     pl->extra_rec >= 0 ? (int)pl->last_chrom : -1, pl->d_fsum, pl->d_fst);
+                     pl->extra_rec >= 0 ? (int)pl->last_chrom : -1, pl->d_fsum, pl->d_fst, pl->d_ctr,
+                     (int)(pl->runs & 1));
 }
 
 template <bool P16, bool FST>
@@ -578,34 +580,58 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
     hipFuncSetAttribute((const void*)k_scan_extra<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->extra_lds);
   }
 
-  // scan chunks (window slots of one chromosome per workgroup).  k_scan_w: every workgroup
-  // resident at once (one dispatch wave, no tail), chunk length a multiple of its 8 wavefronts,
-  // as short as that allows; k_scan_g: two windows per workgroup.
-  uint32_t CH = 2;
+  // scan work items.  k_scan_w: about one workgroup per resident slot (one dispatch wave, no
+  // tail), shared among the chromosomes by window count; each wavefront takes one static window,
+  // then windows from its chromosome's pool counters until they run dry (windows cost up to ~3x
+  // each other, so static chunks left the slowest workgroups 2x behind the median).
+  // k_scan_g: two windows per workgroup.
   if (pl->G == WAVE) {
     int occ = 0;
     const hipError_t oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<true, true, false>, SBLOCK, pl->scan_lds)
                                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<false, true, false>, SBLOCK, pl->scan_lds);
     if (oe != hipSuccess || occ < 1) occ = 1;
-    const int64_t cap = (int64_t)occ * ctx->ncu;
-    auto nchunks = [&](uint32_t L) {
-      int64_t t = 0;
-      for (int c = 0; c < nc; ++c) t += (int64_t)((slot_base[c + 1] - slot_base[c] + L - 1) / L);
-      return t;
-    };
-    CH = SBLOCK / WAVE;
-    if (const char* ev = std::getenv("SFS2D_CHUNK")) CH = std::max<uint32_t>(8, (uint32_t)std::atoi(ev) & ~7u);   // tuning
-    while (nchunks(CH) > cap) CH += SBLOCK / WAVE;
-  }
-  for (int c = 0; c < nc; ++c) {
-    for (unsigned long long s = slot_base[c]; s < slot_base[c + 1]; s += CH) {
-      Chunk ch{};
-      ch.chrom = (uint32_t)c; ch.slot_lo = (uint32_t)s;
-      ch.slot_hi = (uint32_t)std::min<unsigned long long>(s + CH, slot_base[c + 1]);
-      ch.wid_lo = (uint32_t)(s - slot_base[c]);
-      ch.cb = (uint32_t)data->chrom_off[c];
-      pl->chunks.push_back(ch);
+    int64_t cap = (int64_t)occ * ctx->ncu;
+    if (const char* ev = std::getenv("SFS2D_WGS")) cap = std::max<int64_t>(1, std::atoll(ev));   // tuning
+    const double S = (double)std::max<unsigned long long>(1, slot_base[nc] - slot_base[0]);
+    constexpr uint32_t NW = SBLOCK / WAVE;
+    std::vector<double> order;
+    for (int c = 0; c < nc; ++c) {
+      const uint32_t ns = (uint32_t)(slot_base[c + 1] - slot_base[c]);
+      if (!ns) continue;
+      const uint32_t wmax = (ns + NW - 1) / NW;
+      const uint32_t nwg = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(wmax, std::llround(cap * (ns / S))));
+      uint32_t npool = std::min<uint32_t>(nwg, CTR_POOLS);
+      if (const char* ev = std::getenv("SFS2D_POOLS")) npool = std::max(1u, std::min<uint32_t>(npool, (uint32_t)std::atoi(ev)));   // tuning
+      for (uint32_t k = 0; k < nwg; ++k) {
+        Chunk ch{};
+        ch.chrom = (uint32_t)c; ch.slot_lo = (uint32_t)slot_base[c]; ch.slot_hi = (uint32_t)slot_base[c + 1];
+        ch.wid_lo = 0; ch.cb = (uint32_t)data->chrom_off[c];
+        ch.first = k * NW; ch.nstatic = nwg * NW; ch.pool = npool | ((k % npool) << 16);
+        pl->chunks.push_back(ch);
+        order.push_back((k + 0.5) / nwg);
+      }
     }
+    // spread every chromosome's workgroups evenly over the grid: the first ~ncu workgroups are the
+    // older of the two on their CU (issue priority), so a chromosome made only of younger ones
+    // finished ~25% later than one of older ones; mixed, each pool drains at the common rate
+    std::vector<size_t> idx(pl->chunks.size());
+    for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
+    std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return order[a] < order[b]; });
+    std::vector<Chunk> sorted(idx.size());
+    for (size_t i = 0; i < idx.size(); ++i) sorted[i] = pl->chunks[idx[i]];
+    pl->chunks.swap(sorted);
+  } else {
+    constexpr uint32_t CH = 2;
+    for (int c = 0; c < nc; ++c)
+      for (unsigned long long s = slot_base[c]; s < slot_base[c + 1]; s += CH) {
+        Chunk ch{};
+        ch.chrom = (uint32_t)c; ch.slot_lo = (uint32_t)s;
+        ch.slot_hi = (uint32_t)std::min<unsigned long long>(s + CH, slot_base[c + 1]);
+        ch.wid_lo = (uint32_t)(s - slot_base[c]);
+        ch.cb = (uint32_t)data->chrom_off[c];
+        ch.nstatic = ch.slot_hi - ch.slot_lo; ch.pool = 1;
+        pl->chunks.push_back(ch);
+      }
   }
   pl->last_chrom = last_c;
 
@@ -670,6 +696,8 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
   rc = rc ? rc : dalloc(ctx, &pl->d_repl, nrepl);
   rc = rc ? rc : dalloc(ctx, &pl->d_bcount, (size_t)2 * std::max(1, nc));
   rc = rc ? rc : dalloc(ctx, &pl->d_done, (size_t)pl->nbg);
+  const size_t nctr = (size_t)2 * std::max(1, nc) * CTR_POOLS * CTR_STRIDE;
+  rc = rc ? rc : dalloc(ctx, &pl->d_ctr, nctr);
   rc = rc ? rc : dalloc(ctx, &pl->d_bgval, (size_t)pl->nbg * K.nt);
   rc = rc ? rc : dalloc(ctx, &pl->d_tab, (size_t)pl->nbg * K.nt);
   rc = rc ? rc : dalloc(ctx, &pl->d_lp, (size_t)pl->nbg * K.nt);
@@ -698,6 +726,7 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
   if (e == hipSuccess && pl->do_bg) e = hipMemsetAsync(pl->d_repl, 0, sizeof(uint32_t) * nrepl, st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_bcount, 0, sizeof(uint32_t) * 2 * std::max(1, nc), st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_done, 0, sizeof(uint32_t) * pl->nbg, st);
+  if (e == hipSuccess) e = hipMemsetAsync(pl->d_ctr, 0, sizeof(uint32_t) * nctr, st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_err, 0, 4 * sizeof(uint32_t), st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_bins, 0, sizeof(uint32_t) * nbins, st);
   if (e == hipSuccess && pl->fst) e = hipMemsetAsync(pl->d_fsum, 0, sizeof(unsigned long long) * 2 * ((size_t)pl->nslots + 1), st);
@@ -858,9 +887,12 @@ int sfs2d_plan_check(sfs2d_plan* pl) {
 // diagnostic: stamps of a -DSFS2D_STAMPS build (returns SFS2D_E_ARG in the shipped build)
 int sfs2d__debug_stamps(unsigned long long* out64) {
 #ifdef SFS2D_STAMPS
-  // 64 phase stamps, then per-block (start, end) of k_prep and k_scan_w (2 x 4096 x 2)
+  // 64 phase stamps, then per-block (start, end) of k_prep and k_scan_w (2 x 4096 x 2), then per wave
   if (hipMemcpyFromSymbol(out64, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 64) != hipSuccess) return SFS2D_E_HIP;
   if (hipMemcpyFromSymbol(out64 + 64, HIP_SYMBOL(g_blk), sizeof(unsigned long long) * 2 * 4096 * 2) != hipSuccess)
+    return SFS2D_E_HIP;
+  // then k_scan_w per wavefront (end, windows): 4096 x 8 x 2
+  if (hipMemcpyFromSymbol(out64 + 64 + 2 * 4096 * 2, HIP_SYMBOL(g_wv), sizeof(unsigned long long) * 4096 * 8 * 2) != hipSuccess)
     return SFS2D_E_HIP;
   return 0;
 #else

@@ -99,12 +99,18 @@ struct Tile {   // k_prep work item: SNPs [begin, end) of chromosome chrom = [cb
   uint32_t chrom, begin, end, cb, ce, sbase, nslots, pad1;   // nslots: the chromosome's window slots
 };
 
+constexpr int CTR_POOLS = 8;     // k_scan_w dynamic window pools per chromosome
+constexpr int CTR_STRIDE = 16;   // one 64-B line per pool counter
 constexpr int FST_LDS = 256;             // k_prep: windows per tile accumulated in LDS (others: global)
 constexpr int FST_R = 4;                 // ... in FST_R interleaved copies (lane & 3) to spread same-window atomics
 constexpr double FST_SCALE = 1099511627776.0;   // 2^40: Fst sums as int64 fixed point (deterministic atomics)
 
 struct Chunk {  // k_scan work item: window slots [slot_lo, slot_hi) of one chromosome
-  uint32_t chrom, slot_lo, slot_hi, wid_lo, cb, pad0, pad1, pad2;
+  uint32_t chrom, slot_lo, slot_hi, wid_lo, cb;
+  // k_scan_w (slot_lo..slot_hi = the whole chromosome, wid_lo = 0): wavefront w's first window is
+  // slot_lo + first + w; the windows from slot_lo + nstatic on are taken dynamically from `npool`
+  // interleaved pools (pool p: nstatic + p + npool * j), this workgroup drawing from pool `pool`
+  uint32_t first, nstatic, pool;   // pool: npool | pool << 16
 };
 
 struct PL {     // per-bin background table entry
@@ -143,7 +149,18 @@ __device__ unsigned long long g_blk[2][4096][2];   // per-block start / end (k_p
   do {                                                                                           \
     if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[i] = __builtin_amdgcn_s_memrealtime();     \
   } while (0)
+__device__ unsigned long long g_wv[4096 * 8][2];   // k_scan_w per wavefront: end, windows scanned
+#define WV_STAMP(n)                                                                              \
+  do {                                                                                           \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096) {                                          \
+      g_wv[blockIdx.x * 8 + (threadIdx.x >> 6)][0] = __builtin_amdgcn_s_memrealtime();           \
+      g_wv[blockIdx.x * 8 + (threadIdx.x >> 6)][1] = (n);                                        \
+    }                                                                                            \
+  } while (0)
 #else
+#define WV_STAMP(n) \
+  do {              \
+  } while (0)
 #define STAMP(i) \
   do {           \
   } while (0)
@@ -1267,7 +1284,8 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
                                                    const int2* __restrict__ leaves, int nleaves,
                                                    const int4* __restrict__ nodes, int nnodes, int nlevels,
                                                    int write_chrom, unsigned long long* __restrict__ fsum,
-                                                   double* __restrict__ fst_out) {
+                                                   double* __restrict__ fst_out, uint32_t* __restrict__ ctr,
+                                                   int cpar) {
   extern __shared__ double ldsd[];
   __shared__ BgHead sh_hb;
   STAMP(10);
@@ -1308,9 +1326,19 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
       w.v1 = ld4(bins, i0 + 4 * WAVE, w.e);
     }
   };
-  uint32_t s = ch.slot_lo + wv;
+  // window schedule: one static window per wavefront, then the chromosome's pool counters (an
+  // atomic is always one window ahead of its use, so its latency hides under a window's work)
+  uint32_t s = ch.slot_lo + ch.first + wv;
   const bool active = s < ch.slot_hi;
   const uint2 sr0 = (active && mode_bp) ? slots[s] : make_uint2(0, 0);   // in flight during the table work
+  const uint32_t npool = ch.pool & 0xffffu, pool = ch.pool >> 16;
+  const bool dyn = ch.slot_lo + ch.nstatic < ch.slot_hi;
+  const uint32_t dbase = ch.slot_lo + ch.nstatic + pool;
+  uint32_t* myctr = ctr + (((size_t)cpar * P.nchrom + ch.chrom) * CTR_POOLS + pool) * CTR_STRIDE;
+  uint32_t gq = 0;
+  if (active && dyn && lane == 0) gq = atomicAdd(myctr, 1u);
+  if (blockIdx.x == 0)   // the other parity's counters, for the next run
+    for (int k = tid; k < P.nchrom * CTR_POOLS; k += SBLOCK) ctr[((size_t)(1 - cpar) * P.nchrom * CTR_POOLS + k) * CTR_STRIDE] = 0u;
 
   for (int k = tid; k < 2 * LNT; k += SBLOCK) Dt[k] = dfg[k];
   BgHead hb;
@@ -1322,7 +1350,7 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
     hb = head[bg];
   } else {
     fused_table(P.nb2, P.nh, P.nt, P.n1p, P.n2p, P.n1, P.n2, P.t1a, P.t1b, P.nchrom, ch.chrom,
-                ch.wid_lo == 0 && (int)ch.chrom == write_chrom, bg,
+                ch.first == 0 && (int)ch.chrom == write_chrom, bg,
                 Rc, rs, repl, bcount, par, tab, LPg, head, LPl, HB, leaves, nleaves, nodes, nnodes, nlevels, lnx,
                 &sh_hb);
     hb = sh_hb;
@@ -1356,8 +1384,14 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
   bounds(s, sr0, cur);
   STAMP(11);
   int it = 0;
-  for (; s < ch.slot_hi; s += SBLOCK / WAVE, ++it) {
-    const uint32_t sn = s + SBLOCK / WAVE;
+  uint32_t sn = ch.slot_hi;
+  for (; s < ch.slot_hi; s = sn, ++it) {
+    sn = ch.slot_hi;
+    if (dyn) {
+      const uint32_t j = __builtin_amdgcn_readfirstlane(gq);
+      sn = dbase + npool * j < ch.slot_hi ? dbase + npool * j : ch.slot_hi;
+      if (sn < ch.slot_hi && lane == 0) gq = atomicAdd(myctr, 1u);
+    }
     const bool more = sn < ch.slot_hi;
     const uint2 srn = (mode_bp && more) ? slots[sn] : make_uint2(0, 0);
     const uint32_t wid = ch.wid_lo + (s - ch.slot_lo);
@@ -1501,6 +1535,7 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
     cur = nxt;
   }
   STAMP(15);
+  WV_STAMP(it);
 #ifdef SFS2D_STAMPS
   __builtin_amdgcn_s_barrier();   // diagnostic build only: the block's end is its last active wave's
 #endif

@@ -297,3 +297,28 @@ def test_fst_vs_oracle(n1p, n2p, mode, ws):
     for g, (b, e) in zip(got, wins):
         assert _fst_close(float(g), O.window_fst(p, np.arange(b, e), ocfg)), (g, b, e)
     pl.close()
+
+
+@pytest.mark.parametrize("wgs", ["3", "17"])
+def test_dynamic_window_pools(monkeypatch, wgs):
+    """k_scan_w with few workgroups: most windows come from the per-chromosome pool counters
+    (both counter parities, over repeated runs) and every window is still scanned exactly once."""
+    from sfs2d import _lib as L
+    from sfs2d.engine import Engine, ScanConfig
+    from sfs2d.synth import synth_genome
+    monkeypatch.setenv("SFS2D_WGS", wgs)
+    p = synth_genome(3, [12000, 6000, 5], 25, 25, seed=int(wgs))
+    ocfg = O.Cfg(25, 25)
+    bgs = O.chrom_backgrounds(p, ocfg)
+    for mode, ws in ((L.WINDOW_SNPS, 16), (L.WINDOW_BP, 3000)):
+        cfg = ScanConfig(n1p=25, n2p=25, window_mode=mode, window=ws)
+        wins = O.snp_windows(p, ws)[0] if mode == L.WINDOW_SNPS else O.bp_windows(p, ws)
+        _records_vs_oracle(p, cfg, ocfg, wins, lambda c: bgs[c])
+        eng = Engine.get(0)
+        dev = eng.upload(p)
+        pl = eng.plan(dev, cfg)
+        outs = []
+        for _ in range(3):
+            pl.run()
+            outs.append(pl.read().tobytes())
+        assert outs[0] == outs[1] == outs[2]

@@ -2,6 +2,7 @@
 """Diagnostic: per-phase wall-clock stamps of block 0 of each kernel (needs libsfs2d_stamps.so,
 built with -DSFS2D_STAMPS).  usage: SFS2D_LIB=.../libsfs2d_stamps.so python tools/stamps.py config2"""
 import ctypes as C
+import numpy as np
 import os
 import sys
 
@@ -19,10 +20,11 @@ pl = eng.plan(dev, ScanConfig(n1p=25, n2p=25, window=20000, fst=True))
 for _ in range(3):
     pl.run()
 pl.check()
-buf = (C.c_ulonglong * (64 + 2 * 4096 * 2))()
+buf = (C.c_ulonglong * (64 + 2 * 4096 * 2 + 4096 * 8 * 2))()
 assert L.lib().sfs2d__debug_stamps(buf) == 0
 t = list(buf[:64])
-blk = list(buf[64:])
+blk = list(buf[64:64 + 16384])
+wvs = np.array(buf[64 + 16384:], dtype=np.int64).reshape(4096 * 8, 2)
 def d(a, b):
     return (t[b] - t[a]) * 0.01 if t[a] and t[b] else float("nan")
 print(which, "K1 blk0: zero %.2f  loop %.2f  flush %.2f us" % (d(20, 21), d(21, 22), d(22, 23)))
@@ -37,7 +39,8 @@ print(which, "gaps: K1end->K2start %.2f  K2end->K3start %.2f us" % (d(23, 0), d(
 import numpy as np
 for k, name in ((0, "k_prep"), (1, "k_scan_w")):
     a = np.array(blk[k * 8192:(k + 1) * 8192], dtype=np.int64).reshape(4096, 2)
-    a = a[(a[:, 0] > 0) & (a[:, 1] > 0)]
+    ids = np.nonzero((a[:, 0] > 0) & (a[:, 1] > 0))[0]
+    a = a[ids]
     if not len(a):
         continue
     t0 = a[:, 0].min()
@@ -45,3 +48,22 @@ for k, name in ((0, "k_prep"), (1, "k_scan_w")):
     dur = en - st
     print(which, f"{name}: blocks {len(a)}  start max {st.max():.2f}  end max {en.max():.2f}  "
           f"dur min/med/max {dur.min():.2f}/{np.median(dur):.2f}/{dur.max():.2f} us")
+    # end time by blockIdx % 8 (the usual XCD round robin)
+    print(which, f"{name}: end by block%8 (mean/max):",
+          " ".join(f"{en[ids % 8 == x].mean():.0f}/{en[ids % 8 == x].max():.0f}" for x in range(8)))
+    q = np.percentile(en, [10, 50, 90])
+    print(which, f"{name}: end p10/p50/p90 {q[0]:.1f}/{q[1]:.1f}/{q[2]:.1f} us")
+
+# k_scan_w per wavefront: windows scanned and end time; per chromosome (blocks grouped by chunk order)
+nb = len([1 for i in range(4096) if blk[8192 + 2 * i] > 0])
+w = wvs[: nb * 8]
+live = w[:, 0] > 0
+t0 = np.array(blk[8192:8192 + 2 * nb:2], dtype=np.int64).min()
+en = (w[:, 0] - t0) * 0.01
+print(which, f"k_scan_w waves: {live.sum()}  windows/wave min/med/max {w[live,1].min()}/{int(np.median(w[live,1]))}/{w[live,1].max()}"
+      f"  end min/med/max {en[live].min():.1f}/{np.median(en[live]):.1f}/{en[live].max():.1f} us")
+if which != "config2":
+    # workgroups are interleaved over the grid: block b scans chromosome b % 32 (equal chromosomes)
+    chrom = (np.arange(nb * 8) // 8) % 32
+    ce = [(en[chrom == c].min(), en[chrom == c].max(), int(w[chrom == c, 1].sum())) for c in range(32)]
+    print(which, "per chromosome end min-max / windows:", " ".join(f"{a:.0f}-{b:.0f}/{n}" for a, b, n in ce))
