@@ -707,7 +707,7 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
   rc = rc ? rc : dalloc(ctx, &pl->d_leaves, pw.leaves.size());
   rc = rc ? rc : dalloc(ctx, &pl->d_nodes, pw.nodes.size());
   rc = rc ? rc : dalloc(ctx, &pl->d_slices, pl->slices.size());
-  const size_t nbins = ((size_t)data->n + 3) / 4 * 4 + 64;   // 16-B vector reads may overhang n
+  const size_t nbins = ((size_t)data->n + 3) / 4 * 4 + SCAN_PAD;   // k_scan_w's step loads overhang n
   rc = rc ? rc : dalloc(ctx, &pl->d_bins, nbins);
   rc = rc ? rc : dalloc(ctx, &pl->d_out, (size_t)pl->nrec);
   rc = rc ? rc : dalloc(ctx, &pl->d_err, 4);

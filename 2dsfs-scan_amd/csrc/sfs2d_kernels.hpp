@@ -99,6 +99,7 @@ struct Tile {   // k_prep work item: SNPs [begin, end) of chromosome chrom = [cb
   uint32_t chrom, begin, end, cb, ce, sbase, nslots, pad1;   // nslots: the chromosome's window slots
 };
 
+constexpr int SCAN_PAD = 512;   // readable words past the end of the per-SNP bins (k_scan_w prefetch)
 constexpr int CTR_POOLS = 8;     // k_scan_w dynamic window pools per chromosome
 constexpr int CTR_STRIDE = 16;   // one 64-B line per pool counter
 constexpr int FST_LDS = 256;             // k_prep: windows per tile accumulated in LDS (others: global)
@@ -226,6 +227,16 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
+// s2 = sum of a over the wave; sa / sb = sums of b over lanes 0-31 / 32-63
+__device__ __forceinline__ void wave_sum_dpp_halves(double a, double b, double& s2, double& sa, double& sb) {
+  a += dpp_d<0xB1>(a);  b += dpp_d<0xB1>(b);
+  a += dpp_d<0x4E>(a);  b += dpp_d<0x4E>(b);
+  a += dpp_d<0x141>(a); b += dpp_d<0x141>(b);
+  a += dpp_d<0x140>(a); b += dpp_d<0x140>(b);
+  s2 = (readlane_d(a, 0) + readlane_d(a, 16)) + (readlane_d(a, 32) + readlane_d(a, 48));
+  sa = readlane_d(b, 0) + readlane_d(b, 16);
+  sb = readlane_d(b, 32) + readlane_d(b, 48);
+}
 __device__ __forceinline__ double wave_sum_dpp(double v) {
   v += dpp_d<0xB1>(v);    // quad_perm [1,0,3,2]
   v += dpp_d<0x4E>(v);    // quad_perm [2,3,0,1]
@@ -1054,7 +1065,7 @@ __device__ __forceinline__ double fst_take(unsigned long long* fsum, size_t s) {
 
 struct Win {
   uint32_t b, e;
-  uint4 v0, v1;   // bins of the first chunk (SNPs [b & ~3, +512))
+  uint32_t u[8];   // bins of this lane's first 8 SNPs, b + lane + 64 j (0 past e)
   bool has;
 };
 
@@ -1320,10 +1331,10 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
       w.b = ch.cb + (ch.wid_lo + (s - ch.slot_lo)) * P.ws;
       w.e = w.b + P.ws;
     }
-    if (w.has) {
-      const uint32_t i0 = (w.b & ~3u) + 4 * lane;
-      w.v0 = ld4(bins, i0, w.e);
-      w.v1 = ld4(bins, i0 + 4 * WAVE, w.e);
+    if (w.has) {   // the bins buffer has SCAN_PAD readable words past n; masked in the last step
+      const uint32_t* q = bins + w.b + lane;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w.u[j] = q[64 * j];
     }
   };
   // window schedule: one static window per wavefront, then the chromosome's pool counters (an
@@ -1356,16 +1367,10 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
     hb = sh_hb;
   }
   for (int k = lane; k < per / 4; k += WAVE) reinterpret_cast<uint4*>(W)[k] = make_uint4(0, 0, 0, 0);
-  // lp of the 1D bins owned by this lane in the per-bin pass (bins 1+lane, 65+lane)
+  if (tid == 0) LPl[0] = 0.0;   // bin 0 ((0,0), never counted): excluded SNPs read it and add 0
   __syncthreads();
-  double lpa[2], lpb[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int k = 1 + lane + WAVE * j;
-    lpa[j] = k <= P.n1p - 1 ? LPl[P.t1a + k] : 0.0;
-    lpb[j] = k <= P.n2p - 1 ? LPl[P.t1b + k] : 0.0;
-  }
   const bool filt = P.ann_want >= 0;
+  const bool half1d = P.n1p <= 33 && P.n2p <= 33;
   const uint32_t zflags = bg_zero_flags(hb);
   const bool nan2 = hb.flags & BGF_NAN2, nan1a = hb.flags & BGF_NAN1A, nan1b = hb.flags & BGF_NAN1B;
 
@@ -1380,6 +1385,10 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
       for (int c = tid; c < P.nchrom; c += SBLOCK) bcount[(size_t)(1 - par) * P.nchrom + c] = 0u;
   }
   if (!active) return;
+  const uint32_t one1 = P16 ? 0x10000u : 1u;   // 1D increment (P16: counts in the upper halves)
+  uint32_t* const H1a_l = H1a + rep;            // this lane's replica column of the 1D histograms
+  uint32_t* const H1b_l = H1b + rep;
+  uint32_t* const T_l = W + trash;
   Win cur;
   bounds(s, sr0, cur);
   STAMP(11);
@@ -1404,62 +1413,94 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
       cur = nxt;
       continue;
     }
-    // per-lane counters, two 16-bit fields each: {n2 | nlast}, {n1a | n1b}, nvar (a lane sees at
-    // most 1/64 of a window; windows of >= LNX_N SNPs are recounted on the exact path)
-    uint32_t cA = 0, cB = 0, cV = 0;
+    // SNP j of this lane is b + lane + 64 j: steps of 64 SNPs in pairs, the first 8 steps from the
+    // prefetched registers (a step wholly past e is skipped; SNPs past e are w = 0, i.e. excluded).
+    // Counters are wave-uniform ballot counts.  Excluded SNPs (k2 = 0) add 0 to the lane's trash
+    // word, whose lower half therefore stays 0 and gives rank 0, D(0) = 0 and LPl[0] = 0; the 1D
+    // atomics add to the upper halves (P16), so a 1D increment landing in the trash cannot disturb it.
+    const uint32_t nsnp = cur.e - cur.b;
+    const int lim = (int)nsnp - lane;
+
     double acc2 = 0.0;
-    uint32_t kw[8];   // the first chunk's 2D words, cleared after the window
-    const uint32_t a0 = cur.b & ~3u;
-    const bool one_chunk = cur.e <= a0 + 8 * WAVE;
-    bool ov = false;   // some SNP's rank in its 2D bin reached LNT (only in windows > LNT SNPs)
-    for (uint32_t base = a0; base < cur.e; base += 8 * WAVE) {
-      const uint32_t i0 = base + 4 * lane, i1 = i0 + 4 * WAVE;
-      const uint4 c0 = base == a0 ? cur.v0 : ld4(bins, i0, cur.e);
-      const uint4 c1 = base == a0 ? cur.v1 : ld4(bins, i1, cur.e);
-      const uint32_t cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-      // two halves of four SNPs: atomics, then every table read of the half, then the sums
+    uint32_t n2 = 0, nlast = 0, n1a = 0, n1b = 0, nvar = 0;
+    uint32_t kw[8];   // the 2D words of the first 8 steps, cleared after the window
+    auto pair = [&](uint32_t w0, uint32_t w1, int j, bool keep) {
+      if (64 * (j + 2) > (int)nsnp) {   // the window's last steps: SNPs past e are excluded
+        w0 = 64 * j < lim ? w0 : 0u;
+        w1 = 64 * (j + 1) < lim ? w1 : 0u;
+      }
+      const uint32_t ww[2] = {w0, w1};
+      uint32_t rk[2], kk[2];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        uint32_t rk[4], kk[4];
+      for (int q = 0; q < 2; ++q) {
+        const uint32_t w = ww[q];
+        const uint32_t k2 = bin_k2(w), g1 = bin_g1(w), g2 = bin_g2(w);
+        n2 += __popcll(__ballot(k2 != 0u));
+        n1a += __popcll(__ballot(g1 != 0u));
+        n1b += __popcll(__ballot(g2 != 0u));
+        const uint32_t word = k2 ? (P16 ? (k2 >> 1) : k2) : trash;
+        const uint32_t sh = P16 ? ((k2 & 1u) << 4) : 0u;
+        const uint32_t old = atomicAdd(&W[word], k2 ? (1u << sh) : 0u);
+        rk[q] = P16 ? __builtin_amdgcn_ubfe(old, sh, 16) : (k2 ? old : 0u);
+        kk[q] = k2;
+        if (keep) kw[(j + q) & 7] = word;
+        atomicAdd(g1 ? H1a_l + g1 * R1 : T_l, one1);
+        atomicAdd(g2 ? H1b_l + g2 * R1 : T_l, one1);
+      }
+      double d[2], lp[2];
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const int j = 4 * h + jj;
-          const uint32_t i = (h ? i1 : i0) + jj;
-          const uint32_t w = (i >= cur.b && i < cur.e) ? cc[j] : 0u;   // the vectors overhang [b, e)
-          const uint32_t k2 = bin_k2(w), g1 = bin_g1(w), g2 = bin_g2(w);
-          cA += (k2 ? 1u : 0u) + ((w >> 15) & 0x10000u);
-          cB += (g1 ? 1u : 0u) + (g2 ? 0x10000u : 0u);
-          cV += (w >> 30) & 1u;
-          const uint32_t word = k2 ? (P16 ? (k2 >> 1) : k2) : trash;
-          const uint32_t sh = P16 ? ((k2 & 1) << 4) : 0u;
-          const uint32_t old = atomicAdd(&W[word], 1u << sh);
-          rk[jj] = k2 ? (P16 ? ((old >> sh) & 0xffffu) : old) : 0u;   // the trash word's value is junk
-          kk[jj] = k2;
-          if (base == a0) kw[j] = word;
-          atomicAdd(&W[g1 ? (uint32_t)(h2w + g1 * R1 + rep) : trash], 1u);
-          atomicAdd(&W[g2 ? (uint32_t)(h2w + h1w + g2 * R1 + rep) : trash], 1u);
-        }
-        double d[4], lp[4];
+      for (int q = 0; q < 2; ++q) {
+        d[q] = Dt[min(rk[q], (uint32_t)LNT - 1u)];   // D[LNT-1] = 0: ranks past the table add 0
+        lp[q] = LPl[kk[q]];
+      }
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          d[jj] = Dt[min(rk[jj], (uint32_t)LNT - 1u)];   // D[LNT-1] = 0: ranks past the table add 0
-          lp[jj] = LPl[kk[jj]];
-        }
+      for (int q = 0; q < 2; ++q) acc2 += d[q] - lp[q];
+    };
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          ov |= rk[jj] >= (uint32_t)(LNT - 1);
-          acc2 += kk[jj] ? d[jj] - lp[jj] : 0.0;
-        }
+    for (int j = 0; j < 8; j += 2)
+      if (64 * j < (int)nsnp) pair(cur.u[j], cur.u[j + 1], j, true);
+    if (nsnp > 8 * WAVE) {
+      const uint32_t* qb = bins + cur.b + lane;
+      uint32_t x0 = 64 * 8 < lim ? qb[64 * 8] : 0u, x1 = 64 * 9 < lim ? qb[64 * 9] : 0u;
+      for (int j = 8; 64 * j < (int)nsnp; j += 2) {
+        const uint32_t w0 = x0, w1 = x1;
+        x0 = 64 * (j + 2) < lim ? qb[64 * (j + 2)] : 0u;   // one pair ahead
+        x1 = 64 * (j + 3) < lim ? qb[64 * (j + 3)] : 0u;
+        pair(w0, w1, j, false);
       }
     }
+    if (!P.fold || filt) {   // rare settings: unfolded (SNPs in the excluded last 2D bin), variant_type filter
+      for (uint32_t i0 = cur.b; i0 < cur.e; i0 += WAVE) {   // wave-uniform trip count
+        const uint32_t w = i0 + lane < cur.e ? bins[i0 + lane] : 0u;
+        nlast += __popcll(__ballot((w & B_LAST) != 0u));
+        nvar += __popcll(__ballot((w & B_VAR) != 0u));
+      }
+    }
+    if (!filt) nvar = nsnp;
+    ulonglong2 fq = make_ulonglong2(0ull, 0ull);   // this window's Fst sums (k_prep), used at the end
+    if (FST && lane == 0) fq = reinterpret_cast<const ulonglong2*>(fsum)[s];
+    const bool ov = nsnp > (uint32_t)(LNT - 1);   // some rank may have passed the D table
     if (it == 0) STAMP(12);
-    // next window: its slot record is in, issue its first chunk now
+    // next window: its slot record is in, issue its first steps now
     Win nxt;
     nxt.has = false;
     if (more) bounds(sn, srn, nxt);
     group_sync<WAVE>();
-    // 1D spectra: one lane per folded inner bin reads (and clears) its R1 replicas
+    // 1D spectra: one lane per folded inner bin reads (and clears) its R1 replicas; with <= 32 inner
+    // bins per population, lanes 0-31 take population 1 and lanes 32-63 population 2 (acca)
     double acca = 0.0, accb = 0.0;
+    constexpr uint32_t S1 = P16 ? 16u : 0u;
+    if (half1d) {
+      const bool pa = lane < 32;
+      const int k = 1 + (lane & 31);
+      if (k <= (pa ? P.n1p : P.n2p) - 1) {
+        uint4* q = reinterpret_cast<uint4*>((pa ? H1a : H1b) + k * R1);
+        const uint4 v = *q;
+        *q = make_uint4(0, 0, 0, 0);
+        const uint32_t x = (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
+        acca = x ? xlnx(x, Ft, lnx) - (double)x * LPl[(pa ? P.t1a : P.t1b) + k] : 0.0;
+      }
+    } else
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int k = 1 + lane + WAVE * j;
@@ -1467,19 +1508,19 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
         uint4* q = reinterpret_cast<uint4*>(H1a + k * R1);
         const uint4 v = *q;
         *q = make_uint4(0, 0, 0, 0);
-        const uint32_t x = v.x + v.y + v.z + v.w;
-        acca += x ? xlnx(x, Ft, lnx) - (double)x * lpa[j] : 0.0;
+        const uint32_t x = (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
+        acca += x ? xlnx(x, Ft, lnx) - (double)x * LPl[P.t1a + k] : 0.0;
       }
       if (k <= P.n2p - 1) {
         uint4* q = reinterpret_cast<uint4*>(H1b + k * R1);
         const uint4 v = *q;
         *q = make_uint4(0, 0, 0, 0);
-        const uint32_t x = v.x + v.y + v.z + v.w;
-        accb += x ? xlnx(x, Ft, lnx) - (double)x * lpb[j] : 0.0;
+        const uint32_t x = (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
+        accb += x ? xlnx(x, Ft, lnx) - (double)x * LPl[P.t1b + k] : 0.0;
       }
     }
     // bins with x > LNT-1 SNPs: the ranks from LNT-1 on add F(x) - F(LNT-1) (read before the clear)
-    if (__ballot(ov)) {
+    if (ov) {
       constexpr uint32_t L1 = LNT - 1;
       const double fl = Ft[L1];
       for (int k = lane; k < h2w; k += WAVE) {
@@ -1490,19 +1531,21 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
       }
     }
     // clear the 2D words this window touched
-    if (one_chunk) {
+    if (nsnp <= 8 * WAVE) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) W[kw[j]] = 0u;
+      for (int j = 0; j < 8; ++j)
+        if (64 * j < (int)nsnp) W[kw[j]] = 0u;
     } else {
       uint4* q = reinterpret_cast<uint4*>(W);
       for (int k = lane; k < h2w / 4; k += WAVE) q[k] = make_uint4(0, 0, 0, 0);
     }
     if (it == 0) STAMP(13);
-    const double s2 = wave_sum_dpp(acc2), sa = wave_sum_dpp(acca), sb = wave_sum_dpp(accb);
-    cA = wave_sum_dpp_u(cA);
-    cB = wave_sum_dpp_u(cB);
-    const uint32_t n2 = cA & 0xffffu, nlast = cA >> 16, n1a = cB & 0xffffu, n1b = cB >> 16;
-    const uint32_t nvar = filt ? wave_sum_dpp_u(cV) : cur.e - cur.b;
+    double s2, sa, sb;
+    if (half1d) {
+      wave_sum_dpp_halves(acc2, acca, s2, sa, sb);
+    } else {
+      s2 = wave_sum_dpp(acc2); sa = wave_sum_dpp(acca); sb = wave_sum_dpp(accb);
+    }
     WinOut w;
     w.snp_count = nvar; w.n2_all = n2 + nlast; w.n2 = n2; w.n1a = n1a; w.n1b = n1b;
     w.t2d = 2.0 * (s2 - xlnx(n2, Ft, lnx));
@@ -1525,7 +1568,10 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
       if (nan1a) w.t1a = __builtin_nan("");
       if (nan1b) w.t1b = __builtin_nan("");
     }
-    if (FST && lane == 0) fst_out[s] = fst_take(fsum, s);
+    if (FST && lane == 0) {
+      fst_out[s] = fq.y != 0 ? (double)(long long)fq.x / (double)(long long)fq.y : __builtin_nan("");
+      reinterpret_cast<ulonglong2*>(fsum)[s] = make_ulonglong2(0ull, 0ull);
+    }
     if (lane == 0) {
       write_rec(out + s, ch.chrom, wid, cur.b, cur.e, w, zflags);
       if (mode_bp) slots[s] = make_uint2(0u, 0u);   // leave the slot table clean for the next run
