@@ -37,6 +37,7 @@
 //   k_scan_extra  combined_scan's final-window helper (quirk Q9).
 #pragma once
 
+#include <type_traits>
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -102,8 +103,14 @@ struct Tile {   // k_prep work item: SNPs [begin, end) of chromosome chrom = [cb
 constexpr int SCAN_PAD = 512;   // readable words past the end of the per-SNP bins (k_scan_w prefetch)
 constexpr int CTR_POOLS = 8;     // k_scan_w dynamic window pools per chromosome
 constexpr int CTR_STRIDE = 16;   // one 64-B line per pool counter
-constexpr int FST_LDS = 256;             // k_prep: windows per tile accumulated in LDS (others: global)
-constexpr int FST_R = 4;                 // ... in FST_R interleaved copies (lane & 3) to spread same-window atomics
+#ifndef SFS2D_FST_LDS
+#define SFS2D_FST_LDS 256
+#endif
+#ifndef SFS2D_FST_R
+#define SFS2D_FST_R 4
+#endif
+constexpr int FST_LDS = SFS2D_FST_LDS;             // k_prep: windows per tile accumulated in LDS (others: global)
+constexpr int FST_R = SFS2D_FST_R;                 // ... in FST_R interleaved copies (lane & 3) to spread same-window atomics
 constexpr double FST_SCALE = 1099511627776.0;   // 2^40: Fst sums as int64 fixed point (deterministic atomics)
 
 struct Chunk {  // k_scan work item: window slots [slot_lo, slot_hi) of one chromosome
@@ -323,6 +330,38 @@ __device__ __forceinline__ uint32_t classify(const KParams& P, uint32_t c, bool 
          (var_ok ? B_VAR : 0u) | (last ? B_LAST : 0u);
 }
 
+// a wave-uniform value held in a VGPR: k_prep's per-SNP code reads a dozen parameters, and as
+// scalars they (with the lane masks of four unrolled SNPs) overflow the SGPR file into v_readlane
+// reloads inside the loop
+__device__ __forceinline__ int vreg(int x) {
+  int r;
+  asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
+  return r;
+}
+__device__ __forceinline__ unsigned int vreg(unsigned int x) { return (unsigned int)vreg((int)x); }
+
+// classify() for counts inside the grid (r1 + a1 <= n1 and r2 + a2 <= n2, so no out-of-grid key and
+// no KeyError): the same word from fewer, branch-free operations.  x1 = x2 = 0 iff k2 = 0; with
+// a1 <= n1, 1 <= min(a1, n1 - a1) <= n1p - 1 is exactly the v1a condition of classify().
+__device__ __forceinline__ uint32_t classify_fast(const KParams& P, uint32_t c, bool var_ok, bool pos_ok, int& k2all,
+                                                 int& u1a, int& u1b) {
+  const uint32_t r1 = c & 0xffu, a1 = (c >> 8) & 0xffu, r2 = (c >> 16) & 0xffu, a2 = c >> 24;
+  const bool pass = var_ok & pos_ok;
+  const bool sw = (int)(a1 + a2) > P.fold_thr;
+  const uint32_t x1 = sw ? r1 : a1, x2 = sw ? r2 : a2;
+  const uint32_t k2 = x1 * (uint32_t)(P.n2 + 1) + x2;
+  const bool in2 = pass & (k2 != 0u);
+  const bool last = in2 & (k2 == (uint32_t)(P.nb2 - 1));
+  const uint32_t g1 = min(a1, (uint32_t)P.n1 - a1), g2 = min(a2, (uint32_t)P.n2 - a2);
+  const bool v1a = pass & (g1 - 1u < (uint32_t)(P.n1p - 1));
+  const bool v1b = pass & (g2 - 1u < (uint32_t)(P.n2p - 1));
+  k2all = in2 ? (int)k2 : -1;
+  u1a = (pass & (a1 != 0u)) ? (int)a1 : -1;
+  u1b = (pass & (a2 != 0u)) ? (int)a2 : -1;
+  return ((in2 & !last) ? k2 : 0u) | ((v1a ? g1 : 0u) << 16) | ((v1b ? g2 : 0u) << 23) | (var_ok ? B_VAR : 0u) |
+         (last ? B_LAST : 0u);
+}
+
 __device__ __forceinline__ uint32_t bin_k2(uint32_t w) { return w & 0xffffu; }
 __device__ __forceinline__ uint32_t bin_g1(uint32_t w) { return (w >> 16) & 0x7fu; }
 __device__ __forceinline__ uint32_t bin_g2(uint32_t w) { return (w >> 23) & 0x7fu; }
@@ -346,17 +385,27 @@ __global__ void k_init_lnx(double* lnx, double* dtab, double* ftab, double* rtab
 // ------------------------------------------------------------------------------------------ K1
 
 // Per-SNP Fst terms (see fst_terms below for the definition) from the raw counts; 1/k from rcp.
-__device__ __forceinline__ bool fst_snp(uint32_t c, bool member, const double* rcp, double& num, double& den) {
+__device__ __forceinline__ void fst_snp(uint32_t c, bool member, const double* rcp, double& num, double& den) {
+  // Hudson's terms in the form num = A1 + A2 - 2 p1 p2, den = p1 + p2 - 2 p1 p2 with p = a / n and
+  // A = p^2 - p(1-p)/(n-1) = a(a-1) / (n(n-1)); a SNP outside the set takes a = 0 (num = den = 0)
   const uint32_t r1 = c & 0xffu, a1 = (c >> 8) & 0xffu, r2 = (c >> 16) & 0xffu, a2 = c >> 24;
   const uint32_t n1c = r1 + a1, n2c = r2 + a2;
   const bool ok = member & (n1c >= 2u) & (n2c >= 2u);
-  const uint32_t m1 = ok ? n1c : 2u, m2 = ok ? n2c : 2u;   // u8 counts: n <= 510 < RCPN
-  const double i1 = rcp[m1], i2 = rcp[m2], j1 = rcp[m1 - 1], j2 = rcp[m2 - 1];
-  const double p1 = (double)a1 * i1, p2 = (double)a2 * i2;
-  const double d = p1 - p2;
-  num = ok ? d * d - p1 * (1.0 - p1) * j1 - p2 * (1.0 - p2) * j2 : 0.0;
-  den = ok ? p1 * (1.0 - p2) + p2 * (1.0 - p1) : 0.0;
-  return ok;
+  const uint32_t b1 = ok ? a1 : 0u, b2 = ok ? a2 : 0u;
+  const uint32_t m1 = max(n1c, 2u), m2 = max(n2c, 2u);   // u8 counts: n <= 510 < RCPN
+  const double i1 = rcp[m1], j1 = rcp[m1 - 1], i2 = rcp[m2], j2 = rcp[m2 - 1];
+  const double p1 = (double)b1 * i1, p2 = (double)b2 * i2;
+  const double A1 = (double)(b1 * (b1 - 1u)) * i1 * j1, A2 = (double)(b2 * (b2 - 1u)) * i2 * j2;
+  const double m = p1 * p2;
+  num = fma(-2.0, m, A1 + A2);
+  den = fma(-2.0, m, p1 + p2);
+}
+
+// x * 2^40 rounded to the nearest integer, |x| < 2^11 (the magic-number conversion: 1.5 * 2^52 pins the
+// exponent, the low mantissa bits then hold the integer)
+__device__ __forceinline__ unsigned long long fst_fixed(double x) {
+  const double y = fma(x, FST_SCALE, 6755399441055744.0);
+  return (unsigned long long)(__double_as_longlong(y) - 0x4338000000000000ll);
 }
 
 template <bool DO_BG, bool DO_SEG, bool LDS_HIST, bool DO_BINS, bool FILT, bool FST>
@@ -399,9 +448,13 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
   // fixed-point add of one lane's (num, den) pair into window wid of this chromosome
   const int frep = threadIdx.x & (FST_R - 1);
   auto fst_add = [&](uint32_t wid, double num, double den) {
-    const unsigned long long qn = (unsigned long long)__double2ll_rn(num * FST_SCALE);
-    const unsigned long long qd = (unsigned long long)__double2ll_rn(den * FST_SCALE);
+    const unsigned long long qn = fst_fixed(num), qd = fst_fixed(den);
+    if ((qn | qd) == 0ull) return;
     const uint32_t j = wid - wlo;
+#ifdef SFS2D_EXP_NOATOM
+    if (qn == 0x123456789ull && qd == 7ull) sh_fst[j & 7] = qn;   // experiment: no atomics
+    return;
+#endif
     if (j < (uint32_t)FST_LDS) {
       atomicAdd(&sh_fst[2 * (j * FST_R + frep)], qn);
       atomicAdd(&sh_fst[2 * (j * FST_R + frep) + 1], qd);
@@ -421,25 +474,32 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
 
   // one 16-B vector = 4 consecutive SNPs; elements outside [t.begin, t.end) are masked.
   // wprev / wnext: window ids of the SNPs just before / after the vector.
-  auto process = [&](uint32_t i0, const uint4& cv, const uint4& pv, const uint2& av, uint32_t wprev, uint32_t wnext) {
+  // EDGE: the step reaches past the tile (elements outside [t.begin, t.end) are masked);
+  // FAST: no lane of the wave holds counts outside the grid (classify_fast)
+  KParams Q = P;   // the per-SNP parameters as VGPR copies (vreg)
+  Q.n1 = vreg(P.n1); Q.n2 = vreg(P.n2); Q.n1p = vreg(P.n1p); Q.n2p = vreg(P.n2p); Q.nb2 = vreg(P.nb2);
+  Q.fold_thr = vreg(P.fold_thr); Q.h1a = vreg(P.h1a); Q.h1b = vreg(P.h1b);
+  Q.wmag = vreg(P.wmag); Q.wsh1 = vreg(P.wsh1); Q.wsh2 = vreg(P.wsh2);
+  auto process = [&](auto EDGE_C, auto FAST_C, uint32_t i0, const uint4& cv, const uint4& pv, const uint2& av,
+                     uint32_t wprev, uint32_t wnext) {
+    constexpr bool EDGE = decltype(EDGE_C)::value, FAST = decltype(FAST_C)::value;
     const uint32_t cc[4] = {cv.x, cv.y, cv.z, cv.w};
     const uint32_t pp[4] = {pv.x, pv.y, pv.z, pv.w};
     const uint32_t aa[4] = {av.x & 0xffffu, av.x >> 16, av.y & 0xffffu, av.y >> 16};
     uint32_t w[4];
     if (DO_SEG) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) w[k] = wid_fast(P, pp[k]);
+      for (int k = 0; k < 4; ++k) w[k] = wid_fast(Q, pp[k]);
     }
     uint32_t bw[4];
     uint32_t segcode = 0;   // bit 2k: SNP k opens a window, bit 2k+1: it closes one
-    // Fst: this lane's sums for the window of its first SNP (key); SNPs of a later window in the
-    // same vector (a boundary inside it: rare) are added on their own
-    uint32_t fkey = 0xffffffffu;
-    double fn = 0.0, fd = 0.0;
+    // Fst: the terms of the four SNPs; one fixed-point add for the lane when they share a window
+    uint32_t fw[4];
+    bool fm[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint32_t i = i0 + k;
-      const bool in = (i >= t.begin) & (i < t.end);
+      const bool in = EDGE ? (i >= t.begin) & (i < t.end) : true;
       bool var_ok = in, pos_ok = true;
       if (filt) var_ok = in & ((int)aa[k] == P.ann_want);
       if (pos_filter) {
@@ -447,28 +507,19 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
         pos_ok = (!P.has_start | (p >= P.start_pos)) & (!P.has_end | (p <= P.end_pos));
       }
       int k2all, u1a, u1b;
-      bw[k] = classify(P, cc[k], var_ok, pos_ok, err, k2all, u1a, u1b);
+      bw[k] = FAST ? classify_fast(Q, cc[k], var_ok, pos_ok, k2all, u1a, u1b)
+                   : classify(P, cc[k], var_ok, pos_ok, err, k2all, u1a, u1b);
       if (FST) {
-        const uint32_t wk = DO_SEG ? w[k] : div_fast(P, i - t.cb);
-        const bool in_slot = DO_SEG | (wk < t.nslots);   // fixed-SNP windows: the tail is dropped
-        double num, den;
-        if (fst_snp(cc[k], in & (k2all >= 0) & in_slot, sh_rcp, num, den)) {
-          if (fkey == 0xffffffffu) fkey = wk;
-          if (wk == fkey) {
-            fn += num;
-            fd += den;
-          } else {
-            fst_add(wk, num, den);
-          }
-        }
+        fw[k] = DO_SEG ? w[k] : div_fast(Q, i - t.cb);
+        fm[k] = in & (k2all >= 0) & (DO_SEG | (fw[k] < t.nslots));   // fixed-SNP windows: the tail is dropped
       }
       if (DO_BG) {
         if (LDS_HIST) {
           // no branches: skipped SNPs add to the lane's trash word (keeps exec masks, and the
           // scalar registers they take, out of the unrolled loop)
           atomicAdd(&sh_hist[(in & (k2all >= 0)) ? (k2all << hsh) + rep : trash], 1u);
-          atomicAdd(&sh_hist[(in & (u1a >= 0)) ? ((P.h1a + u1a) << hsh) + rep : trash], 1u);
-          atomicAdd(&sh_hist[(in & (u1b >= 0)) ? ((P.h1b + u1b) << hsh) + rep : trash], 1u);
+          atomicAdd(&sh_hist[(in & (u1a >= 0)) ? ((Q.h1a + u1a) << hsh) + rep : trash], 1u);
+          atomicAdd(&sh_hist[(in & (u1b >= 0)) ? ((Q.h1b + u1b) << hsh) + rep : trash], 1u);
         } else if (in) {
           if (k2all >= 0) atomicAdd(&gh[k2all], 1u);
           if (u1a >= 0) atomicAdd(&gh[P.h1a + u1a], 1u);
@@ -486,7 +537,18 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
       }
       __builtin_amdgcn_sched_barrier(0);   // one SNP at a time: its lane masks die before the next
     }
-    if (FST && fkey != 0xffffffffu) fst_add(fkey, fn, fd);
+    if (FST) {
+      double nk[4], dk[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) fst_snp(cc[k], fm[k], sh_rcp, nk[k], dk[k]);
+      if (!EDGE && fw[0] == fw[3]) {   // inside the tile: all four in that window
+        fst_add(fw[0], (nk[0] + nk[1]) + (nk[2] + nk[3]), (dk[0] + dk[1]) + (dk[2] + dk[3]));
+      } else {   // a window boundary inside the lane's four SNPs (windows never shrink to 0 SNPs here)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (fm[k]) fst_add(fw[k], nk[k], dk[k]);
+      }
+    }
     // window boundaries are rare: one divergent pass over the set bits
     if (DO_SEG && segcode) {
       for (uint32_t c = segcode; c; c &= c - 1) {
@@ -497,7 +559,7 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
       }
     }
     if (DO_BINS) {
-      if (i0 >= t.begin && i0 + 4 <= t.end) {
+      if (!EDGE || (i0 >= t.begin && i0 + 4 <= t.end)) {
         *reinterpret_cast<uint4*>(bins + i0) = make_uint4(bw[0], bw[1], bw[2], bw[3]);
       } else {
 #pragma unroll
@@ -530,7 +592,28 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
       if (lane == 0) wpa = wid_fast(P, xa_prev);
       if (edge_next) wna = wid_fast(P, xa_next);
     }
-    process(ia, ca, pa, aav, wpa, wna);
+    // counts outside the grid (r + a > n: an error or an out-of-grid key) take the exact classify()
+    const bool bad = ((ca.x & 0xffu) + ((ca.x >> 8) & 0xffu) > (uint32_t)P.n1) |
+                     (((ca.x >> 16) & 0xffu) + (ca.x >> 24) > (uint32_t)P.n2) |
+                     ((ca.y & 0xffu) + ((ca.y >> 8) & 0xffu) > (uint32_t)P.n1) |
+                     (((ca.y >> 16) & 0xffu) + (ca.y >> 24) > (uint32_t)P.n2) |
+                     ((ca.z & 0xffu) + ((ca.z >> 8) & 0xffu) > (uint32_t)P.n1) |
+                     (((ca.z >> 16) & 0xffu) + (ca.z >> 24) > (uint32_t)P.n2) |
+                     ((ca.w & 0xffu) + ((ca.w >> 8) & 0xffu) > (uint32_t)P.n1) |
+                     (((ca.w >> 16) & 0xffu) + (ca.w >> 24) > (uint32_t)P.n2);
+    const bool edge = base < t.begin || base + STEP > t.end;   // block-uniform
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    if (edge || __ballot(bad)) process(T_{}, F_{}, ia, ca, pa, aav, wpa, wna);   // rare: exact, masked
+    else {
+#ifdef SFS2D_MARK
+      asm volatile("; HOT_BEGIN");
+#endif
+      process(F_{}, T_{}, ia, ca, pa, aav, wpa, wna);
+#ifdef SFS2D_MARK
+      asm volatile("; HOT_END");
+#endif
+    }
   }
   STAMP(22);
   if (err) atomicOr(err_word, err);
