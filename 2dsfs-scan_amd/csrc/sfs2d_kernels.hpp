@@ -572,6 +572,74 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
   // one 16-B vector of counts (+ positions) per thread per step; loads are clamped into the tile
   // (lanes past its end re-read its last vector, masked) so that no load sits behind a branch; the
   // lanes at the wave edges fetch their neighbour positions in the same batch
+  // The common step (not a tile's first or last, every count inside the grid, no filter): classify_fast
+  // inline with precomputed LDS byte offsets, and window-boundary bookkeeping only in lanes whose
+  // neighbours differ.  Everything else goes through process() above.
+  constexpr bool FASTOK = !FILT && (!DO_BG || LDS_HIST);
+  const uint32_t s2 = (uint32_t)hsh + 2u;                        // bin -> byte offset shift
+  uint32_t* const hist_l = sh_hist + rep;                        // this lane's histogram copy
+  uint32_t* const h1a_l = hist_l + ((uint32_t)P.h1a << hsh);
+  uint32_t* const h1b_l = hist_l + ((uint32_t)P.h1b << hsh);
+  uint32_t* const trash_p = sh_hist + trash;
+  const uint32_t n2p1 = vreg(P.n2 + 1), nb2m1 = vreg(P.nb2 - 1), n1pm1 = vreg(P.n1p - 1), n2pm1 = vreg(P.n2p - 1);
+  auto process_fast = [&](uint32_t i0, const uint4& cv, const uint4& pv, uint32_t wprev, uint32_t wnext) {
+    const uint32_t cc[4] = {cv.x, cv.y, cv.z, cv.w};
+    const uint32_t pp[4] = {pv.x, pv.y, pv.z, pv.w};
+    uint32_t w[4], bw[4];
+    if (DO_SEG) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w[k] = wid_fast(Q, pp[k]);
+    }
+    uint32_t fw[4];
+    bool fm[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t c = cc[k];
+      const uint32_t r1 = c & 0xffu, a1 = (c >> 8) & 0xffu, r2 = (c >> 16) & 0xffu, a2 = c >> 24;
+      const bool sw = (int)(a1 + a2) > Q.fold_thr;
+      const uint32_t x1 = sw ? r1 : a1, x2 = sw ? r2 : a2;
+      const uint32_t k2 = __umul24(x1, n2p1) + x2;                 // 0 iff (x1, x2) = (0, 0)
+      const bool in2 = k2 != 0u, last = k2 == nb2m1;
+      const uint32_t g1 = min(a1, (uint32_t)Q.n1 - a1), g2 = min(a2, (uint32_t)Q.n2 - a2);
+      const uint32_t f1 = g1 - 1u < n1pm1 ? g1 : 0u, f2 = g2 - 1u < n2pm1 ? g2 : 0u;
+      bw[k] = (last ? B_LAST : k2) | (f1 << 16) | (f2 << 23) | B_VAR;
+      if (DO_BG) {
+        atomicAdd(in2 ? (uint32_t*)((char*)hist_l + (k2 << s2)) : trash_p, 1u);
+        atomicAdd(a1 ? (uint32_t*)((char*)h1a_l + (a1 << s2)) : trash_p, 1u);
+        atomicAdd(a2 ? (uint32_t*)((char*)h1b_l + (a2 << s2)) : trash_p, 1u);
+        b2 += (in2 & !last) ? 1u : 0u;
+      }
+      if (FST) {
+        fw[k] = DO_SEG ? w[k] : div_fast(Q, i0 + k - t.cb);
+        fm[k] = in2 & (DO_SEG | (fw[k] < t.nslots));
+      }
+    }
+    if (FST) {
+      double nk[4], dk[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) fst_snp(cc[k], fm[k], sh_rcp, nk[k], dk[k]);
+      if (fw[0] == fw[3]) {
+        fst_add(fw[0], (nk[0] + nk[1]) + (nk[2] + nk[3]), (dk[0] + dk[1]) + (dk[2] + dk[3]));
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (fm[k]) fst_add(fw[k], nk[k], dk[k]);
+      }
+    }
+    // window boundaries: ids are non-decreasing along the tile, so a lane holds one iff its
+    // neighbours' ids differ (rare)
+    if (DO_SEG && wprev != wnext) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t qp = k ? w[k - 1] : wprev, qn = k < 3 ? w[k + 1] : wnext;
+        uint32_t* sl = reinterpret_cast<uint32_t*>(slots + ((size_t)t.sbase + w[k]));
+        if (qp != w[k]) sl[0] = i0 + k + 1u;   // .x = first + 1, .y = last + 1
+        if (qn != w[k]) sl[1] = i0 + k + 1u;
+      }
+    }
+    if (DO_BINS) *reinterpret_cast<uint4*>(bins + i0) = make_uint4(bw[0], bw[1], bw[2], bw[3]);
+  };
+
   constexpr uint32_t STEP = 4 * BLOCK1;
   const uint32_t ab = t.begin & ~3u, alast = (t.end - 1u) & ~3u;
   for (uint32_t base = ab; base < t.end; base += STEP) {
@@ -593,23 +661,21 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
       if (edge_next) wna = wid_fast(P, xa_next);
     }
     // counts outside the grid (r + a > n: an error or an out-of-grid key) take the exact classify()
-    const bool bad = ((ca.x & 0xffu) + ((ca.x >> 8) & 0xffu) > (uint32_t)P.n1) |
-                     (((ca.x >> 16) & 0xffu) + (ca.x >> 24) > (uint32_t)P.n2) |
-                     ((ca.y & 0xffu) + ((ca.y >> 8) & 0xffu) > (uint32_t)P.n1) |
-                     (((ca.y >> 16) & 0xffu) + (ca.y >> 24) > (uint32_t)P.n2) |
-                     ((ca.z & 0xffu) + ((ca.z >> 8) & 0xffu) > (uint32_t)P.n1) |
-                     (((ca.z >> 16) & 0xffu) + (ca.z >> 24) > (uint32_t)P.n2) |
-                     ((ca.w & 0xffu) + ((ca.w >> 8) & 0xffu) > (uint32_t)P.n1) |
-                     (((ca.w >> 16) & 0xffu) + (ca.w >> 24) > (uint32_t)P.n2);
-    const bool edge = base < t.begin || base + STEP > t.end;   // block-uniform
+    // (called allele counts r + a by byte dot products)
+    auto nc1 = [](uint32_t c) { return __builtin_amdgcn_udot4(c, 0x00000101u, 0u, false); };
+    auto nc2 = [](uint32_t c) { return __builtin_amdgcn_udot4(c, 0x01010000u, 0u, false); };
+    const bool bad = (max(max(nc1(ca.x), nc1(ca.y)), max(nc1(ca.z), nc1(ca.w))) > (uint32_t)P.n1) |
+                     (max(max(nc2(ca.x), nc2(ca.y)), max(nc2(ca.z), nc2(ca.w))) > (uint32_t)P.n2);
+    // a tile's first and last steps hold its edges, the chromosome's first / last SNP included
+    const bool edge = base == ab || base + STEP >= t.end;   // block-uniform
     using T_ = std::true_type;
     using F_ = std::false_type;
-    if (edge || __ballot(bad)) process(T_{}, F_{}, ia, ca, pa, aav, wpa, wna);   // rare: exact, masked
+    if (!FASTOK || edge || __ballot(bad)) process(T_{}, F_{}, ia, ca, pa, aav, wpa, wna);   // exact, masked
     else {
 #ifdef SFS2D_MARK
       asm volatile("; HOT_BEGIN");
 #endif
-      process(F_{}, T_{}, ia, ca, pa, aav, wpa, wna);
+      process_fast(ia, ca, pa, wpa, wna);
 #ifdef SFS2D_MARK
       asm volatile("; HOT_END");
 #endif

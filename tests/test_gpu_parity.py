@@ -322,3 +322,42 @@ def test_dynamic_window_pools(monkeypatch, wgs):
             pl.run()
             outs.append(pl.read().tobytes())
         assert outs[0] == outs[1] == outs[2]
+
+
+def test_called_counts_above_sample_size_inside_long_tiles():
+    """SNPs whose called allele count r + a exceeds 2 * pop_size without leaving the grid (no fold
+    swap, so the 2D key is the alt count): the reference counts them; k_prep routes their steps
+    through the exact classify, the rest of the tile through the fast path.  Records, Fst and the
+    background histograms against the oracle."""
+    import twoDSFS_class as T
+    from sfs2d import _lib as L
+    from sfs2d.engine import Engine, ScanConfig
+    from sfs2d.pack import PackedSNPs, pack_counts
+    from sfs2d.synth import synth_genome
+    p = synth_genome(2, [40000, 9000], 25, 25, seed=4242)
+    r1, a1 = p.counts & 0xff, (p.counts >> 8) & 0xff
+    r2, a2 = (p.counts >> 16) & 0xff, p.counts >> 24
+    pick = (np.random.default_rng(3).random(p.n) < 0.004) & (a1 + a2 <= 50)
+    q = PackedSNPs(pack_counts(np.where(pick, r1 + 7, r1), a1, r2, a2), p.pos, p.chrom_off, p.chrom_names,
+                   p.ann_id, p.ann_names)
+    ocfg = O.Cfg(25, 25)
+    bgs = O.chrom_backgrounds(q, ocfg)
+    wins = O.bp_windows(q, 20000)
+    _records_vs_oracle(q, ScanConfig(n1p=25, n2p=25, window=20000), ocfg, wins, lambda c: bgs[c])
+    eng = Engine.get(0)
+    dev = eng.upload(q)
+    h2, u1, u2 = eng.bg_hist(dev, ScanConfig(n1p=25, n2p=25), 0)
+    assert np.array_equal(np.asarray(h2), np.asarray(bgs[0][0]))
+    assert np.array_equal(T._fold_counts(u1), np.asarray(bgs[0][1]))
+    assert np.array_equal(T._fold_counts(u2), np.asarray(bgs[0][2]))
+    pl = eng.plan(dev, ScanConfig(n1p=25, n2p=25, window=20000, fst=True))
+    pl.run()
+    pl.check()
+    recs = pl.read()
+    fst = pl.read_fst()
+    live = (recs["flags"][: len(fst)] & L.W_EMPTY) == 0
+    got = fst[live]
+    assert len(got) == len(wins)
+    for g, (c, st, b, e) in list(zip(got, wins))[::7]:
+        assert _fst_close(float(g), O.window_fst(q, np.arange(b, e), ocfg)), (g, b, e)
+    pl.close()
