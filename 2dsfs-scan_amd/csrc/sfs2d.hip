@@ -10,6 +10,7 @@
 // All device state a run touches (slot table, background replicas and counters, LDS) is left
 // zeroed by the run itself, so plans replay without memsets.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cmath>
@@ -90,7 +91,7 @@ struct sfs2d_ctx {
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   double* d_lnx = nullptr;
-  double* d_df = nullptr;   // D(r), F(x) (LNT each), then 1/k (RCPN)
+  double* d_df = nullptr;   // D(r), F(x) (LNT each), then (1/k, 1/(k(k-1))) pairs (RCPN)
   std::string err;
 };
 
@@ -159,6 +160,10 @@ struct sfs2d_plan {
   int tcount = 0;
   int tevery = 1;                // sample every tevery-th run
   int64_t tseen = 0;             // runs since timing was set
+  // events of the run being enqueued: k_prep start/stop, scan start/stop (null: not sampled).  They
+  // go into the kernels' own dispatch packets (hipExtLaunchKernelGGL), so they stamp the kernel's
+  // start and end as the command processor sees them -- the durations rocprofv3 reports.
+  hipEvent_t kev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
 namespace {
@@ -197,8 +202,8 @@ int plan_par(const sfs2d_plan* pl) { return pl->fused ? (int)(pl->runs & 1) : 0;
 
 template <bool P16, bool FUSED, bool FST>
 void launch_scan_w(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
-  hipLaunchKernelGGL((k_scan_w<P16, FUSED, FST>), dim3((unsigned)pl->chunks.size()), dim3(SBLOCK), pl->scan_lds,
-                     pl->ctx->stream, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
+  hipExtLaunchKernelGGL((k_scan_w<P16, FUSED, FST>), dim3((unsigned)pl->chunks.size()), dim3(SBLOCK), pl->scan_lds,
+                     pl->ctx->stream, pl->kev[2], pl->kev[3], 0, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
                      per_chrom, pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, bp, pl->d_repl, pl->d_bcount,
                      plan_par(pl), pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels,
                      pl->extra_rec >= 0 ? (int)pl->last_chrom : -1, pl->d_fsum, pl->d_fst, pl->d_ctr,
@@ -207,8 +212,8 @@ void launch_scan_w(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
 
 template <bool P16, bool FST>
 void launch_scan_g(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
-  hipLaunchKernelGGL((k_scan_g<P16, FST>), dim3((unsigned)pl->chunks.size()), dim3(BLOCK), pl->scan_lds,
-                     pl->ctx->stream, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_head, per_chrom,
+  hipExtLaunchKernelGGL((k_scan_g<P16, FST>), dim3((unsigned)pl->chunks.size()), dim3(BLOCK), pl->scan_lds,
+                     pl->ctx->stream, pl->kev[2], pl->kev[3], 0, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_head, per_chrom,
                      pl->ctx->d_lnx, out, bp, pl->d_fsum, pl->d_fst);
 }
 
@@ -235,11 +240,11 @@ template <bool B, bool S, bool L, bool N, bool F, bool FS>
 hipError_t launch_prep3(sfs2d_plan* pl) {
   const sfs2d_data* d = pl->data;
   const int par = plan_par(pl);
-  hipLaunchKernelGGL((k_prep<B, S, L, N, F, FS>), dim3((unsigned)pl->tiles.size()), dim3(BLOCK1),
-                     (B && L) ? pl->bg_lds : 0, pl->ctx->stream, pl->K, d->counts, d->pos, d->ann, pl->d_tiles,
+  hipExtLaunchKernelGGL((k_prep<B, S, L, N, F, FS>), dim3((unsigned)pl->tiles.size()), dim3(BLOCK1),
+                     (B && L) ? pl->bg_lds : 0, pl->ctx->stream, pl->kev[0], pl->kev[1], 0, pl->K, d->counts, d->pos, d->ann, pl->d_tiles,
                      pl->d_repl + (size_t)par * REPL * pl->K.nchrom * pl->K.nh, pl->d_slots, pl->d_bins,
                      pl->d_bcount + (size_t)par * pl->K.nchrom, pl->d_err, L ? pl->hr : 1,
-                     pl->ctx->d_df + 2 * LNT, pl->d_fsum);
+                     reinterpret_cast<const double2*>(pl->ctx->d_df + 2 * LNT), pl->d_fsum);
   return hipGetLastError();
 }
 
@@ -325,7 +330,7 @@ int sfs2d_ctx_create(int device, sfs2d_ctx** out) {
   c->stream = c->own;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) c->ncu = prop.multiProcessorCount;
-  if (dalloc(c, &c->d_lnx, LNX_N) || dalloc(c, &c->d_df, 2 * LNT + RCPN)) {
+  if (dalloc(c, &c->d_lnx, LNX_N) || dalloc(c, &c->d_df, 2 * LNT + 2 * RCPN)) {
     hipFree(c->d_lnx); hipStreamDestroy(c->own); delete c; return SFS2D_E_NOMEM;
   }
   hipLaunchKernelGGL(k_init_lnx, dim3(LNX_N / 256), dim3(256), 0, c->stream, c->d_lnx, c->d_df, c->d_df + LNT,
@@ -773,23 +778,43 @@ int sfs2d_plan_run_phase(sfs2d_plan* pl, int phase, sfs2d_window* out_dev) {
     te = &pl->tev[(size_t)pl->tcount * 4];
   if (!pl->do_bg && !pl->bg_ready && phase != 1)
     return set_err(ctx, SFS2D_E_ARG, "supplied-background plan run before sfs2d_plan_set_background");
-  if (te) HIPCHK(ctx, hipEventRecord(te[0], ctx->stream));
+  // sampled runs: k_prep and the scan kernel carry the run's four events in their dispatch packets
+  // (kernel start / end); a phase that does not launch its kernel records the event in the stream
+  for (int k = 0; k < 4; ++k) pl->kev[k] = te ? te[k] : nullptr;
   if (phase == 0 || phase == 1) {
     HIPCHK(ctx, launch_prep(pl, true));
+    if (te && pl->tiles.empty()) {
+      HIPCHK(ctx, hipEventRecord(te[0], ctx->stream));
+      HIPCHK(ctx, hipEventRecord(te[1], ctx->stream));
+    }
+  } else if (te) {
+    HIPCHK(ctx, hipEventRecord(te[0], ctx->stream));
+    HIPCHK(ctx, hipEventRecord(te[1], ctx->stream));
   }
-  if (te) HIPCHK(ctx, hipEventRecord(te[1], ctx->stream));
+  pl->kev[0] = pl->kev[1] = nullptr;
   if (phase == 0 || phase == 2) {
     if (pl->do_bg && !pl->fused) HIPCHK(ctx, launch_bg_slices(pl));
-    if (te) HIPCHK(ctx, hipEventRecord(te[2], ctx->stream));
     sfs2d_window* out = out_dev ? out_dev : pl->d_out;
+    if (te && pl->chunks.empty()) {
+      HIPCHK(ctx, hipEventRecord(te[2], ctx->stream));
+      HIPCHK(ctx, hipEventRecord(te[3], ctx->stream));
+    }
     HIPCHK(ctx, launch_scan_any(pl, out));
     pl->last_out = out;
     pl->runs++;
-  }
-  if (te) {
+  } else if (te) {
+    HIPCHK(ctx, hipEventRecord(te[2], ctx->stream));
     HIPCHK(ctx, hipEventRecord(te[3], ctx->stream));
-    pl->tcount++;
   }
+  pl->kev[2] = pl->kev[3] = nullptr;
+  if (te) pl->tcount++;
+  return 0;
+}
+
+int sfs2d_plan_grids(const sfs2d_plan* pl, int64_t* prep_threads, int64_t* scan_threads) {
+  if (!pl) return SFS2D_E_ARG;
+  if (prep_threads) *prep_threads = (int64_t)pl->tiles.size() * BLOCK1;
+  if (scan_threads) *scan_threads = (int64_t)pl->chunks.size() * (pl->G == WAVE ? SBLOCK : BLOCK);
   return 0;
 }
 

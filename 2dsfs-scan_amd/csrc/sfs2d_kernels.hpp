@@ -55,7 +55,7 @@ constexpr int FBLOCK = 1024;      // k_bg_finalize workgroup
 constexpr int KBLOCK = 512;       // k_bg_slice workgroup
 constexpr int LNX_N = 1 << 20;    // ln(k) table for k < LNX_N (bin counts / window totals)
 constexpr int LNT = 512;          // D(r) and x ln x tables staged in LDS by k_scan_w
-constexpr int RCPN = 512;         // 1/k for k < 512 (Fst: called allele counts ref + alt <= 510), after the LNT tables
+constexpr int RCPN = 512;         // (1/k, 1/(k(k-1))) for k < 512 (Fst: called allele counts ref + alt <= 510), after the LNT tables
 constexpr int REPL = 4;           // replicas of the per-chromosome background histograms
 constexpr int PW_MAX_LEAVES = 256;
 constexpr int LEAVES_PER_SLICE = 4;
@@ -373,7 +373,10 @@ __device__ __forceinline__ uint32_t bin_g2(uint32_t w) { return (w >> 23) & 0x7f
 __global__ void k_init_lnx(double* lnx, double* dtab, double* ftab, double* rtab) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < LNX_N) lnx[i] = i ? log((double)i) : 0.0;
-  if (i < RCPN) rtab[i] = i ? 1.0 / (double)i : 0.0;
+  if (i < RCPN) {   // Fst: (1/n, 1/(n(n-1))) per called allele count n; 0 below n = 2 (not in the set)
+    rtab[2 * i] = i >= 2 ? 1.0 / (double)i : 0.0;
+    rtab[2 * i + 1] = i >= 2 ? 1.0 / ((double)i * (double)(i - 1)) : 0.0;
+  }
   if (i < LNT) {
     const double a = i ? (double)i * log((double)i) : 0.0;
     const double b = (double)(i + 1) * log((double)(i + 1));
@@ -384,18 +387,18 @@ __global__ void k_init_lnx(double* lnx, double* dtab, double* ftab, double* rtab
 
 // ------------------------------------------------------------------------------------------ K1
 
-// Per-SNP Fst terms (see fst_terms below for the definition) from the raw counts; 1/k from rcp.
-__device__ __forceinline__ void fst_snp(uint32_t c, bool member, const double* rcp, double& num, double& den) {
-  // Hudson's terms in the form num = A1 + A2 - 2 p1 p2, den = p1 + p2 - 2 p1 p2 with p = a / n and
-  // A = p^2 - p(1-p)/(n-1) = a(a-1) / (n(n-1)); a SNP outside the set takes a = 0 (num = den = 0)
+// Per-SNP Fst terms (see fst_terms below for the definition) from the raw counts.  Hudson's terms in
+// the form num = A1 + A2 - 2 p1 p2, den = p1 + p2 - 2 p1 p2 with p = a / n and
+// A = p^2 - p(1-p)/(n-1) = a(a-1) / (n(n-1)); rt[n] = (1/n, 1/(n(n-1))) (0 for n < 2).  A SNP outside
+// the set takes a = 0 (num = den = 0).
+__device__ __forceinline__ void fst_snp(uint32_t c, bool member, const double2* rt, double& num, double& den) {
   const uint32_t r1 = c & 0xffu, a1 = (c >> 8) & 0xffu, r2 = (c >> 16) & 0xffu, a2 = c >> 24;
-  const uint32_t n1c = r1 + a1, n2c = r2 + a2;
+  const uint32_t n1c = r1 + a1, n2c = r2 + a2;             // u8 counts: n <= 510 < RCPN
   const bool ok = member & (n1c >= 2u) & (n2c >= 2u);
   const uint32_t b1 = ok ? a1 : 0u, b2 = ok ? a2 : 0u;
-  const uint32_t m1 = max(n1c, 2u), m2 = max(n2c, 2u);   // u8 counts: n <= 510 < RCPN
-  const double i1 = rcp[m1], j1 = rcp[m1 - 1], i2 = rcp[m2], j2 = rcp[m2 - 1];
-  const double p1 = (double)b1 * i1, p2 = (double)b2 * i2;
-  const double A1 = (double)(b1 * (b1 - 1u)) * i1 * j1, A2 = (double)(b2 * (b2 - 1u)) * i2 * j2;
+  const double2 q1 = rt[n1c], q2 = rt[n2c];
+  const double p1 = (double)b1 * q1.x, p2 = (double)b2 * q2.x;
+  const double A1 = (double)__umul24(b1, b1 - 1u) * q1.y, A2 = (double)__umul24(b2, b2 - 1u) * q2.y;
   const double m = p1 * p2;
   num = fma(-2.0, m, A1 + A2);
   den = fma(-2.0, m, p1 + p2);
@@ -414,7 +417,7 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
                                                  const Tile* __restrict__ tiles, uint32_t* __restrict__ repl,
                                                  uint2* __restrict__ slots, uint32_t* __restrict__ bins,
                                                  uint32_t* __restrict__ bcount, uint32_t* __restrict__ err_word,
-                                                 int hr, const double* __restrict__ rcp_g,
+                                                 int hr, const double2* __restrict__ rcp_g,
                                                  unsigned long long* __restrict__ fsum) {
   // repl / bcount: this run's parity buffers.  LDS histogram: hr interleaved copies of every word
   // (lane & (hr-1) picks one), which spreads the many same-bin atomics of a wavefront over banks.
@@ -423,7 +426,7 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
   // FST: per-window sums of the Fst terms, int64 fixed point (num, den) for the tile's first
   // FST_LDS windows (FST_R copies each), the rest straight to the global per-slot sums
   __shared__ unsigned long long sh_fst[FST ? 2 * FST_R * FST_LDS : 1];
-  __shared__ double sh_rcp[FST ? RCPN : 1];
+  __shared__ double2 sh_rcp[FST ? RCPN : 1];
   __shared__ uint32_t sh_wlo;
   STAMP(20);
   BLK_STAMP(0, 0);
@@ -537,16 +540,12 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
       }
       __builtin_amdgcn_sched_barrier(0);   // one SNP at a time: its lane masks die before the next
     }
-    if (FST) {
-      double nk[4], dk[4];
+    if (FST) {   // per SNP (edge steps: masked SNPs may carry any window id)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) fst_snp(cc[k], fm[k], sh_rcp, nk[k], dk[k]);
-      if (!EDGE && fw[0] == fw[3]) {   // inside the tile: all four in that window
-        fst_add(fw[0], (nk[0] + nk[1]) + (nk[2] + nk[3]), (dk[0] + dk[1]) + (dk[2] + dk[3]));
-      } else {   // a window boundary inside the lane's four SNPs (windows never shrink to 0 SNPs here)
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (fm[k]) fst_add(fw[k], nk[k], dk[k]);
+      for (int k = 0; k < 4; ++k) {
+        double nk, dk;
+        fst_snp(cc[k], fm[k], sh_rcp, nk, dk);
+        if (fm[k]) fst_add(fw[k], nk, dk);
       }
     }
     // window boundaries are rare: one divergent pass over the set bits
@@ -615,16 +614,21 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
       }
     }
     if (FST) {
-      double nk[4], dk[4];
+      // the lane's four SNPs in order, one running (num, den) pair per window: a fixed-point add
+      // whenever the window changes (rare) and one at the end
+      double sn = 0.0, sd = 0.0;
+      uint32_t wc = fw[0];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) fst_snp(cc[k], fm[k], sh_rcp, nk[k], dk[k]);
-      if (fw[0] == fw[3]) {
-        fst_add(fw[0], (nk[0] + nk[1]) + (nk[2] + nk[3]), (dk[0] + dk[1]) + (dk[2] + dk[3]));
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (fm[k]) fst_add(fw[k], nk[k], dk[k]);
+      for (int k = 0; k < 4; ++k) {
+        double nk, dk;
+        fst_snp(cc[k], fm[k], sh_rcp, nk, dk);
+        if (k && fw[k] != wc) {
+          fst_add(wc, sn, sd);
+          sn = 0.0; sd = 0.0; wc = fw[k];
+        }
+        sn += nk; sd += dk;
       }
+      fst_add(wc, sn, sd);
     }
     // window boundaries: ids are non-decreasing along the tile, so a lane holds one iff its
     // neighbours' ids differ (rare)

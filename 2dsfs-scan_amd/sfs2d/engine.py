@@ -192,6 +192,12 @@ class Plan:
         self.eng.check(self.eng.lib.sfs2d_plan_time(self.h, iters, *[C.byref(x) for x in v]))
         return tuple(x.value for x in v)
 
+    def grids(self):
+        """(k_prep threads, scan kernel threads) per launch: rocprofv3's Grid_Size of each kernel."""
+        a, b = C.c_int64(), C.c_int64()
+        self.eng.check(self.eng.lib.sfs2d_plan_grids(self.h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
     def stats(self) -> int:
         v = C.c_uint32()
         self.eng.check(self.eng.lib.sfs2d_plan_stats(self.h, C.byref(v)))

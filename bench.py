@@ -35,15 +35,36 @@ WS = 20000
 
 
 def algorithmic_bytes(n_snp, n_slots, n_win, which):
-    """Bytes each kernel must move (DESIGN.md "Kernels"): k_prep reads counts + positions (8 B/SNP),
-    writes the packed bins (4 B/SNP) and the window slot table (8 B/window); k_scan_w reads the bins
-    and, for Fst, the counts (8 B/SNP) and the slot table (8 B/slot) and writes one 64-B record and
-    one 8-B Fst per slot."""
+    """Bytes each kernel must move (DESIGN.md "Kernels"), counted from its inputs and outputs.
+
+    k_prep ("k1"): reads counts + positions (8 B/SNP), writes the packed per-SNP bins (4 B/SNP) and
+    the window slot table (8 B/window).  k_scan_w ("k3"): reads the bins (4 B/SNP), the slot record
+    (8 B/slot) and the slot's Fst sums (16 B/slot), writes one 64-B record and one 8-B Fst value
+    per slot.  "pipeline": SURVEY.md 8(d)'s per-unit figure for a whole step -- 8 B/SNP for the scan
+    pass + 4 B/SNP for the background pass over the same stream + 64 B per output window."""
     if which == "k3":
-        return 8 * n_snp + 8 * n_slots + 72 * n_slots
+        return 4 * n_snp + (8 + 16 + 64 + 8) * n_slots
     if which == "k1":
         return 12 * n_snp + 8 * n_win
-    return 20 * n_snp + 8 * n_win + 80 * n_slots
+    if which == "pipeline":
+        return 12 * n_snp + 64 * n_win
+    raise ValueError(which)
+
+
+def pmc_traffic(kernel, grid):
+    """HBM bytes per launch of `kernel` at `grid` threads from the committed rocprofv3 --pmc passes
+    of this bench command (tools/pmc_bench.sh -> profiles/pmc_bench.json: FETCH_SIZE x 2 per the
+    gfx950 correction of MI355X_MICROARCH.md, + WRITE_SIZE; separate passes).  None when absent."""
+    path = os.path.join(REPO, "profiles", "pmc_bench.json")
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+    except (OSError, ValueError):
+        return None, None
+    for r in d.get("kernels", []):
+        if r.get("kernel", "").startswith(kernel) and int(r.get("grid", -1)) == int(grid):
+            return r["read_bytes"] + r["write_bytes"], d.get("source", path)
+    return None, None
 
 
 def cpu_baseline(p):
@@ -76,11 +97,15 @@ def hbm_stream_roofline(eng, steps=5):
     nwin = int(((recs["flags"] & 0x80000000) == 0).sum())
     b3 = algorithmic_bytes(p.n, pl.nrec, nwin, "k3")
     b1 = algorithmic_bytes(p.n, pl.nrec, nwin, "k1")
+    bp = algorithmic_bytes(p.n, pl.nrec, nwin, "pipeline")
+    tk = (k1 + k2 + k3) * 1e-3
     out = {"bound": "hbm", "achieved": b3 / (k3 * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": b3 / (k3 * 1e-3) / 1e9 / HBM_PEAK_GBS, "kernel": "k_scan", "ms": k3,
-           "k1_GBs": b1 / (k1 * 1e-3) / 1e9, "k1_ms": k1, "k2_ms": k2,
-           "pipeline_GBs": algorithmic_bytes(p.n, pl.nrec, nwin, "all") / ((k1 + k2 + k3) * 1e-3) / 1e9,
-           "windows": nwin, "windows_per_s": nwin / ((k1 + k2 + k3) * 1e-3),
+           "frac": b3 / (k3 * 1e-3) / 1e9 / HBM_PEAK_GBS, "kernel": "k_scan_w", "ms": k3,
+           "k1_GBs": b1 / (k1 * 1e-3) / 1e9, "k1_frac": b1 / (k1 * 1e-3) / 1e9 / HBM_PEAK_GBS, "k1_ms": k1,
+           "k2_ms": k2,
+           "pipeline_GBs": bp / tk / 1e9, "pipeline_frac": bp / tk / 1e9 / HBM_PEAK_GBS,
+           "pipeline_bytes_note": "SURVEY 8(d): 12 B/SNP + 64 B/window per step over k_prep + gap + k_scan_w",
+           "windows": nwin, "windows_per_s": nwin / tk,
            "workload": "config 3 stream on 1 GPU: 32 chrom x 1.5625e6 SNPs, 20 kb, per-chromosome bg"}
     pl.close()
     dev.close()
@@ -192,6 +217,9 @@ def main():
     if rank == 0:
         b3 = algorithmic_bytes(p.n, nrec, nwin_rank, "k3")
         achieved = b3 / (k3 * 1e-3) / 1e9
+        bp = algorithmic_bytes(p.n, nrec, nwin_rank, "pipeline")
+        step_s = dt / args.steps
+        traffic, tsrc = pmc_traffic("k_scan_w", pl.grids()[1])
         line = {
             "metric": "genomic windows/s (T2D+T1D+Fst) at 20 kb, n1=n2=50; HBM GB/s fraction",
             "value": value, "unit": "windows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -206,10 +234,15 @@ def main():
             "kernels_ms": {"k_prep": k1, "k_bg_slice_or_gap": k2, "k_scan_w": k3, "timed_runs": nr,
                            "exact_path_windows": pl.stats()},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "k_scan_w", "ms": k3,
-                         "note": "k_scan_w, algorithmic bytes 8 B/SNP + 80 B/slot per launch over its event-timed "
-                                 "duration; the 8 MB config-2 stream is MALL-resident (see roofline_hbm)"},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_scan_w", "ms": k3, "algorithmic_bytes": b3,
+                         "note": "k_scan_w: algorithmic bytes 4 B/SNP + 96 B/slot per launch over its average "
+                                 "duration (kernel start/end events in the dispatch packets of every 8th timed run); "
+                                 "the 8 MB config-2 stream is MALL-resident (see roofline_hbm for the HBM-sized "
+                                 "stream); traffic: " + (tsrc or "no PMC pass committed")},
+            "roofline_pipeline": {"bound": "hbm", "achieved": bp / step_s / 1e9, "peak": HBM_PEAK_GBS,
+                                  "unit": "GB/s", "frac": bp / step_s / 1e9 / HBM_PEAK_GBS,
+                                  "note": "whole step (SURVEY 8(d): 12 B/SNP + 64 B/window) over ms_per_step"},
         }
         if not args.no_hbm_stream and world == 1:
             line["roofline_hbm"] = hbm_stream_roofline(eng)

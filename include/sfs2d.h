@@ -141,18 +141,22 @@ int sfs2d_plan_bg_buffer(sfs2d_plan* plan, void** dev_ptr, int64_t* nbytes);
 int sfs2d_plan_fst_read(sfs2d_plan* plan, double* out_host, int64_t cap);
 int sfs2d_plan_fst_buffer(sfs2d_plan* plan, void** dev_ptr, int64_t* nslots);
 int sfs2d_plan_run_phase(sfs2d_plan* plan, int phase, sfs2d_window* out_dev);
+/* launch geometry (threads per grid) of k_prep and of the scan kernel: matches the Grid_Size column
+ * of rocprofv3 kernel traces, so profiles can be joined to a plan */
+int sfs2d_plan_grids(const sfs2d_plan* plan, int64_t* prep_threads, int64_t* scan_threads);
 /* cumulative number of windows re-evaluated on the exact path (|T| ~ 0: proportionality test) */
 int sfs2d_plan_stats(sfs2d_plan* plan, uint32_t* exact_windows);
 /* last run's error word (0 = ok, else SFS2D_E_KEY / SFS2D_E_GRID); synchronises */
 int sfs2d_plan_check(sfs2d_plan* plan);
-/* live timing: record HIP events around each kernel of every `every`-th of the following runs,
- * for up to `max_samples` runs (sampling keeps the events' own cost out of the other runs);
- * sfs2d_plan_timing_read averages the sampled runs' per-kernel durations */
+/* live timing: every `every`-th of the following runs (up to `max_samples` of them) launches k_prep
+ * and the scan kernel with start/stop events in their own dispatch packets (hipExtLaunchKernelGGL):
+ * kernel start/end timestamps, the durations rocprofv3 --kernel-trace reports; no extra packets
+ * between kernels.  sfs2d_plan_timing_read averages the sampled runs' per-kernel durations */
 int sfs2d_plan_set_timing(sfs2d_plan* plan, int max_runs);   /* = sampled(plan, max_runs, 1) */
 int sfs2d_plan_set_timing_sampled(sfs2d_plan* plan, int max_samples, int every);
-/* average device time per kernel over the sampled runs (synchronises): k1 = k_prep, k2 = background
- * tables (k_bg_slice; for plans whose scan kernel builds the tables itself, the gap between the two
- * kernels), k3 = the window scan (+ the final-window helper when SFS2D_F_PREV_EXTRA is set) */
+/* average device time per kernel over the sampled runs (synchronises): k1 = k_prep, k2 = end of
+ * k_prep to start of the scan kernel (k_bg_slice when the plan launches it, else the launch gap),
+ * k3 = the window scan kernel (k_scan_w / k_scan_g) */
 int sfs2d_plan_timing_read(sfs2d_plan* plan, int* nruns, double* ms_k1, double* ms_k2, double* ms_k3);
 /* standalone timing loop: average device time per kernel over `iters` runs */
 int sfs2d_plan_time(sfs2d_plan* plan, int iters, double* ms_per_run, double* ms_k1, double* ms_k2, double* ms_k3);
