@@ -2,7 +2,7 @@
 
 Layers: ``pack`` (SNP dict -> SoA), ``_lib`` (ctypes over include/sfs2d.h), ``engine``
 (contexts, resident data, plans), ``post`` (the reference drivers' sequential semantics),
-``ingest`` (VCF + popmap), ``synth`` (seeded synthetic streams), ``dist`` (one process per GPU).
+``vcf`` (native VCF + popmap ingest), ``synth`` (seeded synthetic streams), ``dist`` (one process per GPU).
 """
 from .pack import PackedSNPs, pack_snp_dict, to_snp_dict  # noqa: F401
 

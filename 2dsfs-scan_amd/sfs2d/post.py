@@ -170,6 +170,31 @@ def bysnp_scan(recs, packed, S, with_diff, final_warning):
     return res
 
 
+def window_fst_labels(recs, fst, packed, w, bp):
+    """{window label: Fst or None} in scan order; labels as combined_scan (bp windows: wid) or the
+    bySNPs drivers (first SNP position - last SNP position of each complete S-SNP window) make them."""
+    names = packed.chrom_names
+    out = {}
+    nslots = min(len(fst), num_slots(recs))
+    if bp:
+        for r, f in zip(recs[:nslots], fst[:nslots]):
+            if r["flags"] & L.W_EMPTY:
+                continue
+            s = 1 + int(r["wid"]) * w
+            out[f"{names[int(r['chrom'])]} {s}-{s + w - 1}"] = None if np.isnan(f) else float(f)
+        return out
+    pos = packed.pos
+    start = {}
+    for r, f in zip(recs[:nslots], fst[:nslots]):
+        c = int(r["chrom"])
+        st = start.get(c, int(pos[int(packed.chrom_off[c])]))
+        endp = int(pos[int(r["end"]) - 1])
+        if r["n2_all"] != 0:
+            out[f"{names[c]} {st}-{endp}"] = None if np.isnan(f) else float(f)
+        start[c] = endp + 1
+    return out
+
+
 def sims_process_window(recs, packed, ws, nslots):
     """sims_scan.process_window (451-590): no None guards, T2D_diff = T2D - (T1D_p1 - T1D_p2)/2."""
     names = packed.chrom_names

@@ -1,0 +1,210 @@
+"""VCF(.gz / BGZF) + popmap ingest through the native parser (include/sfs2d_ingest.h).
+
+Drop-in for ``make_data_dict_vcf(vcf_filename, popinfo_filename)`` (twoDSFS_class.py:36-138;
+sims_scan.py:18-120), with its semantics (quirks Q10/Q12/Q13) -- see the header
+for the rules.  ``read_vcf`` returns the parsed columns; from them
+
+* ``VcfTable.to_data_dict()`` rebuilds the reference's dict
+  ``{"CHR-POS": {"segregating", "context", "calls", "annotation"}}`` in the same key order, and
+* ``VcfTable.to_packed(pop1, pop2)`` goes straight to the packed SoA the HIP kernels stream
+  (scan order: chromosome string, then integer position, dict order on ties -- exactly what
+  ``pack_snp_dict(make_data_dict_vcf(...))`` gives, without building the dict).
+
+The parser is C++ (``libsfs2d_ingest.so``, built by ``make -C 2dsfs-scan_amd/csrc``); without it
+every call raises ``Sfs2dError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import List
+
+import numpy as np
+
+from ._lib import Sfs2dError
+from .pack import PackedSNPs, MAX_COUNT
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+INGEST_PATH = os.environ.get("SFS2D_INGEST_LIB", os.path.join(HERE, "..", "csrc", "libsfs2d_ingest.so"))
+
+# exported symbols of include/sfs2d_ingest.h (checked by tests/test_vcf_ingest.py)
+EXPORTS = [
+    "sfs2d_vcf_read", "sfs2d_vcf_free", "sfs2d_vcf_last_error", "sfs2d_vcf_num_records", "sfs2d_vcf_num_pops",
+    "sfs2d_vcf_pop_name", "sfs2d_vcf_num_chroms", "sfs2d_vcf_chrom_name", "sfs2d_vcf_num_annotations",
+    "sfs2d_vcf_annotation", "sfs2d_vcf_columns", "sfs2d_vcf_stats",
+]
+E_INDEX, E_VALUE = -3, -4
+
+_ilib = None
+
+
+def ingest_lib():
+    global _ilib
+    if _ilib is not None:
+        return _ilib
+    if not os.path.exists(INGEST_PATH):
+        raise Sfs2dError(-1, f"native VCF parser not built: {INGEST_PATH} (make -C 2dsfs-scan_amd/csrc)")
+    L = C.CDLL(INGEST_PATH)
+    vp, i32, i64 = C.c_void_p, C.c_int32, C.c_int64
+    L.sfs2d_vcf_read.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.POINTER(vp)]
+    L.sfs2d_vcf_free.argtypes = [vp]
+    L.sfs2d_vcf_last_error.restype = C.c_char_p
+    for f in ("sfs2d_vcf_num_pops", "sfs2d_vcf_num_chroms", "sfs2d_vcf_num_annotations"):
+        getattr(L, f).argtypes = [vp]
+        getattr(L, f).restype = i32
+    L.sfs2d_vcf_num_records.argtypes = [vp]
+    L.sfs2d_vcf_num_records.restype = i64
+    for f in ("sfs2d_vcf_pop_name", "sfs2d_vcf_chrom_name", "sfs2d_vcf_annotation"):
+        getattr(L, f).argtypes = [vp, i32]
+        getattr(L, f).restype = C.c_char_p
+    L.sfs2d_vcf_columns.argtypes = [vp] + [C.POINTER(vp)] * 7
+    L.sfs2d_vcf_stats.argtypes = [vp, C.POINTER(i64), C.POINTER(i64)] + [C.POINTER(C.c_double)] * 3
+    _ilib = L
+    return L
+
+
+def _view(ptr, dtype, count):
+    if count == 0:
+        return np.zeros(0, dtype)
+    buf = (C.c_char * (count * np.dtype(dtype).itemsize)).from_address(ptr)
+    return np.frombuffer(buf, dtype=dtype).copy()
+
+
+@dataclass
+class VcfTable:
+    """Parsed records in dict insertion order (one per distinct CHROM-POS key)."""
+    pops: List[str]
+    chrom_names: List[str]
+    ann_names: List[str]
+    chrom: np.ndarray      # int32 [n]
+    pos: np.ndarray        # int64 [n]; INT64_MIN where POS is not a plain decimal
+    pos_text: List[str]    # POS as written (the key is f"{chrom}-{pos_text}")
+    ann: np.ndarray        # int32 [n]
+    alleles: np.ndarray    # uint8 [n, 2] upper-case REF / ALT
+    calls: np.ndarray      # int32 [n, P, 2]; -1 = population absent from the record
+    stats: dict
+
+    @property
+    def n(self) -> int:
+        return int(len(self.chrom))
+
+    def keys(self) -> List[str]:
+        return [f"{self.chrom_names[c]}-{t}" for c, t in zip(self.chrom.tolist(), self.pos_text)]
+
+    def to_data_dict(self) -> dict:
+        """The reference's make_data_dict_vcf dict (same keys, order, values and types)."""
+        out = {}
+        ref = [chr(x) for x in self.alleles[:, 0].tolist()]
+        alt = [chr(x) for x in self.alleles[:, 1].tolist()]
+        calls = self.calls.tolist()
+        anns = [self.ann_names[a] for a in self.ann.tolist()]
+        for i, key in enumerate(self.keys()):
+            cd = {}
+            for j, (r, a) in enumerate(calls[i]):
+                if r >= 0:
+                    cd[self.pops[j]] = (r, a)
+            out[key] = {"segregating": (ref[i], alt[i]), "context": "-" + ref[i] + "-", "calls": cd,
+                        "annotation": anns[i]}
+        return out
+
+    def to_packed(self, pop1: str = "uv", pop2: str = "bv") -> PackedSNPs:
+        """pack_snp_dict(to_data_dict(), pop1, pop2) without the dict (twoDSFS_class.py:828-835 order)."""
+        for name in self.chrom_names:
+            if "-" in name:
+                raise ValueError(f"too many values to unpack in SNP keys of chromosome {name!r}")
+        pos = self.pos.copy()
+        bad = np.nonzero(pos == np.iinfo(np.int64).min)[0]
+        for i in bad.tolist():
+            t = self.pos_text[i]
+            if "-" in t:
+                raise ValueError(f"too many values to unpack in SNP key {self.chrom_names[self.chrom[i]]}-{t}")
+            pos[i] = int(t)   # ValueError for non-numbers, as int() in the reference's sort key
+        if pos.size and (pos.min() < 0 or pos.max() > 0xFFFFFFFF):
+            raise ValueError("positions must fit in uint32")
+        rank = np.empty(len(self.chrom_names), np.int64)
+        order_names = sorted(range(len(self.chrom_names)), key=lambda c: self.chrom_names[c])
+        rank[order_names] = np.arange(len(order_names))
+        crank = rank[self.chrom] if self.n else np.zeros(0, np.int64)
+        order = np.lexsort((pos, crank))          # stable: dict order among equal (chrom, pos)
+        crank_s = crank[order]
+
+        def pop_counts(pop):
+            if pop not in self.pops:
+                return np.zeros(self.n, np.int64), np.zeros(self.n, np.int64)
+            c = self.calls[order, self.pops.index(pop)].astype(np.int64)
+            c[c < 0] = 0                          # calls.get(pop, (0, 0))
+            return c[:, 0], c[:, 1]
+        r1, a1 = pop_counts(pop1)
+        r2, a2 = pop_counts(pop2)
+        for x in (r1, a1, r2, a2):
+            if x.size and x.max() > MAX_COUNT:
+                raise ValueError("allele counts above 255 do not fit the packed u8x4 layout")
+        counts = (r1.astype(np.uint32) | (a1.astype(np.uint32) << 8) | (r2.astype(np.uint32) << 16)
+                  | (a2.astype(np.uint32) << 24))
+        bounds = np.nonzero(np.diff(crank_s))[0] + 1 if self.n else np.zeros(0, np.int64)
+        offs = np.concatenate([[0], bounds, [self.n]]).astype(np.int64) if self.n else np.zeros(1, np.int64)
+        names = [self.chrom_names[order_names[int(r)]] for r in crank_s[offs[:-1]]] if self.n else []
+        if len(self.ann_names) > 65535:
+            raise ValueError("more than 65535 distinct annotations")
+        return PackedSNPs(counts, pos[order].astype(np.uint32), offs, names,
+                          self.ann[order].astype(np.uint16), list(self.ann_names), pop1, pop2)
+
+
+def read_vcf(vcf_filename, popinfo_filename, nthreads: int = 0) -> VcfTable:
+    """Parse with the native multithreaded parser; raises the reference's exception types."""
+    L = ingest_lib()
+    h = C.c_void_p()
+    rc = L.sfs2d_vcf_read(os.fsencode(str(vcf_filename)), os.fsencode(str(popinfo_filename)), int(nthreads),
+                          C.byref(h))
+    if rc != 0:
+        msg = (L.sfs2d_vcf_last_error() or b"").decode(errors="replace")
+        if rc == E_INDEX:
+            raise IndexError(msg)
+        if rc == E_VALUE:
+            raise ValueError(msg)
+        if rc == -1:
+            raise FileNotFoundError(msg)
+        raise Sfs2dError(rc, msg)
+    try:
+        n = int(L.sfs2d_vcf_num_records(h))
+        P = int(L.sfs2d_vcf_num_pops(h))
+        dec = (lambda b: b.decode("utf-8", "surrogateescape"))
+        pops = [dec(L.sfs2d_vcf_pop_name(h, i)) for i in range(P)]
+        chroms = [dec(L.sfs2d_vcf_chrom_name(h, i)) for i in range(L.sfs2d_vcf_num_chroms(h))]
+        anns = [dec(L.sfs2d_vcf_annotation(h, i)) for i in range(L.sfs2d_vcf_num_annotations(h))]
+        ptrs = [C.c_void_p() for _ in range(7)]
+        L.sfs2d_vcf_columns(h, *[C.byref(p) for p in ptrs])
+        chrom = _view(ptrs[0].value, np.int32, n)
+        pos = _view(ptrs[1].value, np.int64, n)
+        pos_off = _view(ptrs[3].value, np.int64, n + 1)
+        blob = C.string_at(ptrs[2].value, int(pos_off[-1])) if n and pos_off[-1] else b""
+        pos_text = blob.decode("utf-8", "surrogateescape")
+        if len(pos_text) == len(blob):   # ASCII: character offsets are byte offsets
+            po = pos_off.tolist()
+            texts = [pos_text[po[i]:po[i + 1]] for i in range(n)]
+        else:
+            po = pos_off.tolist()
+            texts = [blob[po[i]:po[i + 1]].decode("utf-8", "surrogateescape") for i in range(n)]
+        ann = _view(ptrs[4].value, np.int32, n)
+        alle = _view(ptrs[5].value, np.uint8, 2 * n).reshape(n, 2)
+        calls = _view(ptrs[6].value, np.int32, n * P * 2).reshape(n, P, 2)
+        tb, ln = C.c_int64(), C.c_int64()
+        t = [C.c_double() for _ in range(3)]
+        L.sfs2d_vcf_stats(h, C.byref(tb), C.byref(ln), *[C.byref(x) for x in t])
+        stats = {"text_bytes": tb.value, "lines": ln.value, "t_inflate": t[0].value, "t_parse": t[1].value,
+                 "t_merge": t[2].value}
+    finally:
+        L.sfs2d_vcf_free(h)
+    return VcfTable(pops, chroms, anns, chrom, pos, texts, ann, alle, calls, stats)
+
+
+def make_data_dict_vcf(vcf_filename, popinfo_filename):
+    """twoDSFS_class.py:36-138 / sims_scan.py:18-120: the reference's SNP dict."""
+    return read_vcf(vcf_filename, popinfo_filename).to_data_dict()
+
+
+def make_packed_vcf(vcf_filename, popinfo_filename, pop1: str = "uv", pop2: str = "bv",
+                    nthreads: int = 0) -> PackedSNPs:
+    """VCF + popmap straight to the packed scan-order arrays (no dict)."""
+    return read_vcf(vcf_filename, popinfo_filename, nthreads).to_packed(pop1, pop2)

@@ -20,7 +20,7 @@ import numpy as np
 from sfs2d import _lib as L
 from sfs2d import post
 from sfs2d.engine import Engine, ScanConfig
-from sfs2d.ingest import make_data_dict_vcf  # noqa: F401  (sims_scan.py:18-120)
+from sfs2d.vcf import make_data_dict_vcf  # noqa: F401  (sims_scan.py:18-120)
 from sfs2d.pack import PackedSNPs, pack_snp_dict
 
 _NO_ANN = 1 << 20

@@ -20,7 +20,7 @@ import numpy as np
 from sfs2d import _lib as L
 from sfs2d import post
 from sfs2d.engine import Engine, ScanConfig
-from sfs2d.ingest import make_data_dict_vcf as _make_data_dict_vcf
+from sfs2d.vcf import make_data_dict_vcf as _make_data_dict_vcf
 from sfs2d.pack import PackedSNPs, pack_snp_dict
 
 __all__ = ["LikelihoodInference_jointSFS", "save_csv_stats", "col_names", "chr_ids", "load_chr_ids"]
@@ -90,7 +90,7 @@ class LikelihoodInference_jointSFS:
 
     # ------------------------------------------------------------------ ingest
     def make_data_dict_vcf(self, vcf_filename=None, popinfo_filename=None):
-        """twoDSFS_class.py:36-138 (quirks Q12/Q13 kept; see sfs2d.ingest)."""
+        """twoDSFS_class.py:36-138 (quirks Q12/Q13 kept; see sfs2d.vcf)."""
         return _make_data_dict_vcf(vcf_filename if vcf_filename is not None else self.vcf_filename,
                                    popinfo_filename if popinfo_filename is not None else self.popinfo_filename)
 
@@ -186,6 +186,32 @@ class LikelihoodInference_jointSFS:
         recs = self._scan(p, self._cfg(p, window_mode=L.WINDOW_SNPS, window=snp_window_size,
                                        bg_mode=L.BG_PER_CHROM))
         return post.bysnp_scan(recs, p, snp_window_size, with_diff=True, final_warning=False)
+
+    # ------------------------------------------------------------------ Fst (extension)
+    def window_fst(self, data_dict, window_size=None, snp_window_size=None):
+        """Hudson's Fst per window (not in the reference, whose published FST column is pixy's
+        Weir-Cockerham joined in R, ECBstats_plots.R:16-41): {label: Fst or None}, labels as
+        combined_scan (fixed bp, ``window_size``) or scan_perChr_bySNPs (``snp_window_size``) emit
+        them.  Computed by k_prep on the GPU ("Fst")."""
+        p = self._pack(data_dict)
+        if (window_size is None) == (snp_window_size is None):
+            raise ValueError("give exactly one of window_size / snp_window_size")
+        bp = window_size is not None
+        cfg = self._cfg(p, window_mode=L.WINDOW_BP if bp else L.WINDOW_SNPS,
+                        window=int(window_size if bp else snp_window_size), bg_mode=L.BG_PER_CHROM, fst=True)
+        eng = self._engine()
+        dev = eng.upload(p)
+        try:
+            pl = eng.plan(dev, cfg)
+            try:
+                pl.run()
+                pl.check()
+                recs, fst = pl.read(), pl.read_fst()
+            finally:
+                pl.close()
+        finally:
+            dev.close()
+        return post.window_fst_labels(recs, fst, p, int(window_size if bp else snp_window_size), bp)
 
     # ------------------------------------------------------------------ SFS primitives
     def calculate_2d_sfs(self, data_dict):

@@ -1,4 +1,8 @@
-"""VCF(.gz) + popmap -> SNP dict, with the reference's semantics.
+"""TEST INFRASTRUCTURE ONLY (the oracle): VCF(.gz) + popmap -> SNP dict in plain Python.
+
+Checker for the native parser (2dsfs-scan_amd/csrc/vcf_ingest.cpp, include/sfs2d_ingest.h);
+only tests/ may import it.  Pinned by tests/golden/vcf_expected_*.npz, produced by the
+reference's own make_data_dict_vcf (tests/golden/gen_golden_vcf.py).
 
 Restates ``make_data_dict_vcf`` (twoDSFS_class.py:36-138; sims_scan.py:18-120), including its
 quirks:
