@@ -164,6 +164,13 @@ struct sfs2d_plan {
   // go into the kernels' own dispatch packets (hipExtLaunchKernelGGL), so they stamp the kernel's
   // start and end as the command processor sees them -- the durations rocprofv3 reports.
   hipEvent_t kev[4] = {nullptr, nullptr, nullptr, nullptr};
+  // multi-resolution (sfs2d_plan_attach): an attached plan shares its base's k_prep pass (bins,
+  // background replicas, inner sums); the base's run scans every attached plan before its own
+  std::vector<unsigned long long> slot_base_h;   // window slots per chromosome (prefix sums)
+  uint32_t* d_slot_base = nullptr;
+  sfs2d_plan* base = nullptr;
+  std::vector<sfs2d_plan*> attached;
+  uint32_t fst_m = 0;             // attached Fst: base windows per window (their sums add)
 };
 
 namespace {
@@ -190,6 +197,12 @@ int dalloc(sfs2d_ctx* ctx, T** p, size_t count) {
 }
 
 void plan_free(sfs2d_plan* p) {
+  if (p->base) {   // shared with the base plan
+    p->d_bins = nullptr;
+    p->d_repl = nullptr;
+    p->d_bcount = nullptr;
+  }
+  hipFree(p->d_slot_base);
   hipFree(p->d_tiles); hipFree(p->d_chunks); hipFree(p->d_slots); hipFree(p->d_repl); hipFree(p->d_bcount); hipFree(p->d_ctr);
   hipFree(p->d_done); hipFree(p->d_bgval); hipFree(p->d_tab); hipFree(p->d_lp); hipFree(p->d_head);
   hipFree(p->d_bg1d); hipFree(p->d_leafsum); hipFree(p->d_leaves); hipFree(p->d_nodes); hipFree(p->d_slices);
@@ -198,7 +211,8 @@ void plan_free(sfs2d_plan* p) {
   for (auto& e : p->tev) if (e) hipEventDestroy(e);
 }
 
-int plan_par(const sfs2d_plan* pl) { return pl->fused ? (int)(pl->runs & 1) : 0; }
+// replica parity of the current run (an attached plan reads its base's k_prep output)
+int plan_par(const sfs2d_plan* pl) { return pl->fused ? (int)((pl->base ? pl->base->runs : pl->runs) & 1) : 0; }
 
 template <bool P16, bool FUSED, bool FST>
 void launch_scan_w(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
@@ -301,6 +315,25 @@ hipError_t launch_scan_any(sfs2d_plan* pl, sfs2d_window* out) {
   hipError_t e = hipSuccess;
   if (!pl->chunks.empty()) e = pl->p16 ? launch_scan<true>(pl, out) : launch_scan<false>(pl, out);
   if (e == hipSuccess && pl->extra_rec >= 0) e = pl->p16 ? launch_extra<true>(pl, out) : launch_extra<false>(pl, out);
+  return e;
+}
+
+// one attached plan inside its base's run: its window slots (fixed bp: binary search on the
+// positions), its Fst sums (from the base's), then its scan against the base's k_prep output
+hipError_t launch_attached(sfs2d_plan* a) {
+  const sfs2d_data* d = a->data;
+  const uint32_t ns = (uint32_t)a->nslots;
+  if (!ns) { a->runs++; return hipSuccess; }
+  const dim3 g((ns + 255) / 256);
+  if (a->prm.window_mode == SFS2D_WINDOW_BP)
+    hipLaunchKernelGGL(k_slots_bp, g, dim3(256), 0, a->ctx->stream, d->pos, d->d_chrom_off, a->d_slot_base,
+                       d->nchrom, (uint32_t)a->prm.window, ns, a->d_slots);
+  if (a->fst_m)
+    hipLaunchKernelGGL(k_fst_agg, g, dim3(256), 0, a->ctx->stream, a->base->d_fsum, a->base->d_slot_base,
+                       a->d_slot_base, d->nchrom, a->fst_m, ns, a->d_fsum);
+  const hipError_t e = launch_scan_any(a, a->d_out);
+  a->last_out = a->d_out;
+  a->runs++;
   return e;
 }
 
@@ -513,6 +546,7 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
     slot_base[c + 1] = slot_base[c] + ns;
   }
   pl->nslots = (int64_t)slot_base[nc];
+  pl->slot_base_h = slot_base;
   if (pl->nslots > 0x7fffffffll) { delete pl; return set_err(ctx, SFS2D_E_ARG, "too many window slots (window too small)"); }
   pl->extra_rec = ((prm->flags & SFS2D_F_PREV_EXTRA) && bp && any) ? pl->nslots : -1;
   pl->nrec = pl->nslots + (pl->extra_rec >= 0 ? 1 : 0);
@@ -772,6 +806,7 @@ int sfs2d_plan_set_background(sfs2d_plan* pl, const double* bg2d, const double* 
 int sfs2d_plan_run_phase(sfs2d_plan* pl, int phase, sfs2d_window* out_dev) {
   if (!pl) return SFS2D_E_ARG;
   sfs2d_ctx* ctx = pl->ctx;
+  if (pl->base) return set_err(ctx, SFS2D_E_ARG, "an attached plan runs with its base plan (sfs2d_plan_attach)");
   HIPCHK(ctx, hipSetDevice(ctx->device));
   hipEvent_t* te = nullptr;
   if (pl->timing && phase == 0 && (pl->tseen++ % pl->tevery) == 0 && pl->tcount * 4 < (int)pl->tev.size())
@@ -794,6 +829,7 @@ int sfs2d_plan_run_phase(sfs2d_plan* pl, int phase, sfs2d_window* out_dev) {
   pl->kev[0] = pl->kev[1] = nullptr;
   if (phase == 0 || phase == 2) {
     if (pl->do_bg && !pl->fused) HIPCHK(ctx, launch_bg_slices(pl));
+    for (sfs2d_plan* a : pl->attached) HIPCHK(ctx, launch_attached(a));   // before the base clears its state
     sfs2d_window* out = out_dev ? out_dev : pl->d_out;
     if (te && pl->chunks.empty()) {
       HIPCHK(ctx, hipEventRecord(te[2], ctx->stream));
@@ -957,6 +993,7 @@ int sfs2d_plan_time(sfs2d_plan* pl, int iters, double* ms_run, double* ms_k1, do
     HIPCHK(ctx, launch_prep(pl, true));
     HIPCHK(ctx, hipEventRecord(pl->ev[1], st));
     if (pl->do_bg && !pl->fused) HIPCHK(ctx, launch_bg_slices(pl));
+    for (sfs2d_plan* a : pl->attached) HIPCHK(ctx, launch_attached(a));
     HIPCHK(ctx, hipEventRecord(pl->ev[2], st));
     HIPCHK(ctx, launch_scan_any(pl, pl->d_out));
     pl->runs++;
@@ -981,8 +1018,69 @@ int sfs2d_plan_destroy(sfs2d_plan* pl) {
   if (!pl) return SFS2D_E_ARG;
   hipSetDevice(pl->ctx->device);
   hipStreamSynchronize(pl->ctx->stream);
+  for (sfs2d_plan* a : pl->attached) {   // attached plans go with their base
+    a->base = pl;
+    plan_free(a);
+    delete a;
+  }
+  pl->attached.clear();
+  if (pl->base) {
+    auto& v = pl->base->attached;
+    v.erase(std::remove(v.begin(), v.end(), pl), v.end());
+  }
   plan_free(pl);
   delete pl;
+  return 0;
+}
+
+int sfs2d_plan_attach(sfs2d_plan* base, const sfs2d_params* prm, sfs2d_plan** out) {
+  if (!base || !prm || !out) return SFS2D_E_ARG;
+  sfs2d_ctx* ctx = base->ctx;
+  *out = nullptr;
+  if (base->base) return set_err(ctx, SFS2D_E_ARG, "attach to a base plan, not to an attached one");
+  if (!base->fused)
+    return set_err(ctx, SFS2D_E_ARG, "attached plans need a per-chromosome-background base plan on the small-grid path");
+  const sfs2d_params& b = base->prm;
+  if (prm->n1p != b.n1p || prm->n2p != b.n2p || (prm->fold != 0) != (b.fold != 0) || prm->bg_mode != b.bg_mode ||
+      prm->ann_want != b.ann_want || prm->has_start != b.has_start || prm->has_end != b.has_end ||
+      (prm->has_start && prm->start_pos != b.start_pos) || (prm->has_end && prm->end_pos != b.end_pos))
+    return set_err(ctx, SFS2D_E_ARG, "an attached plan may differ from its base only in the window and flags");
+  const bool bp = prm->window_mode == SFS2D_WINDOW_BP;
+  uint32_t m = 0;
+  if (prm->flags & SFS2D_F_FST) {
+    const bool base_bp = b.window_mode == SFS2D_WINDOW_BP;
+    if (!(b.flags & SFS2D_F_FST) || !base_bp || !bp || prm->window % b.window != 0)
+      return set_err(ctx, SFS2D_E_ARG, "attached Fst needs a fixed-bp Fst base plan whose window divides this one's");
+    m = (uint32_t)(prm->window / b.window);
+  }
+  sfs2d_plan* a = nullptr;
+  int rc = sfs2d_plan_create(ctx, base->data, prm, &a);
+  if (rc) return rc;
+  if (!a->fused || a->G != base->G) {
+    plan_free(a); delete a;
+    return set_err(ctx, SFS2D_E_ARG, "attached plan would take a different kernel path than its base");
+  }
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  hipFree(a->d_bins); hipFree(a->d_repl); hipFree(a->d_bcount);
+  a->d_bins = base->d_bins;
+  a->d_repl = base->d_repl;
+  a->d_bcount = base->d_bcount;
+  a->base = base;
+  a->fst_m = m;
+  rc = 0;
+  std::vector<uint32_t> sb(a->slot_base_h.begin(), a->slot_base_h.end());
+  rc = rc ? rc : dalloc(ctx, &a->d_slot_base, sb.size());
+  if (m && !base->d_slot_base) {
+    std::vector<uint32_t> bsb(base->slot_base_h.begin(), base->slot_base_h.end());
+    rc = rc ? rc : dalloc(ctx, &base->d_slot_base, bsb.size());
+    if (!rc && hipMemcpy(base->d_slot_base, bsb.data(), sizeof(uint32_t) * bsb.size(), hipMemcpyHostToDevice) != hipSuccess)
+      rc = SFS2D_E_HIP;
+  }
+  if (!rc && hipMemcpy(a->d_slot_base, sb.data(), sizeof(uint32_t) * sb.size(), hipMemcpyHostToDevice) != hipSuccess)
+    rc = SFS2D_E_HIP;
+  if (rc) { plan_free(a); delete a; return rc == SFS2D_E_HIP ? set_err(ctx, rc, "attach: copy") : rc; }
+  base->attached.push_back(a);
+  *out = a;
   return 0;
 }
 

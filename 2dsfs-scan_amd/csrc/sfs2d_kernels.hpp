@@ -1843,3 +1843,64 @@ __global__ __launch_bounds__(WAVE) void k_scan_extra(KParams P, const uint32_t* 
 }
 
 }  // namespace sfs2dk
+
+// ------------------------------------------------------------------------------------------ multi-resolution
+
+// Fixed-bp window slots of a plan attached to another plan's k_prep pass (several window sizes from
+// one read of the SNP stream; the reference script runs 20 kb, 500 kb and SNP-count scans over the
+// same data, twoDSFS_class.py:1923-2032).  One thread per slot: window j of chromosome c holds the
+// SNPs with (pos-1)//ws == j (pos 0 -> window 0, as wid_of), found by binary search on the sorted
+// positions: slot = (first + 1, last + 1), (0, 0) when empty -- what k_prep's segmentation writes.
+__device__ __forceinline__ uint32_t lower_bound_pos(const uint32_t* __restrict__ pos, uint32_t lo, uint32_t hi,
+                                                    unsigned long long v) {
+  while (lo < hi) {
+    const uint32_t mid = lo + ((hi - lo) >> 1);
+    if ((unsigned long long)pos[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void k_slots_bp(const uint32_t* __restrict__ pos, const long long* __restrict__ chrom_off,
+                                                  const uint32_t* __restrict__ slot_base, int nchrom, uint32_t ws,
+                                                  uint32_t nslots, uint2* __restrict__ slots) {
+  const uint32_t s = blockIdx.x * 256u + threadIdx.x;
+  if (s >= nslots) return;
+  int lo = 0, hi = nchrom;   // chromosome c with slot_base[c] <= s < slot_base[c+1]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (slot_base[mid] <= s) lo = mid;
+    else hi = mid;
+  }
+  const uint32_t j = s - slot_base[lo];
+  const uint32_t cb = (uint32_t)chrom_off[lo], ce = (uint32_t)chrom_off[lo + 1];
+  const uint32_t b = j ? lower_bound_pos(pos, cb, ce, (unsigned long long)j * ws + 1ull) : cb;
+  const uint32_t e = lower_bound_pos(pos, b, ce, (unsigned long long)(j + 1) * ws + 1ull);
+  slots[s] = b < e ? make_uint2(b + 1u, e) : make_uint2(0u, 0u);
+}
+
+// Fst sums of an attached fixed-bp plan whose window is m times the base plan's: window j of
+// chromosome c is base windows [j*m, (j+1)*m) of c, and the base's int64 fixed-point sums add
+// exactly (the same value as k_prep accumulating the attached windows directly).
+__global__ __launch_bounds__(256) void k_fst_agg(const unsigned long long* __restrict__ bsum,
+                                                 const uint32_t* __restrict__ bslot_base,
+                                                 const uint32_t* __restrict__ slot_base, int nchrom, uint32_t m,
+                                                 uint32_t nslots, unsigned long long* __restrict__ fsum) {
+  const uint32_t s = blockIdx.x * 256u + threadIdx.x;
+  if (s >= nslots) return;
+  int lo = 0, hi = nchrom;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (slot_base[mid] <= s) lo = mid;
+    else hi = mid;
+  }
+  const uint32_t j = s - slot_base[lo];
+  const uint32_t b0 = bslot_base[lo] + j * m, b1 = min(b0 + m, bslot_base[lo + 1]);
+  unsigned long long qn = 0, qd = 0;
+  for (uint32_t b = b0; b < b1; ++b) {
+    qn += bsum[2 * (size_t)b];
+    qd += bsum[2 * (size_t)b + 1];
+  }
+  fsum[2 * (size_t)s] = qn;
+  fsum[2 * (size_t)s + 1] = qd;
+}

@@ -32,7 +32,7 @@ EXPORTS = [
     "sfs2d_plan_fst_read", "sfs2d_plan_fst_buffer", "sfs2d_plan_read",
     "sfs2d_plan_bg_buffer", "sfs2d_plan_run_phase", "sfs2d_plan_check", "sfs2d_plan_time",
     "sfs2d_plan_destroy", "sfs2d_scan", "sfs2d_plan_set_timing", "sfs2d_plan_timing_read",
-    "sfs2d_plan_stats", "sfs2d_plan_grids",
+    "sfs2d_plan_stats", "sfs2d_plan_grids", "sfs2d_plan_attach",
 ]
 
 
@@ -98,6 +98,7 @@ def lib():
     L.sfs2d_plan_set_timing.argtypes = [vp, C.c_int]
     L.sfs2d_plan_stats.argtypes = [vp, C.POINTER(C.c_uint32)]
     L.sfs2d_plan_grids.argtypes = [vp, C.POINTER(i64), C.POINTER(i64)]
+    L.sfs2d_plan_attach.argtypes = [vp, C.POINTER(Params), C.POINTER(vp)]
     L.sfs2d_plan_timing_read.argtypes = [vp, C.POINTER(C.c_int)] + [C.POINTER(C.c_double)] * 3
     L.sfs2d_scan.argtypes = [vp, vp, C.POINTER(Params), vp, vp, vp, vp, i64, C.POINTER(i64)]
     _lib = L

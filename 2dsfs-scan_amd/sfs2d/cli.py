@@ -5,7 +5,7 @@ scripts/src/twoDSFS_class.py (1788-2040): load the SNP dict, run ``combined_scan
 500 kb and ``scan_perChr_bySNPs`` at 500 / 300 SNPs, and write each result with
 ``save_csv_stats`` (1884-1907; chromosome accessions renamed through chromosomes.txt, 1788-1797).
 This CLI runs the same drivers on the GPU path, from the native VCF parser straight to the packed
-arrays (no dict), one resident upload for every window size:
+arrays (no dict), every window size from one resident upload and one k_prep pass (multi_scan):
 
     python -m sfs2d VCF POPMAP --window 20000 --window 500000 --snp-window 500 \\
         --chromosomes chromosomes.txt --out-prefix ECBstats [--fst | --pixy-fst fst_20kb.csv]
@@ -98,24 +98,23 @@ def main(argv=None):
                                          pop2_size=a.pop2_size, variant_type=a.variant_type, fold=not a.no_fold,
                                          device=a.device)
     outs = []
+    t = time.perf_counter()
+    # every window size from one k_prep pass over the resident stream (sfs2d_plan_attach)
+    res = obj.multi_scan(packed, a.window, a.snp_window, fst=a.fst)
+    print(f"multi_scan ({len(a.window)} bp + {len(a.snp_window)} SNP-count window sizes): "
+          f"{time.perf_counter() - t:.2f} s", file=sys.stderr)
     for ws in a.window:
-        t = time.perf_counter()
-        stats = obj.combined_scan(packed, ws)
-        fst = obj.window_fst(packed, window_size=ws) if a.fst else None
         path = f"{a.out_prefix}_{_fmt_kb(ws)}.csv"
-        write_csv(path, stats, chr_ids, fst, pixy)
+        write_csv(path, res[ws], chr_ids, res["fst"][ws] if a.fst else None, pixy)
         outs.append(path)
-        print(f"combined_scan {ws} bp: {len(stats)} windows in {time.perf_counter() - t:.2f} s -> {path}",
-              file=sys.stderr)
+        print(f"combined_scan {ws} bp: {len(res[ws])} windows -> {path}", file=sys.stderr)
     for S in a.snp_window:
-        t = time.perf_counter()
-        stats = obj.scan_perChr_bySNPs(packed, S)
+        stats = res[f"{S}snps"]
         fst = obj.window_fst(packed, snp_window_size=S) if a.fst else None
         path = f"{a.out_prefix}_{S}snps.csv"
         write_csv(path, stats, chr_ids, fst, pixy)
         outs.append(path)
-        print(f"scan_perChr_bySNPs {S} SNPs: {len(stats)} windows in {time.perf_counter() - t:.2f} s -> {path}",
-              file=sys.stderr)
+        print(f"scan_perChr_bySNPs {S} SNPs: {len(stats)} windows -> {path}", file=sys.stderr)
     return outs
 
 

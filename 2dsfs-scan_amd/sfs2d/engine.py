@@ -139,12 +139,22 @@ class DeviceData:
 
 
 class Plan:
-    def __init__(self, eng: Engine, data: DeviceData, cfg: ScanConfig):
-        self.eng, self.data, self.cfg = eng, data, cfg
+    def __init__(self, eng: Engine, data: DeviceData, cfg: ScanConfig, base: "Optional[Plan]" = None):
+        self.eng, self.data, self.cfg, self.base = eng, data, cfg, base
         self.h = C.c_void_p()
+        self.attached = []
         prm = cfg.params()
-        eng.check(eng.lib.sfs2d_plan_create(eng.h, data.h, C.byref(prm), C.byref(self.h)))
+        if base is None:
+            eng.check(eng.lib.sfs2d_plan_create(eng.h, data.h, C.byref(prm), C.byref(self.h)))
+        else:
+            eng.check(eng.lib.sfs2d_plan_attach(base.h, C.byref(prm), C.byref(self.h)))
+            base.attached.append(self)
         self.nrec = int(eng.lib.sfs2d_plan_num_records(self.h))
+
+    def attach(self, cfg: ScanConfig) -> "Plan":
+        """A plan scanned from this plan's k_prep pass (another window size / SNP-count windows):
+        run this (base) plan, then read the attached one (sfs2d_plan_attach)."""
+        return Plan(self.eng, self.data, cfg, base=self)
 
     def set_background(self, bg2d, bg1a, bg1b):
         n1p, n2p = self.cfg.n1p, self.cfg.n2p

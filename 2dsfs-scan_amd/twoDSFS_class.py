@@ -187,6 +187,55 @@ class LikelihoodInference_jointSFS:
                                        bg_mode=L.BG_PER_CHROM))
         return post.bysnp_scan(recs, p, snp_window_size, with_diff=True, final_warning=False)
 
+    # ------------------------------------------------------------------ multi-resolution (extension)
+    def multi_scan(self, data_dict, window_sizes=(), snp_window_sizes=(), fst=False):
+        """combined_scan at every size in ``window_sizes`` and scan_perChr_bySNPs at every size in
+        ``snp_window_sizes`` from ONE pass over the SNP stream (the reference script runs these
+        scans one after another over the same data, twoDSFS_class.py:1923-2032): the smallest
+        fixed-bp scan is the base plan, the others are attached to it (sfs2d_plan_attach).
+        Returns {ws: combined_scan result, "<S>snps": scan_perChr_bySNPs result}, plus
+        {"fst": {ws: window_fst result}} when ``fst`` (fixed-bp windows only)."""
+        p = self._pack(data_dict)
+        bps = sorted(set(int(w) for w in window_sizes))
+        snps = [int(x) for x in dict.fromkeys(snp_window_sizes)]
+        if not bps and not snps:
+            return {}
+        specs = [("bp", w) for w in bps] + [("snps", S) for S in snps]
+        base_ws = bps[0] if bps else None
+
+        def cfg_of(kind, w):
+            bp = kind == "bp"
+            want_fst = fst and bp and base_ws is not None and w % base_ws == 0
+            return self._cfg(p, window_mode=L.WINDOW_BP if bp else L.WINDOW_SNPS, window=w,
+                             bg_mode=L.BG_PER_CHROM, prev_extra=bp, fst=want_fst)
+        eng = self._engine()
+        dev = eng.upload(p)
+        out = {}
+        try:
+            base = eng.plan(dev, cfg_of(*specs[0]))
+            try:
+                plans = [base] + [base.attach(cfg_of(*sp)) for sp in specs[1:]]
+                base.run()
+                base.check()
+                for (kind, w), pl in zip(specs, plans):
+                    pl.check()
+                    recs = pl.read()
+                    if kind == "bp":
+                        out[w] = post.combined_scan(recs, p, w, post.num_slots(recs))
+                        if pl.cfg.fst:
+                            out.setdefault("fst", {})[w] = post.window_fst_labels(recs, pl.read_fst(), p, w, True)
+                    else:
+                        out[f"{w}snps"] = post.bysnp_scan(recs, p, w, with_diff=True, final_warning=False)
+            finally:
+                base.close()
+        finally:
+            dev.close()
+        if fst:
+            for w in bps:
+                if w not in out.get("fst", {}):
+                    out.setdefault("fst", {})[w] = self.window_fst(p, window_size=w)
+        return out
+
     # ------------------------------------------------------------------ Fst (extension)
     def window_fst(self, data_dict, window_size=None, snp_window_size=None):
         """Hudson's Fst per window (not in the reference, whose published FST column is pixy's

@@ -141,6 +141,17 @@ int sfs2d_plan_bg_buffer(sfs2d_plan* plan, void** dev_ptr, int64_t* nbytes);
 int sfs2d_plan_fst_read(sfs2d_plan* plan, double* out_host, int64_t cap);
 int sfs2d_plan_fst_buffer(sfs2d_plan* plan, void** dev_ptr, int64_t* nslots);
 int sfs2d_plan_run_phase(sfs2d_plan* plan, int phase, sfs2d_window* out_dev);
+/* Multi-resolution: attach to `base` (a per-chromosome-background plan on the small-grid path) a
+ * plan over the same data whose params differ only in window_mode / window / flags.  The base's
+ * run then makes ONE k_prep pass over the SNP stream (background histograms, per-SNP bins, the
+ * base's segmentation and Fst sums) and scans every attached plan from it before its own scan:
+ * fixed-bp windows get their slots by binary search on the resident positions, SNP-count windows
+ * need none; SFS2D_F_FST on an attached plan needs a fixed-bp Fst base whose window divides the
+ * attached window (the base's per-window int64 fixed-point sums add exactly).  The reference
+ * script scans the same data at 20 kb, 500 kb and 500 / 300 SNPs (twoDSFS_class.py:1923-2032).
+ * An attached plan is not run on its own (its run calls fail); read it with sfs2d_plan_read /
+ * sfs2d_plan_fst_read after the base's run.  Destroying the base destroys its attached plans. */
+int sfs2d_plan_attach(sfs2d_plan* base, const sfs2d_params* params, sfs2d_plan** out);
 /* launch geometry (threads per grid) of k_prep and of the scan kernel: matches the Grid_Size column
  * of rocprofv3 kernel traces, so profiles can be joined to a plan */
 int sfs2d_plan_grids(const sfs2d_plan* plan, int64_t* prep_threads, int64_t* scan_threads);

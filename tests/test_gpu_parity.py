@@ -361,3 +361,34 @@ def test_called_counts_above_sample_size_inside_long_tiles():
     for g, (c, st, b, e) in list(zip(got, wins))[::7]:
         assert _fst_close(float(g), O.window_fst(q, np.arange(b, e), ocfg)), (g, b, e)
     pl.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ws,n1p,n2p", [(100000, 11, 11), (500000, 11, 11), (500000, 18, 14), (2000000, 25, 25)])
+def test_sparse_windows_all_present(ws, n1p, n2p):
+    """LD-pruned real SNPs (tests/golden/vcf_test.vcf.gz via the native parser): every non-empty
+    fixed-bp window is scanned with exactly its SNP range, whatever wave of its workgroup owns it
+    (a grid whose replica table is smaller than the workgroup once left waves without their first
+    window)."""
+    import os
+    from sfs2d import _lib as L
+    from sfs2d.engine import Engine, ScanConfig
+    from sfs2d.vcf import read_vcf
+    g = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    p = read_vcf(os.path.join(g, "vcf_test.vcf.gz"), os.path.join(g, "popmap_3pop.txt")).to_packed("uv", "bv")
+    eng = Engine.get(0)
+    dev = eng.upload(p)
+    try:
+        recs = eng.scan(dev, ScanConfig(n1p=n1p, n2p=n2p, window=ws))
+    finally:
+        dev.close()
+    got = {(int(r["chrom"]), int(r["wid"])): (int(r["begin"]), int(r["end"])) for r in recs
+           if not r["flags"] & L.W_EMPTY}
+    exp = {}
+    for c in range(p.nchrom):
+        lo, hi = int(p.chrom_off[c]), int(p.chrom_off[c + 1])
+        w = (p.pos[lo:hi].astype(np.int64) - 1) // ws
+        for u in np.unique(w):
+            ii = np.nonzero(w == u)[0]
+            exp[(c, int(u))] = (lo + int(ii[0]), lo + int(ii[-1]) + 1)
+    assert got == exp

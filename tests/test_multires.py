@@ -1,0 +1,81 @@
+"""Multi-resolution scans (sfs2d_plan_attach / LikelihoodInference_jointSFS.multi_scan): every window
+size from one k_prep pass must give exactly what the single-size drivers give, and the chr1 case the
+reference's own outputs (tests/golden, twoDSFS_class.py:787-991, 1422-1541)."""
+import numpy as np
+import pytest
+
+import golden_util as gu
+
+pytestmark = pytest.mark.gpu
+
+_G = gu.Golden()
+
+
+def _obj(n1p, n2p, pop1="uv", pop2="bv"):
+    import twoDSFS_class as T
+    return T.LikelihoodInference_jointSFS(None, None, pop1=pop1, pop2=pop2, pop1_size=n1p, pop2_size=n2p)
+
+
+def _same(a, b):
+    assert list(a) == list(b)
+    for k in a:
+        assert a[k] == b[k] or all(gu.close(a[k][f], b[k][f]) for f in a[k]), k
+
+
+def test_chr1_against_reference():
+    p = _G.packed("chr1")
+    cfg = _G.cfg("chr1")
+    obj = _obj(cfg["n1p"], cfg["n2p"], cfg["pop1"], cfg["pop2"])
+    res = obj.multi_scan(p, [500000, 20000], [500])
+    calls = {(c["fn"], tuple(c["args"])): c for c in _G.calls("chr1")}
+    for key, got in ((("combined_scan", (20000,)), res[20000]), (("combined_scan", (500000,)), res[500000]),
+                     (("scan_perChr_bySNPs", (500,)), res["500snps"])):
+        ref = gu.decode_results(calls[key]["out"]["results"])
+        errs = gu.compare_results(got, ref)
+        assert not errs, (key, errs[:5])
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_matches_single_plans(seed):
+    from sfs2d.synth import synth_genome
+    p = synth_genome(3, [40000, 25000, 9000], 25, 25, seed=seed)
+    obj = _obj(25, 25)
+    res = obj.multi_scan(p, [20000, 100000, 60000, 500000], [500, 300], fst=True)
+    for ws in (20000, 60000, 100000, 500000):
+        _same(res[ws], obj.combined_scan(p, ws))
+        single = obj.window_fst(p, window_size=ws)
+        assert list(res["fst"][ws]) == list(single)
+        for k, v in single.items():
+            w = res["fst"][ws][k]
+            assert (v is None and w is None) or abs(w - v) <= 1e-9 * max(1.0, abs(v)), (ws, k, w, v)
+    for S in (500, 300):
+        _same(res[f"{S}snps"], obj.scan_perChr_bySNPs(p, S))
+
+
+def test_repeated_runs_identical():
+    from sfs2d import _lib as L
+    from sfs2d.engine import Engine, ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(2, [30000, 12000], 25, 25, seed=7)
+    eng = Engine.get(0)
+    dev = eng.upload(p)
+    try:
+        base = eng.plan(dev, ScanConfig(n1p=25, n2p=25, window=20000, prev_extra=True, fst=True))
+        a1 = base.attach(ScanConfig(n1p=25, n2p=25, window=500000, prev_extra=True, fst=True))
+        a2 = base.attach(ScanConfig(n1p=25, n2p=25, window_mode=L.WINDOW_SNPS, window=500))
+        with pytest.raises(Exception):
+            a1.run()   # attached plans run with their base
+        outs = []
+        for _ in range(3):
+            base.run()
+            base.check()
+            outs.append([pl.read().tobytes() for pl in (base, a1, a2)] + [a1.read_fst().tobytes()])
+        assert outs[0] == outs[1] == outs[2]
+        with pytest.raises(Exception):   # Fst on a window the base's does not divide
+            base.attach(ScanConfig(n1p=25, n2p=25, window=30000, fst=True))
+        with pytest.raises(Exception):   # a different grid
+            base.attach(ScanConfig(n1p=20, n2p=25, window=500000))
+        base.close()
+        assert not a1.h and not a2.h
+    finally:
+        dev.close()
