@@ -225,6 +225,11 @@ class Plan:
 
     def close(self):
         if self.h:
+            for a in self.attached:   # destroyed by the library together with this base
+                a.h = C.c_void_p()
+            self.attached = []
+            if self.base is not None and self in self.base.attached:
+                self.base.attached.remove(self)
             self.eng.lib.sfs2d_plan_destroy(self.h)
             self.h = C.c_void_p()
 
