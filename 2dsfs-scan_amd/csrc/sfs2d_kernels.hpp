@@ -426,7 +426,9 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
   // FST: per-window sums of the Fst terms, int64 fixed point (num, den) for the tile's first
   // FST_LDS windows (FST_R copies each), the rest straight to the global per-slot sums
   __shared__ unsigned long long sh_fst[FST ? 2 * FST_R * FST_LDS : 1];
-  __shared__ double2 sh_rcp[FST ? RCPN : 1];
+  // the fast path's called counts are in the grid (n <= 2*pop_size <= 254): half the table in LDS;
+  // the exact path (any u8 counts, n <= 510) reads the global table
+  __shared__ double2 sh_rcp[FST ? RCPN / 2 : 1];
   __shared__ uint32_t sh_wlo;
   STAMP(20);
   BLK_STAMP(0, 0);
@@ -438,7 +440,7 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
   const int trash = P.nh * hr + lane0;   // LDS word after the histogram (64 of them)
   if (FST) {
     for (int k = threadIdx.x; k < 2 * FST_R * FST_LDS; k += BLOCK1) sh_fst[k] = 0ull;
-    for (int k = threadIdx.x; k < RCPN; k += BLOCK1) sh_rcp[k] = rcp_g[k];
+    for (int k = threadIdx.x; k < RCPN / 2; k += BLOCK1) sh_rcp[k] = rcp_g[k];
     if (threadIdx.x == 0) sh_wlo = DO_SEG ? wid_fast(P, pos[t.begin]) : div_fast(P, t.begin - t.cb);
   }
   if (DO_BG) {
@@ -544,7 +546,7 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         double nk, dk;
-        fst_snp(cc[k], fm[k], sh_rcp, nk, dk);
+        fst_snp(cc[k], fm[k], rcp_g, nk, dk);
         if (fm[k]) fst_add(fw[k], nk, dk);
       }
     }

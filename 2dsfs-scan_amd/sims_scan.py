@@ -148,11 +148,69 @@ def process_window(data_dict, bg_2d_sfs, bg_p1_sfs, bg_p2_sfs, window_size, pop1
     return post.sims_process_window(recs, p, window_size, post.num_slots(recs))
 
 
+def _concat(packs):
+    """Replicates -> one packed data set (each replicate's chromosomes one after the other; the
+    annotation tables merged).  Returns the data set and each replicate's first chromosome index."""
+    names, counts, pos, ann, offs, base = [], [], [], [], [0], []
+    ann_names, ann_ix = [], {}
+    for q in packs:
+        base.append(len(names))
+        names.extend(q.chrom_names)
+        counts.append(q.counts)
+        pos.append(q.pos)
+        remap = np.zeros(max(1, len(q.ann_names)), np.uint16)
+        for i, a in enumerate(q.ann_names):
+            if a not in ann_ix:
+                ann_ix[a] = len(ann_names)
+                ann_names.append(a)
+            remap[i] = ann_ix[a]
+        ann.append(remap[q.ann_id] if q.n else np.zeros(0, np.uint16))
+        offs.extend((offs[-1] + q.chrom_off[1:]).tolist())
+    cat = (lambda xs, dt: np.concatenate(xs) if xs else np.zeros(0, dt))
+    return PackedSNPs(cat(counts, np.uint32), cat(pos, np.uint32), np.array(offs, np.int64), names,
+                      cat(ann, np.uint16), ann_names), base
+
+
+def process_windows_batch(replicates, bg_2d_sfs, bg_p1_sfs, bg_p2_sfs, window_size, pop1, pop2, pop1_size,
+                          pop2_size, start_position=None, end_position=None, variant_type=None):
+    """``process_window`` (sims_scan.py:451-590) over many replicate data sets in ONE scan launch:
+    all replicates resident in HBM as one data set, one supplied background, one plan.  Returns the
+    list of per-replicate result dicts, each equal to ``process_window(replicate, ...)``; the first
+    replicate (in order) whose window has no SNP / an empty background raises ZeroDivisionError, as
+    the reference's loop over replicates would (sims_scan.py:619-622)."""
+    packs = [_pack(d, pop1, pop2) for d in replicates]
+    if not packs:
+        return []
+    data, base = _concat(packs)
+    eng = Engine.get(DEVICE)
+    cfg = ScanConfig(n1p=pop1_size, n2p=pop2_size, fold=True, window_mode=L.WINDOW_BP, window=window_size,
+                     bg_mode=L.BG_SUPPLIED, ann_want=_ann(data, variant_type),
+                     start_position=None if start_position is None else int(start_position),
+                     end_position=None if end_position is None else int(end_position))
+    bg = _bg_arrays(bg_2d_sfs, bg_p1_sfs, bg_p2_sfs, pop1_size, pop2_size)
+    dev = eng.upload(data)
+    try:
+        recs = eng.scan(dev, cfg, bg)
+    finally:
+        dev.close()
+    chrom = recs["chrom"].astype(np.int64)
+    out = []
+    for i, q in enumerate(packs):
+        sel = (chrom >= base[i]) & (chrom < base[i] + q.nchrom)
+        sub = recs[sel].copy()
+        sub["chrom"] -= base[i]
+        out.append(post.sims_process_window(sub, q, window_size, len(sub)))
+    return out
+
+
 def likelihood_scan(main_dir, output, popinfo_filename, pop1='p1', pop2='p2', pop1_size=5, pop2_size=5,
                     window_size=500000, bg_end=500000):
     """sims_scan.py:593-644: per generation, background = the concatenated VCF's SNPs with
     pos in [0, bg_end] (2D folded, 1D unfolded); every replicate VCF scanned in fixed windows.
-    The reference hard-codes the popmap path and sizes; here they are arguments."""
+    The reference hard-codes the popmap path and sizes; here they are arguments.  The replicates of a
+    generation are parsed by the native VCF reader and scanned in one launch
+    (``process_windows_batch``); rows come out in the reference's order."""
+    from sfs2d.vcf import read_vcf
     generations = get_gens(main_dir)
     col_names = ['generation', 'iteration', 'region', 'window_coords', 'snp_count', 'T2D', 'T1D_p1', 'T1D_p2',
                  'new_term_p1', 'new_term_p2', 'T2D_diff']
@@ -163,18 +221,17 @@ def likelihood_scan(main_dir, output, popinfo_filename, pop1='p1', pop2='p2', po
             target_vcfs = glob.glob(f"{main_dir}/iter*/*{generation}*.vcf.gz")
             concatenated_vcfs = glob.glob(f"{main_dir}/concatenated_vcfs/gen.{generation}.concatenated.vcf.gz")
             for vcf in concatenated_vcfs:
-                data_dict = make_data_dict_vcf(vcf, popinfo_filename)
-                bg_2d_sfs = calculate_2d_sfs(data_dict, pop1, pop2, pop1_size, pop2_size, start_position=0,
+                bgp = read_vcf(vcf, popinfo_filename).to_packed(pop1, pop2)
+                bg_2d_sfs = calculate_2d_sfs(bgp, pop1, pop2, pop1_size, pop2_size, start_position=0,
                                              end_position=bg_end, variant_type=None)
-                bg_p1_sfs = calculate_1d_sfs(data_dict, pop1, pop1_size, start_position=0, end_position=bg_end,
+                bg_p1_sfs = calculate_1d_sfs(bgp, pop1, pop1_size, start_position=0, end_position=bg_end,
                                              variant_type=None)
-                bg_p2_sfs = calculate_1d_sfs(data_dict, pop2, pop2_size, start_position=0, end_position=bg_end,
+                bg_p2_sfs = calculate_1d_sfs(bgp, pop2, pop2_size, start_position=0, end_position=bg_end,
                                              variant_type=None)
-                for vcf_input in target_vcfs:
-                    data_dict_target = make_data_dict_vcf(vcf_input, popinfo_filename)
-                    results = process_window(data_dict_target, bg_2d_sfs, bg_p1_sfs, bg_p2_sfs, window_size, pop1,
-                                             pop2, pop1_size, pop2_size, start_position=None, end_position=None,
-                                             variant_type=None)
+                targets = [read_vcf(v, popinfo_filename).to_packed(pop1, pop2) for v in target_vcfs]
+                batch = process_windows_batch(targets, bg_2d_sfs, bg_p1_sfs, bg_p2_sfs, window_size, pop1, pop2,
+                                              pop1_size, pop2_size)
+                for vcf_input, results in zip(target_vcfs, batch):
                     iteration_number = int(vcf_input.split('.')[2])
                     for window_coords, result in results.items():
                         window_start, window_end = window_coords.split(' ')[1].split('-')
