@@ -119,6 +119,8 @@ struct sfs2d_plan {
   int nbg = 0;
   bool do_bg = false, do_seg = false, lds_hist = true, bg_ready = false;
   bool fused = false;       // per-chromosome tables built inside k_scan_w (parity-alternating replicas)
+  bool sliced = false;      // per-chromosome tables by k_bg_slice without its tail; k_scan_w combines
+                            // the leaf sums (parity-alternating inner sums)
   bool fst = false;         // SFS2D_F_FST: Fst per slot into d_fst
   double* d_fst = nullptr;
   unsigned long long* d_fsum = nullptr;   // k_prep's per-slot Fst sums (int64 fixed point), cleared by the scan
@@ -201,6 +203,9 @@ void plan_free(sfs2d_plan* p) {
     p->d_bins = nullptr;
     p->d_repl = nullptr;
     p->d_bcount = nullptr;
+    if (p->sliced) {
+      p->d_tab = nullptr; p->d_lp = nullptr; p->d_head = nullptr; p->d_leafsum = nullptr; p->d_bg1d = nullptr;
+    }
   }
   hipFree(p->d_slot_base);
   hipFree(p->d_tiles); hipFree(p->d_chunks); hipFree(p->d_slots); hipFree(p->d_repl); hipFree(p->d_bcount); hipFree(p->d_ctr);
@@ -212,7 +217,11 @@ void plan_free(sfs2d_plan* p) {
 }
 
 // replica parity of the current run (an attached plan reads its base's k_prep output)
-int plan_par(const sfs2d_plan* pl) { return pl->fused ? (int)((pl->base ? pl->base->runs : pl->runs) & 1) : 0; }
+int plan_par(const sfs2d_plan* pl) {
+  return (pl->fused || pl->sliced) ? (int)((pl->base ? pl->base->runs : pl->runs) & 1) : 0;
+}
+// replica parity: only fused plans alternate replicas (k_bg_slice clears what it reads)
+int repl_par(const sfs2d_plan* pl) { return pl->fused ? plan_par(pl) : 0; }
 
 template <bool P16, bool FUSED, bool FST>
 void launch_scan_w(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
@@ -221,7 +230,7 @@ void launch_scan_w(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
                      per_chrom, pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, bp, pl->d_repl, pl->d_bcount,
                      plan_par(pl), pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels,
                      pl->extra_rec >= 0 ? (int)pl->last_chrom : -1, pl->d_fsum, pl->d_fst, pl->d_ctr,
-                     (int)(pl->runs & 1));
+                     (int)(pl->runs & 1), pl->d_leafsum, pl->d_bg1d, pl->sliced ? 1 : 0);
 }
 
 template <bool P16, bool FST>
@@ -256,7 +265,7 @@ hipError_t launch_prep3(sfs2d_plan* pl) {
   const int par = plan_par(pl);
   hipExtLaunchKernelGGL((k_prep<B, S, L, N, F, FS>), dim3((unsigned)pl->tiles.size()), dim3(BLOCK1),
                      (B && L) ? pl->bg_lds : 0, pl->ctx->stream, pl->kev[0], pl->kev[1], 0, pl->K, d->counts, d->pos, d->ann, pl->d_tiles,
-                     pl->d_repl + (size_t)par * REPL * pl->K.nchrom * pl->K.nh, pl->d_slots, pl->d_bins,
+                     pl->d_repl + (size_t)repl_par(pl) * REPL * pl->K.nchrom * pl->K.nh, pl->d_slots, pl->d_bins,
                      pl->d_bcount + (size_t)par * pl->K.nchrom, pl->d_err, L ? pl->hr : 1,
                      reinterpret_cast<const double2*>(pl->ctx->d_df + 2 * LNT), pl->d_fsum);
   return hipGetLastError();
@@ -288,9 +297,9 @@ hipError_t launch_prep(sfs2d_plan* pl, bool bins) {
 // per-run per-chromosome backgrounds
 hipError_t launch_bg_slices(sfs2d_plan* pl) {
   hipLaunchKernelGGL(k_bg_slice, dim3((unsigned)pl->slices.size() + 1, (unsigned)pl->nbg), dim3(KBLOCK), 0,
-                     pl->ctx->stream, pl->K, pl->d_repl, pl->d_bcount, pl->d_tab, pl->d_lp, pl->d_head, pl->d_leafsum,
-                     pl->d_bg1d, pl->d_done, pl->d_slices, (int)pl->slices.size(), pl->d_leaves, pl->nleaves,
-                     pl->d_nodes, pl->nnodes);
+                     pl->ctx->stream, pl->K, pl->d_repl, pl->d_bcount + (size_t)plan_par(pl) * pl->K.nchrom, pl->d_tab,
+                     pl->d_lp, pl->d_head, pl->d_leafsum, pl->d_bg1d, pl->d_done, pl->d_slices, (int)pl->slices.size(),
+                     pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->sliced ? 0 : 1);
   return hipGetLastError();
 }
 
@@ -515,7 +524,16 @@ static int make_kparams(sfs2d_ctx* ctx, const sfs2d_params* prm, int nchrom, KPa
   return 0;
 }
 
+static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* prm, int force_sliced,
+                       sfs2d_plan** out);
+
 int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* prm, sfs2d_plan** out) {
+  return plan_create(ctx, data, prm, -1, out);
+}
+
+// force_sliced: -1 choose (windows per wave), 0 fused, 1 sliced (attached plans follow their base)
+static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* prm, int force_sliced,
+                       sfs2d_plan** out) {
   if (!ctx || !data || !prm || !out) return set_err(ctx, SFS2D_E_ARG, "null argument");
   *out = nullptr;
   HIPCHK(ctx, hipSetDevice(ctx->device));
@@ -596,7 +614,21 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
     delete pl;
     return set_err(ctx, SFS2D_E_ARG, "2D grid too large for LDS with 32-bit bins (windows of >= 65536 SNPs)");
   }
-  pl->fused = pl->do_bg && pl->G == WAVE;
+  // per-chromosome backgrounds on the small-grid path: k_bg_slice (many workgroups per background)
+  // then k_scan_w copies the table and combines the leaf sums in its prologue ("sliced"); the fused
+  // alternative (every scan workgroup sums the replicas and builds the table itself) is kept for
+  // comparison (SFS2D_FUSED=1): it is ~2x longer per workgroup
+  // for the small-grid path.  Which wins depends on windows per wavefront: with about one window
+  // each (1e6-SNP chromosome: 2.8k windows on 4k resident wavefronts) the table build IS the
+  // kernel's critical path and the sliced path is ~5% faster per run; with tens of windows each
+  // (config 3: 34) the fused prologue is amortised and its loop variant is faster.
+  // SFS2D_FUSED=0/1 forces one.
+  const bool small = pl->do_bg && pl->G == WAVE;
+  const double wpw = (double)pl->nslots / (2.0 * ctx->ncu * (SBLOCK / WAVE));   // windows per resident wave
+  pl->sliced = small && wpw < 4.0;
+  if (const char* ev = std::getenv("SFS2D_FUSED")) pl->sliced = small && ev[0] == '0';
+  if (force_sliced >= 0) pl->sliced = small && force_sliced == 1;
+  pl->fused = small && !pl->sliced;
   pl->fst = (prm->flags & SFS2D_F_FST) != 0;
   if (pl->scan_lds > 64 * 1024) {
     const int lds = (int)pl->scan_lds;
@@ -626,8 +658,14 @@ int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params
   // k_scan_g: two windows per workgroup.
   if (pl->G == WAVE) {
     int occ = 0;
-    const hipError_t oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<true, true, false>, SBLOCK, pl->scan_lds)
-                                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<false, true, false>, SBLOCK, pl->scan_lds);
+    // (the grid is one dispatch wave of resident workgroups: occupancy of the variant that runs)
+    hipError_t oe;
+    if (pl->fused)
+      oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<true, true, true>, SBLOCK, pl->scan_lds)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<false, true, true>, SBLOCK, pl->scan_lds);
+    else
+      oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<true, false, true>, SBLOCK, pl->scan_lds)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<false, false, true>, SBLOCK, pl->scan_lds);
     if (oe != hipSuccess || occ < 1) occ = 1;
     int64_t cap = (int64_t)occ * ctx->ncu;
     if (const char* ev = std::getenv("SFS2D_WGS")) cap = std::max<int64_t>(1, std::atoll(ev));   // tuning
@@ -905,7 +943,7 @@ int sfs2d_plan_run_many(sfs2d_plan* pl, int nruns, sfs2d_window* out_dev) {
 int sfs2d_plan_bg_buffer(sfs2d_plan* pl, void** dev_ptr, int64_t* nbytes) {
   if (!pl || !dev_ptr || !nbytes) return SFS2D_E_ARG;
   // the replica buffer the next run's k_prep accumulates into (fused plans alternate two)
-  *dev_ptr = pl->d_repl + (size_t)plan_par(pl) * REPL * pl->data->nchrom * pl->K.nh;
+  *dev_ptr = pl->d_repl + (size_t)repl_par(pl) * REPL * pl->data->nchrom * pl->K.nh;
   *nbytes = pl->do_bg ? (int64_t)REPL * pl->data->nchrom * pl->K.nh * 4 : 0;
   return 0;
 }
@@ -1038,7 +1076,7 @@ int sfs2d_plan_attach(sfs2d_plan* base, const sfs2d_params* prm, sfs2d_plan** ou
   sfs2d_ctx* ctx = base->ctx;
   *out = nullptr;
   if (base->base) return set_err(ctx, SFS2D_E_ARG, "attach to a base plan, not to an attached one");
-  if (!base->fused)
+  if (!base->fused && !base->sliced)
     return set_err(ctx, SFS2D_E_ARG, "attached plans need a per-chromosome-background base plan on the small-grid path");
   const sfs2d_params& b = base->prm;
   if (prm->n1p != b.n1p || prm->n2p != b.n2p || (prm->fold != 0) != (b.fold != 0) || prm->bg_mode != b.bg_mode ||
@@ -1054,9 +1092,9 @@ int sfs2d_plan_attach(sfs2d_plan* base, const sfs2d_params* prm, sfs2d_plan** ou
     m = (uint32_t)(prm->window / b.window);
   }
   sfs2d_plan* a = nullptr;
-  int rc = sfs2d_plan_create(ctx, base->data, prm, &a);
+  int rc = plan_create(ctx, base->data, prm, base->sliced ? 1 : 0, &a);
   if (rc) return rc;
-  if (!a->fused || a->G != base->G) {
+  if (a->fused != base->fused || a->sliced != base->sliced || a->G != base->G) {
     plan_free(a); delete a;
     return set_err(ctx, SFS2D_E_ARG, "attached plan would take a different kernel path than its base");
   }
@@ -1065,6 +1103,14 @@ int sfs2d_plan_attach(sfs2d_plan* base, const sfs2d_params* prm, sfs2d_plan** ou
   a->d_bins = base->d_bins;
   a->d_repl = base->d_repl;
   a->d_bcount = base->d_bcount;
+  if (base->sliced) {   // the base's k_bg_slice tables (the attached scans combine the same leaf sums)
+    hipFree(a->d_tab); hipFree(a->d_lp); hipFree(a->d_head); hipFree(a->d_leafsum); hipFree(a->d_bg1d);
+    a->d_tab = base->d_tab;
+    a->d_lp = base->d_lp;
+    a->d_head = base->d_head;
+    a->d_leafsum = base->d_leafsum;
+    a->d_bg1d = base->d_bg1d;
+  }
   a->base = base;
   a->fst_m = m;
   rc = 0;

@@ -801,7 +801,9 @@ __global__ __launch_bounds__(KBLOCK) void k_bg_slice(KParams P, uint32_t* __rest
                                                      double* __restrict__ leafsum, Bg1D* __restrict__ bg1d,
                                                      uint32_t* __restrict__ done, const int4* __restrict__ slices,
                                                      int nslices, const int2* __restrict__ leaves, int nleaves,
-                                                     const int4* __restrict__ nodes, int nnodes) {
+                                                     const int4* __restrict__ nodes, int nnodes, int tail) {
+  // tail == 0: no last-block combination -- the scan kernel combines the leaf sums itself (its
+  // prologue), and bcount is a per-run parity buffer cleared by the scan kernel
   __shared__ double pv[4 * 128 + 8];
   __shared__ double acc8[KBLOCK];
   __shared__ uint32_t u1[2 * 256 + 2];
@@ -913,6 +915,7 @@ __global__ __launch_bounds__(KBLOCK) void k_bg_slice(KParams P, uint32_t* __rest
     }
   }
 
+  if (!tail) return;
   // completion: the last block of this background combines (threadfence-reduction pattern)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   __syncthreads();
@@ -1101,6 +1104,15 @@ struct TabGlobal {   // the PL table written by k_bg_slice / k_bg_finalize
   __device__ __forceinline__ PL at(int k) const { return T[k]; }
 };
 
+struct TabLocal {    // k_bg_slice's table with the log proportions from LDS (the workgroup's own p[-1] rule)
+  const PL* T;
+  const double* LPl;
+  __device__ __forceinline__ PL at(int k) const {
+    PL e = T[k];
+    e.lp = LPl[k];
+    return e;
+  }
+};
 struct TabFused {    // k_scan_w's own table: lp in LDS, counts summed from this run's replicas
   const double* LPl;
   const uint32_t* R;   // this chromosome's replica 0; replica r at R + r * rs
@@ -1439,7 +1451,7 @@ __device__ __forceinline__ void fused_table(int nb2, int nh, int nt, int n1p, in
 // SNP adds D(r) - lp_k; the 1D atomics land in lane-&3 replicas; then one lane per 1D bin adds
 // x ln x - x lp; the touched 2D words are cleared; DPP sums; one record.
 template <bool P16, bool FUSED, bool FST>
-__global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 4 : 1))) void k_scan_w(KParams P, const uint32_t* __restrict__ bins,
+__global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_scan_w(KParams P, const uint32_t* __restrict__ bins,
                                                    const Chunk* __restrict__ chunks, uint2* __restrict__ slots,
                                                    PL* __restrict__ tab, double* __restrict__ LPg,
                                                    BgHead* __restrict__ head, int bg_per_chrom,
@@ -1451,7 +1463,8 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
                                                    const int4* __restrict__ nodes, int nnodes, int nlevels,
                                                    int write_chrom, unsigned long long* __restrict__ fsum,
                                                    double* __restrict__ fst_out, uint32_t* __restrict__ ctr,
-                                                   int cpar) {
+                                                   int cpar, const double* __restrict__ leafsum,
+                                                   const Bg1D* __restrict__ bg1d, int sliced) {
   extern __shared__ double ldsd[];
   __shared__ BgHead sh_hb;
   STAMP(10);
@@ -1513,7 +1526,49 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
   if (!FUSED) {
     const double* LP = LPg + (size_t)bg * P.nt;
     for (int k = tid; k < P.nt; k += SBLOCK) LPl[k] = LP[k];
-    hb = head[bg];
+    if (sliced) {
+      // this run's per-chromosome table from k_bg_slice (proportions, logs, 1D part final) and its
+      // leaf sums: numpy's tree over the leaves, then scipy's p[-1] rule on the 2D table -- the
+      // combination k_bg_slice's last block would do, here in every workgroup (no grid-wide
+      // completion step between the kernels).  Scratch: the histogram area (zeroed below).
+      const bool writer = ch.first == 0 && (int)ch.chrom == write_chrom;
+      double* lsum = reinterpret_cast<double*>(HB);
+      if (tid < nleaves) lsum[tid] = leafsum[(size_t)bg * nleaves + tid];
+      const int4 my_node = tid < nnodes ? nodes[tid] : make_int4(0, 0, -1, 0);
+      __syncthreads();
+      for (int l = 0; l < nlevels; ++l) {
+        if (my_node.z == l) lsum[nleaves + tid] = lsum[my_node.x] + lsum[my_node.y];
+        __syncthreads();
+      }
+      if (tid == 0) {
+        const double B2 = (double)bcount[(size_t)par * P.nchrom + bg];
+        const Bg1D o = bg1d[bg];
+        uint32_t flags = o.flags;
+        if (B2 == 0.0) flags |= BGF_B2_ZERO;
+        const int M2 = P.nb2 - 2;
+        if (M2 >= 1 && B2 != 0.0) {
+          const double S = (nleaves + nnodes) ? lsum[nleaves + nnodes - 1] : 0.0;
+          const double padj = 1.0 - S;
+          if (padj < -1e-15) {
+            flags |= BGF_NAN2;
+          } else if (fabs(padj) > 1e-15) {
+            const double l2 = log(padj);
+            LPl[M2] = l2;
+            if (writer) { tab[(size_t)bg * P.nt + M2].lp = l2; LPg[(size_t)bg * P.nt + M2] = l2; }
+          }
+        }
+        BgHead h;
+        h.B2 = B2; h.B1a = o.B1a; h.B1b = o.B1b; h.flags = flags; h.pad = 0;
+        sh_hb = h;
+        if (writer) head[bg] = h;
+      }
+      if (blockIdx.x == 0)   // the other parity's inner sums, for the next run
+        for (int c = tid; c < P.nchrom; c += SBLOCK) bcount[(size_t)(1 - par) * P.nchrom + c] = 0u;
+      __syncthreads();
+      hb = sh_hb;
+    } else {
+      hb = head[bg];
+    }
   } else {
     fused_table(P.nb2, P.nh, P.nt, P.n1p, P.n2p, P.n1, P.n2, P.t1a, P.t1b, P.nchrom, ch.chrom,
                 ch.first == 0 && (int)ch.chrom == write_chrom, bg,
@@ -1715,8 +1770,8 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(FUSED ? 
                                       TabFused{LPl, Rc, rs, P.nb2, P.n1, P.n2, P.n1p, P.h1a, P.h1b, P.t1a, P.t1b}, hb,
                                       lnx, W, H1a, H1b, nullptr, nullptr);
       else
-        w = eval_exact<WAVE, P16, R1>(P, bins, cur.b, cur.e, TabGlobal{tab + (size_t)bg * P.nt}, hb, lnx, W, H1a,
-                                      H1b, nullptr, nullptr);
+        w = eval_exact<WAVE, P16, R1>(P, bins, cur.b, cur.e, TabLocal{tab + (size_t)bg * P.nt, LPl}, hb, lnx, W,
+                                      H1a, H1b, nullptr, nullptr);
       if (lane == 0) atomicAdd(err_word + 1, 1u);   // statistics: windows that took the exact path
     } else {
       if (nan2) w.t2d = __builtin_nan("");
