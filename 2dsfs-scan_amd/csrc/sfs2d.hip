@@ -158,14 +158,14 @@ struct sfs2d_plan {
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   // live timing ring: events around each kernel of every run while timing is on
   bool timing = false;
-  std::vector<hipEvent_t> tev;   // 4 per sampled run
+  std::vector<hipEvent_t> tev;   // 6 per sampled run (start / end of k_prep, k_bg_slice, the scan)
   int tcount = 0;
   int tevery = 1;                // sample every tevery-th run
   int64_t tseen = 0;             // runs since timing was set
   // events of the run being enqueued: k_prep start/stop, scan start/stop (null: not sampled).  They
   // go into the kernels' own dispatch packets (hipExtLaunchKernelGGL), so they stamp the kernel's
   // start and end as the command processor sees them -- the durations rocprofv3 reports.
-  hipEvent_t kev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t kev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   // multi-resolution (sfs2d_plan_attach): an attached plan shares its base's k_prep pass (bins,
   // background replicas, inner sums); the base's run scans every attached plan before its own
   std::vector<unsigned long long> slot_base_h;   // window slots per chromosome (prefix sums)
@@ -226,7 +226,7 @@ int repl_par(const sfs2d_plan* pl) { return pl->fused ? plan_par(pl) : 0; }
 template <bool P16, bool FUSED, bool FST>
 void launch_scan_w(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
   hipExtLaunchKernelGGL((k_scan_w<P16, FUSED, FST>), dim3((unsigned)pl->chunks.size()), dim3(SBLOCK), pl->scan_lds,
-                     pl->ctx->stream, pl->kev[2], pl->kev[3], 0, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
+                     pl->ctx->stream, pl->kev[4], pl->kev[5], 0, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
                      per_chrom, pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, bp, pl->d_repl, pl->d_bcount,
                      plan_par(pl), pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels,
                      pl->extra_rec >= 0 ? (int)pl->last_chrom : -1, pl->d_fsum, pl->d_fst, pl->d_ctr,
@@ -236,7 +236,7 @@ void launch_scan_w(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
 template <bool P16, bool FST>
 void launch_scan_g(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
   hipExtLaunchKernelGGL((k_scan_g<P16, FST>), dim3((unsigned)pl->chunks.size()), dim3(BLOCK), pl->scan_lds,
-                     pl->ctx->stream, pl->kev[2], pl->kev[3], 0, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_head, per_chrom,
+                     pl->ctx->stream, pl->kev[4], pl->kev[5], 0, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_head, per_chrom,
                      pl->ctx->d_lnx, out, bp, pl->d_fsum, pl->d_fst);
 }
 
@@ -296,8 +296,8 @@ hipError_t launch_prep(sfs2d_plan* pl, bool bins) {
 
 // per-run per-chromosome backgrounds
 hipError_t launch_bg_slices(sfs2d_plan* pl) {
-  hipLaunchKernelGGL(k_bg_slice, dim3((unsigned)pl->slices.size() + 1, (unsigned)pl->nbg), dim3(KBLOCK), 0,
-                     pl->ctx->stream, pl->K, pl->d_repl, pl->d_bcount + (size_t)plan_par(pl) * pl->K.nchrom, pl->d_tab,
+  hipExtLaunchKernelGGL(k_bg_slice, dim3((unsigned)pl->slices.size() + 1, (unsigned)pl->nbg), dim3(KBLOCK), 0,
+                     pl->ctx->stream, pl->kev[2], pl->kev[3], 0, pl->K, pl->d_repl, pl->d_bcount + (size_t)plan_par(pl) * pl->K.nchrom, pl->d_tab,
                      pl->d_lp, pl->d_head, pl->d_leafsum, pl->d_bg1d, pl->d_done, pl->d_slices, (int)pl->slices.size(),
                      pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->sliced ? 0 : 1);
   return hipGetLastError();
@@ -847,40 +847,40 @@ int sfs2d_plan_run_phase(sfs2d_plan* pl, int phase, sfs2d_window* out_dev) {
   if (pl->base) return set_err(ctx, SFS2D_E_ARG, "an attached plan runs with its base plan (sfs2d_plan_attach)");
   HIPCHK(ctx, hipSetDevice(ctx->device));
   hipEvent_t* te = nullptr;
-  if (pl->timing && phase == 0 && (pl->tseen++ % pl->tevery) == 0 && pl->tcount * 4 < (int)pl->tev.size())
-    te = &pl->tev[(size_t)pl->tcount * 4];
+  if (pl->timing && phase == 0 && (pl->tseen++ % pl->tevery) == 0 && pl->tcount * 6 < (int)pl->tev.size())
+    te = &pl->tev[(size_t)pl->tcount * 6];
   if (!pl->do_bg && !pl->bg_ready && phase != 1)
     return set_err(ctx, SFS2D_E_ARG, "supplied-background plan run before sfs2d_plan_set_background");
-  // sampled runs: k_prep and the scan kernel carry the run's four events in their dispatch packets
-  // (kernel start / end); a phase that does not launch its kernel records the event in the stream
-  for (int k = 0; k < 4; ++k) pl->kev[k] = te ? te[k] : nullptr;
+  // sampled runs: each kernel carries its start / end events in its own dispatch packet; a kernel
+  // this run does not launch gets both events recorded in the stream instead (duration ~0)
+  for (int k = 0; k < 6; ++k) pl->kev[k] = te ? te[k] : nullptr;
+  auto mark = [&](int k) -> int {
+    if (te) {
+      HIPCHK(ctx, hipEventRecord(te[k], ctx->stream));
+      HIPCHK(ctx, hipEventRecord(te[k + 1], ctx->stream));
+    }
+    return 0;
+  };
+  int rc = 0;
   if (phase == 0 || phase == 1) {
     HIPCHK(ctx, launch_prep(pl, true));
-    if (te && pl->tiles.empty()) {
-      HIPCHK(ctx, hipEventRecord(te[0], ctx->stream));
-      HIPCHK(ctx, hipEventRecord(te[1], ctx->stream));
-    }
-  } else if (te) {
-    HIPCHK(ctx, hipEventRecord(te[0], ctx->stream));
-    HIPCHK(ctx, hipEventRecord(te[1], ctx->stream));
+    if (pl->tiles.empty() && (rc = mark(0))) return rc;
+  } else if ((rc = mark(0))) {
+    return rc;
   }
-  pl->kev[0] = pl->kev[1] = nullptr;
   if (phase == 0 || phase == 2) {
     if (pl->do_bg && !pl->fused) HIPCHK(ctx, launch_bg_slices(pl));
+    else if ((rc = mark(2))) return rc;
     for (sfs2d_plan* a : pl->attached) HIPCHK(ctx, launch_attached(a));   // before the base clears its state
     sfs2d_window* out = out_dev ? out_dev : pl->d_out;
-    if (te && pl->chunks.empty()) {
-      HIPCHK(ctx, hipEventRecord(te[2], ctx->stream));
-      HIPCHK(ctx, hipEventRecord(te[3], ctx->stream));
-    }
+    if (pl->chunks.empty() && (rc = mark(4))) return rc;
     HIPCHK(ctx, launch_scan_any(pl, out));
     pl->last_out = out;
     pl->runs++;
-  } else if (te) {
-    HIPCHK(ctx, hipEventRecord(te[2], ctx->stream));
-    HIPCHK(ctx, hipEventRecord(te[3], ctx->stream));
+  } else if ((rc = mark(2)) || (rc = mark(4))) {
+    return rc;
   }
-  pl->kev[2] = pl->kev[3] = nullptr;
+  for (auto& e : pl->kev) e = nullptr;
   if (te) pl->tcount++;
   return 0;
 }
@@ -901,7 +901,7 @@ int sfs2d_plan_set_timing_sampled(sfs2d_plan* pl, int max_runs, int every) {
   sfs2d_ctx* ctx = pl->ctx;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   for (auto& e : pl->tev) if (e) hipEventDestroy(e);
-  pl->tev.assign((size_t)max_runs * 4, nullptr);
+  pl->tev.assign((size_t)max_runs * 6, nullptr);
   for (auto& e : pl->tev) HIPCHK(ctx, hipEventCreate(&e));
   pl->tcount = 0;
   pl->timing = max_runs > 0;
@@ -913,11 +913,11 @@ int sfs2d_plan_timing_read(sfs2d_plan* pl, int* nruns, double* ms_k1, double* ms
   sfs2d_ctx* ctx = pl->ctx;
   double t[3] = {0, 0, 0};
   for (int r = 0; r < pl->tcount; ++r) {
-    hipEvent_t* te = &pl->tev[(size_t)r * 4];
-    HIPCHK(ctx, hipEventSynchronize(te[3]));
+    hipEvent_t* te = &pl->tev[(size_t)r * 6];
+    HIPCHK(ctx, hipEventSynchronize(te[5]));
     for (int k = 0; k < 3; ++k) {
       float ms = 0;
-      HIPCHK(ctx, hipEventElapsedTime(&ms, te[k], te[k + 1]));
+      HIPCHK(ctx, hipEventElapsedTime(&ms, te[2 * k], te[2 * k + 1]));
       t[k] += ms;
     }
   }
