@@ -173,6 +173,8 @@ struct sfs2d_plan {
   sfs2d_plan* base = nullptr;
   std::vector<sfs2d_plan*> attached;
   uint32_t fst_m = 0;             // attached Fst: base windows per window (their sums add)
+  bool fst_win = false;           // Fst by window kernels (fst_windows) instead of k_prep's sums
+  int nfst = 0;                   // k_bg_slice's extra Fst workgroups
 };
 
 namespace {
@@ -246,10 +248,10 @@ hipError_t launch_scan(sfs2d_plan* pl, sfs2d_window* out) {
   const int bp = pl->prm.window_mode == SFS2D_WINDOW_BP ? 1 : 0;
   if (pl->G == WAVE) {
     if (pl->fused) {
-      if (pl->fst) launch_scan_w<P16, true, true>(pl, out, per_chrom, bp);
+      if (pl->fst && !pl->fst_win) launch_scan_w<P16, true, true>(pl, out, per_chrom, bp);
       else launch_scan_w<P16, true, false>(pl, out, per_chrom, bp);
     } else {
-      if (pl->fst) launch_scan_w<P16, false, true>(pl, out, per_chrom, bp);
+      if (pl->fst && !pl->fst_win) launch_scan_w<P16, false, true>(pl, out, per_chrom, bp);
       else launch_scan_w<P16, false, false>(pl, out, per_chrom, bp);
     }
   } else {
@@ -273,7 +275,7 @@ hipError_t launch_prep3(sfs2d_plan* pl) {
 
 template <bool B, bool S, bool L, bool N, bool F>
 hipError_t launch_prep2(sfs2d_plan* pl) {
-  if (N && pl->fst) return launch_prep3<B, S, L, N, F, N>(pl);   // Fst only with the bins pass
+  if (N && pl->fst && !pl->fst_win) return launch_prep3<B, S, L, N, F, N>(pl);   // Fst only with the bins pass
   return launch_prep3<B, S, L, N, F, false>(pl);
 }
 
@@ -296,10 +298,12 @@ hipError_t launch_prep(sfs2d_plan* pl, bool bins) {
 
 // per-run per-chromosome backgrounds
 hipError_t launch_bg_slices(sfs2d_plan* pl) {
-  hipExtLaunchKernelGGL(k_bg_slice, dim3((unsigned)pl->slices.size() + 1, (unsigned)pl->nbg), dim3(KBLOCK), 0,
+  hipExtLaunchKernelGGL(k_bg_slice, dim3((unsigned)pl->slices.size() + 1 + (unsigned)pl->nfst, (unsigned)pl->nbg), dim3(KBLOCK), 0,
                      pl->ctx->stream, pl->kev[2], pl->kev[3], 0, pl->K, pl->d_repl, pl->d_bcount + (size_t)plan_par(pl) * pl->K.nchrom, pl->d_tab,
                      pl->d_lp, pl->d_head, pl->d_leafsum, pl->d_bg1d, pl->d_done, pl->d_slices, (int)pl->slices.size(),
-                     pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->sliced ? 0 : 1);
+                     pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->sliced ? 0 : 1, pl->nfst,
+                     pl->data->counts, pl->d_bins, pl->d_slots, reinterpret_cast<const double2*>(pl->ctx->d_df + 2 * LNT),
+                     pl->d_fst, (uint32_t)pl->nslots);
   return hipGetLastError();
 }
 
@@ -340,6 +344,10 @@ hipError_t launch_attached(sfs2d_plan* a) {
   if (a->fst_m)
     hipLaunchKernelGGL(k_fst_agg, g, dim3(256), 0, a->ctx->stream, a->base->d_fsum, a->base->d_slot_base,
                        a->d_slot_base, d->nchrom, a->fst_m, ns, a->d_fsum);
+  if (a->fst_win)   // before the scan clears the slots
+    hipLaunchKernelGGL(k_fst_win, dim3((unsigned)std::min<uint32_t>(2048u, (ns + 3u) / 4u)), dim3(256), 0,
+                       a->ctx->stream, d->counts, a->d_bins, a->d_slots,
+                       reinterpret_cast<const double2*>(a->ctx->d_df + 2 * LNT), a->d_fst, ns);
   const hipError_t e = launch_scan_any(a, a->d_out);
   a->last_out = a->d_out;
   a->runs++;
@@ -629,6 +637,10 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   if (const char* ev = std::getenv("SFS2D_FUSED")) pl->sliced = small && ev[0] == '0';
   if (force_sliced >= 0) pl->sliced = small && force_sliced == 1;
   pl->fused = small && !pl->sliced;
+  // Fst of sliced fixed-bp plans: by extra k_bg_slice workgroups (the GPU is mostly idle during
+  // that latency-bound kernel) instead of k_prep's per-SNP sums (config 2: k_prep -3 us)
+  pl->fst_win = pl->sliced && bp && (prm->flags & SFS2D_F_FST);
+  pl->nfst = pl->fst_win ? (int)std::min<int64_t>(1024, std::max<int64_t>(1, (pl->nslots + 7) / 8)) : 0;   // ~1 window per wave
   pl->fst = (prm->flags & SFS2D_F_FST) != 0;
   if (pl->scan_lds > 64 * 1024) {
     const int lds = (int)pl->scan_lds;
@@ -1087,9 +1099,13 @@ int sfs2d_plan_attach(sfs2d_plan* base, const sfs2d_params* prm, sfs2d_plan** ou
   uint32_t m = 0;
   if (prm->flags & SFS2D_F_FST) {
     const bool base_bp = b.window_mode == SFS2D_WINDOW_BP;
-    if (!(b.flags & SFS2D_F_FST) || !base_bp || !bp || prm->window % b.window != 0)
-      return set_err(ctx, SFS2D_E_ARG, "attached Fst needs a fixed-bp Fst base plan whose window divides this one's");
-    m = (uint32_t)(prm->window / b.window);
+    if (!bp)
+      return set_err(ctx, SFS2D_E_ARG, "attached Fst needs fixed-bp windows");
+    if (!base->sliced) {   // fused bases: the base's k_prep sums, added per attached window
+      if (!(b.flags & SFS2D_F_FST) || !base_bp || prm->window % b.window != 0)
+        return set_err(ctx, SFS2D_E_ARG, "attached Fst needs a fixed-bp Fst base plan whose window divides this one's");
+      m = (uint32_t)(prm->window / b.window);
+    }
   }
   sfs2d_plan* a = nullptr;
   int rc = plan_create(ctx, base->data, prm, base->sliced ? 1 : 0, &a);
@@ -1113,6 +1129,8 @@ int sfs2d_plan_attach(sfs2d_plan* base, const sfs2d_params* prm, sfs2d_plan** ou
   }
   a->base = base;
   a->fst_m = m;
+  a->fst_win = base->sliced && (prm->flags & SFS2D_F_FST);   // k_fst_win on the attached slots
+  a->nfst = 0;
   rc = 0;
   std::vector<uint32_t> sb(a->slot_base_h.begin(), a->slot_base_h.end());
   rc = rc ? rc : dalloc(ctx, &a->d_slot_base, sb.size());

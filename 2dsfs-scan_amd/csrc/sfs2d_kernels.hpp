@@ -725,6 +725,55 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
   BLK_STAMP(0, 1);
 }
 
+
+// Fst per fixed-bp window, one wavefront per window (windows wave_id, wave_id + nwaves, ...): the
+// window's SNPs from its slot record (k_prep's segmentation), membership from the packed bins (in
+// the 2D SFS, the excluded last bin included), terms by fst_snp, fp64 lane sums in a fixed order and
+// one DPP reduction (deterministic).  Used instead of k_prep's per-SNP fixed-point sums where the
+// GPU has idle capacity: extra workgroups of k_bg_slice (sliced plans), or k_fst_win alone.
+__device__ __forceinline__ void fst_windows(const uint32_t* __restrict__ counts, const uint32_t* __restrict__ bins,
+                                            const uint2* __restrict__ slots, const double2* __restrict__ rt,
+                                            double* __restrict__ fst_out, uint32_t nslots, uint32_t wave_id,
+                                            uint32_t nwaves) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  for (uint32_t s = wave_id; s < nslots; s += nwaves) {
+    const uint2 sr = slots[s];
+    if (sr.x == 0u) {
+      if (lane == 0) fst_out[s] = __builtin_nan("");
+      continue;
+    }
+    const uint32_t b = sr.x - 1u, e = sr.y;
+    double sn = 0.0, sd = 0.0;
+    // rows of 64 SNPs, eight rows' loads in flight at a time (a window is ~6 rows at 20 kb)
+    for (uint32_t r0 = b; r0 < e; r0 += 8 * WAVE) {
+      uint32_t c[8], w[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t i = r0 + 64 * j + lane;
+        c[j] = i < e ? counts[i] : 0u;
+        w[j] = i < e ? bins[i] : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        double nk, dk;
+        fst_snp(c[j], (bin_k2(w[j]) != 0u) | ((w[j] & B_LAST) != 0u), rt, nk, dk);
+        sn += nk;
+        sd += dk;
+      }
+    }
+    double tn, ta, tb;
+    wave_sum_dpp_halves(sn, sd, tn, ta, tb);
+    const double td = ta + tb;
+    if (lane == 0) fst_out[s] = td != 0.0 ? tn / td : __builtin_nan("");
+  }
+}
+
+__global__ __launch_bounds__(256) void k_fst_win(const uint32_t* __restrict__ counts, const uint32_t* __restrict__ bins,
+                                                 const uint2* __restrict__ slots, const double2* __restrict__ rt,
+                                                 double* __restrict__ fst_out, uint32_t nslots) {
+  fst_windows(counts, bins, slots, rt, fst_out, nslots, blockIdx.x * 4u + (threadIdx.x >> 6), gridDim.x * 4u);
+}
+
 // ------------------------------------------------------------------------------------------ K2
 
 // numpy pairwise_sum leaf (numpy/_core/src/umath/loops_utils.h.src): n < 8 sequential from 0.0,
@@ -801,7 +850,11 @@ __global__ __launch_bounds__(KBLOCK) void k_bg_slice(KParams P, uint32_t* __rest
                                                      double* __restrict__ leafsum, Bg1D* __restrict__ bg1d,
                                                      uint32_t* __restrict__ done, const int4* __restrict__ slices,
                                                      int nslices, const int2* __restrict__ leaves, int nleaves,
-                                                     const int4* __restrict__ nodes, int nnodes, int tail) {
+                                                     const int4* __restrict__ nodes, int nnodes, int tail,
+                                                     int nfst, const uint32_t* __restrict__ counts,
+                                                     const uint32_t* __restrict__ bins, const uint2* __restrict__ slots,
+                                                     const double2* __restrict__ rt, double* __restrict__ fst_out,
+                                                     uint32_t nslots) {
   // tail == 0: no last-block combination -- the scan kernel combines the leaf sums itself (its
   // prologue), and bcount is a per-run parity buffer cleared by the scan kernel
   __shared__ double pv[4 * 128 + 8];
@@ -813,6 +866,12 @@ __global__ __launch_bounds__(KBLOCK) void k_bg_slice(KParams P, uint32_t* __rest
   const int s = blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & (WAVE - 1);
+  if (s > nslices) {   // the extra workgroups (background 0's row only): Fst per window, using the
+                       // GPU while this kernel's table blocks wait on memory
+    if (b == 0) fst_windows(counts, bins, slots, rt, fst_out, nslots, (uint32_t)(s - nslices - 1) * (KBLOCK / WAVE) + (tid >> 6),
+                            (uint32_t)nfst * (KBLOCK / WAVE));
+    return;
+  }
   const size_t rstride = (size_t)P.nchrom * P.nh;
   uint32_t* R = repl + (size_t)b * P.nh;
   PL* T = tab + (size_t)b * P.nt;

@@ -205,7 +205,7 @@ class LikelihoodInference_jointSFS:
 
         def cfg_of(kind, w):
             bp = kind == "bp"
-            want_fst = fst and bp and base_ws is not None and w % base_ws == 0
+            want_fst = fst and bp and base_ws is not None   # (the library refuses what it cannot attach)
             return self._cfg(p, window_mode=L.WINDOW_BP if bp else L.WINDOW_SNPS, window=w,
                              bg_mode=L.BG_PER_CHROM, prev_extra=bp, fst=want_fst)
         eng = self._engine()
@@ -214,7 +214,16 @@ class LikelihoodInference_jointSFS:
         try:
             base = eng.plan(dev, cfg_of(*specs[0]))
             try:
-                plans = [base] + [base.attach(cfg_of(*sp)) for sp in specs[1:]]
+                plans = [base]
+                for sp in specs[1:]:
+                    c = cfg_of(*sp)
+                    try:
+                        plans.append(base.attach(c))
+                    except L.Sfs2dError:
+                        if not c.fst:
+                            raise
+                        c.fst = False   # Fst for this window size from its own plan below
+                        plans.append(base.attach(c))
                 base.run()
                 base.check()
                 for (kind, w), pl in zip(specs, plans):

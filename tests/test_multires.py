@@ -40,8 +40,8 @@ def test_matches_single_plans(seed):
     from sfs2d.synth import synth_genome
     p = synth_genome(3, [40000, 25000, 9000], 25, 25, seed=seed)
     obj = _obj(25, 25)
-    res = obj.multi_scan(p, [20000, 100000, 60000, 500000], [500, 300], fst=True)
-    for ws in (20000, 60000, 100000, 500000):
+    res = obj.multi_scan(p, [20000, 100000, 60000, 30000, 500000], [500, 300], fst=True)
+    for ws in (20000, 30000, 60000, 100000, 500000):
         _same(res[ws], obj.combined_scan(p, ws))
         single = obj.window_fst(p, window_size=ws)
         assert list(res["fst"][ws]) == list(single)
@@ -71,8 +71,8 @@ def test_repeated_runs_identical():
             base.check()
             outs.append([pl.read().tobytes() for pl in (base, a1, a2)] + [a1.read_fst().tobytes()])
         assert outs[0] == outs[1] == outs[2]
-        with pytest.raises(Exception):   # Fst on a window the base's does not divide
-            base.attach(ScanConfig(n1p=25, n2p=25, window=30000, fst=True))
+        with pytest.raises(Exception):   # Fst on SNP-count windows
+            base.attach(ScanConfig(n1p=25, n2p=25, window_mode=L.WINDOW_SNPS, window=300, fst=True))
         with pytest.raises(Exception):   # a different grid
             base.attach(ScanConfig(n1p=20, n2p=25, window=500000))
         base.close()
