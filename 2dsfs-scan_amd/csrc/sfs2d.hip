@@ -499,6 +499,77 @@ int sfs2d_data_wrap_device(sfs2d_ctx* ctx, const uint32_t* d_counts, const uint3
   return 0;
 }
 
+int sfs2d_data_synth_sims(sfs2d_ctx* ctx, const sfs2d_synth_params* sp, const uint16_t* win_snps,
+                          const uint32_t* miss_cdf1, int32_t nm1, const uint32_t* miss_cdf2, int32_t nm2,
+                          sfs2d_data** out) {
+  if (!ctx || !sp || !out || !miss_cdf1 || !miss_cdf2 || nm1 < 1 || nm2 < 1 ||
+      (sp->n_replicates && sp->n_windows && !win_snps))
+    return set_err(ctx, SFS2D_E_ARG, "null argument");
+  if (sp->n1p < 1 || sp->n2p < 1 || 2 * sp->n1p > 255 || 2 * sp->n2p > 255 || sp->window_bp < 1 ||
+      (unsigned long long)sp->n_windows * sp->window_bp > 0xffffffffull)
+    return set_err(ctx, SFS2D_E_ARG, "bad synthetic parameters");
+  *out = nullptr;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const uint64_t nw = (uint64_t)sp->n_replicates * sp->n_windows;
+  std::vector<unsigned long long> woff(nw + 1, 0);
+  std::vector<int64_t> coff(sp->n_replicates + 1, 0);
+  for (uint64_t w = 0; w < nw; ++w) {
+    if (win_snps[w] > sp->window_bp) return set_err(ctx, SFS2D_E_ARG, "more SNPs than bp in a window");
+    woff[w + 1] = woff[w] + win_snps[w];
+  }
+  for (uint32_t r = 0; r < sp->n_replicates; ++r) coff[r + 1] = (int64_t)woff[(uint64_t)(r + 1) * sp->n_windows];
+  const int64_t n = (int64_t)woff[nw];
+  sfs2d_data* d = new sfs2d_data();
+  d->ctx = ctx;
+  d->owned = true;
+  int rc = data_meta(ctx, d, coff.data(), (int32_t)sp->n_replicates, n);
+  if (rc) { hipFree(d->d_chrom_off); delete d; return rc; }
+  const size_t np = ((size_t)n + 3) / 4 * 4 + 64;   // readable to round_up(n, 4) (+ k_scan_w overhang)
+  unsigned long long* d_woff = nullptr;
+  uint32_t* d_mt = nullptr;
+  if (dalloc(ctx, &d->counts, np) || dalloc(ctx, &d->pos, np) || dalloc(ctx, &d->ann, np) ||
+      dalloc(ctx, &d_woff, nw + 1) || dalloc(ctx, &d_mt, (size_t)nm1 + nm2)) {
+    hipFree(d->counts); hipFree(d->pos); hipFree(d->ann); hipFree(d_woff); hipFree(d->d_chrom_off); delete d;
+    return SFS2D_E_NOMEM;
+  }
+  hipError_t e = hipMemsetAsync(d->ann, 0, sizeof(uint16_t) * np, ctx->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(d->counts, 0, sizeof(uint32_t) * np, ctx->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(d->pos, 0, sizeof(uint32_t) * np, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_woff, woff.data(), sizeof(unsigned long long) * (nw + 1), hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_mt, miss_cdf1, sizeof(uint32_t) * nm1, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_mt + nm1, miss_cdf2, sizeof(uint32_t) * nm2, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess && nw) {
+    SynthP S;
+    S.seed = sp->seed; S.gen = sp->generation; S.nwin = sp->n_windows; S.ws = sp->window_bp;
+    S.n1 = 2u * (uint32_t)sp->n1p; S.n2 = 2u * (uint32_t)sp->n2p; S.nm1 = (uint32_t)nm1; S.nm2 = (uint32_t)nm2;
+    const unsigned grid = (unsigned)std::min<uint64_t>(16384, (nw + 3) / 4);
+    hipLaunchKernelGGL(k_synth_sims, dim3(grid), dim3(256), 0, ctx->stream, S, d_woff, (unsigned long long)nw,
+                       d_mt, d_mt + nm1, d->counts, d->pos);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  hipFree(d_woff);
+  hipFree(d_mt);
+  if (e != hipSuccess) {
+    hipFree(d->counts); hipFree(d->pos); hipFree(d->ann); hipFree(d->d_chrom_off); delete d;
+    return set_err(ctx, SFS2D_E_HIP, std::string("synthetic data: ") + hipGetErrorString(e));
+  }
+  d->last_pos.assign(sp->n_replicates, sp->n_windows * sp->window_bp);   // upper bound: trailing slots stay empty
+  d->strict = true;
+  *out = d;
+  return 0;
+}
+
+int sfs2d_data_read(const sfs2d_data* d, uint32_t* counts, uint32_t* pos, int64_t n) {
+  if (!d || n != d->n) return SFS2D_E_ARG;
+  sfs2d_ctx* ctx = d->ctx;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  if (counts && n) HIPCHK(ctx, hipMemcpy(counts, d->counts, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost));
+  if (pos && n) HIPCHK(ctx, hipMemcpy(pos, d->pos, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost));
+  return 0;
+}
+
 int sfs2d_data_free(sfs2d_data* d) {
   if (!d) return SFS2D_E_ARG;
   hipSetDevice(d->ctx->device);

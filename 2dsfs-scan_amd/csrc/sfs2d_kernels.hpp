@@ -1958,7 +1958,6 @@ __global__ __launch_bounds__(WAVE) void k_scan_extra(KParams P, const uint32_t* 
   if (threadIdx.x == 0) write_rec(out + extra_rec, pc, bl, pb, pe, w, flags);
 }
 
-}  // namespace sfs2dk
 
 // ------------------------------------------------------------------------------------------ multi-resolution
 
@@ -2020,3 +2019,82 @@ __global__ __launch_bounds__(256) void k_fst_agg(const unsigned long long* __res
   fsum[2 * (size_t)s] = qn;
   fsum[2 * (size_t)s + 1] = qd;
 }
+
+// ------------------------------------------------------------------------------------------ synthetic sims data
+
+// BASELINE config 4 (sims_scan.likelihood_scan at scale: thousands of replicates x 2,000 windows,
+// Poisson(358.5) SNPs per window) generated in HBM instead of parsed from VCFs.  Counter-based
+// Philox4x32-10 keyed by (seed) with counter (global SNP index, call, generation): every SNP's draws
+// are independent of launch geometry, and the host twin (sfs2d.synth.sims_host) reproduces them bit
+// for bit -- only correctly rounded IEEE operations (mul, add, div, sqrt, floor; no contraction:
+// the _rn intrinsics) and integer table look-ups.
+//   position: window w, SNP j of k_w: w*ws + 1 + floor((j + u) * ws / k_w)  (strictly increasing)
+//   ancestral f: u^3 or 1 - u^3 (a U-shaped spectrum); per population f_i = clip(f + 0.1 (u - 1/2))
+//   missing alleles: Binomial(2 n_i, miss) by inverse-CDF table (u32 thresholds from the host)
+//   alt_i ~ normal approximation of Binomial(m_i, f_i): floor(m f + sqrt(m f (1-f)) z + 1/2) clipped
+//   to [0, m], z = (sum of 4 uniforms - 2) * sqrt(3); ref_i = m_i - alt_i
+struct SynthP {
+  unsigned long long seed;
+  uint32_t gen, nwin, ws, n1, n2, nm1, nm2;   // n1 / n2 = 2 * pop size; nm = miss-table length
+};
+
+__device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const unsigned long long p0 = (unsigned long long)0xD2511F53u * c.x, p1 = (unsigned long long)0xCD9E8D57u * c.z;
+    const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0, h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
+    c = make_uint4(h1 ^ c.y ^ k.x, l1, h0 ^ c.w ^ k.y, l0);
+    k.x += 0x9E3779B9u;
+    k.y += 0xBB67AE85u;
+  }
+  return c;
+}
+
+__device__ __forceinline__ double u01(uint32_t x) { return __dmul_rn(__dadd_rn((double)x, 0.5), 2.3283064365386963e-10); }
+
+__device__ __forceinline__ uint32_t synth_alt(double f, uint32_t m, uint4 z4) {
+  const double z = __dmul_rn(__dadd_rn(__dadd_rn(__dadd_rn(u01(z4.x), u01(z4.y)), __dadd_rn(u01(z4.z), u01(z4.w))), -2.0),
+                             1.7320508075688772);
+  const double mf = __dmul_rn((double)m, f);
+  const double sd = __dsqrt_rn(__dmul_rn(mf, __dadd_rn(1.0, -f)));
+  const double x = floor(__dadd_rn(__dadd_rn(mf, __dmul_rn(sd, z)), 0.5));
+  return x <= 0.0 ? 0u : (x >= (double)m ? m : (uint32_t)x);
+}
+
+__device__ __forceinline__ uint32_t synth_miss(const uint32_t* __restrict__ tab, uint32_t nt, uint32_t x) {
+  uint32_t k = 0;   // smallest k with x < tab[k] (tab: cumulative thresholds, last = 0xffffffff)
+  while (k + 1 < nt && x >= tab[k]) ++k;
+  return k;
+}
+
+__global__ __launch_bounds__(256) void k_synth_sims(SynthP S, const unsigned long long* __restrict__ woff,
+                                                    unsigned long long nwtot, const uint32_t* __restrict__ mt1,
+                                                    const uint32_t* __restrict__ mt2, uint32_t* __restrict__ counts,
+                                                    uint32_t* __restrict__ pos) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  const unsigned long long nwaves = (unsigned long long)gridDim.x * 4u;
+  const uint2 key = make_uint2((uint32_t)S.seed, (uint32_t)(S.seed >> 32));
+  for (unsigned long long w = blockIdx.x * 4ull + (threadIdx.x >> 6); w < nwtot; w += nwaves) {
+    const unsigned long long o = woff[w], k = woff[w + 1] - o;
+    const uint32_t wl = (uint32_t)(w % S.nwin);
+    for (unsigned long long j = lane; j < k; j += WAVE) {
+      const unsigned long long g = o + j;
+      const uint4 a = philox4x32(make_uint4((uint32_t)g, (uint32_t)(g >> 32), 0u, S.gen), key);
+      const uint4 b = philox4x32(make_uint4((uint32_t)g, (uint32_t)(g >> 32), 1u, S.gen), key);
+      const uint4 z1 = philox4x32(make_uint4((uint32_t)g, (uint32_t)(g >> 32), 2u, S.gen), key);
+      const uint4 z2 = philox4x32(make_uint4((uint32_t)g, (uint32_t)(g >> 32), 3u, S.gen), key);
+      const double u = u01(a.x);
+      const double u3 = __dmul_rn(__dmul_rn(u, u), u);
+      const double f = (b.w & 1u) ? u3 : __dadd_rn(1.0, -u3);
+      const double f1 = fmin(1.0, fmax(0.0, __dadd_rn(f, __dmul_rn(0.1, __dadd_rn(u01(a.z), -0.5)))));
+      const double f2 = fmin(1.0, fmax(0.0, __dadd_rn(f, __dmul_rn(0.1, __dadd_rn(u01(a.w), -0.5)))));
+      const uint32_t m1 = S.n1 - synth_miss(mt1, S.nm1, b.x), m2 = S.n2 - synth_miss(mt2, S.nm2, b.y);
+      const uint32_t a1 = synth_alt(f1, m1, z1), a2 = synth_alt(f2, m2, z2);
+      counts[g] = (m1 - a1) | (a1 << 8) | ((m2 - a2) << 16) | (a2 << 24);
+      const double t = __dmul_rn(__dadd_rn((double)j, u01(b.z)), (double)S.ws);
+      pos[g] = wl * S.ws + 1u + (uint32_t)floor(__ddiv_rn(t, (double)k));
+    }
+  }
+}
+
+}  // namespace sfs2dk

@@ -32,7 +32,8 @@ EXPORTS = [
     "sfs2d_plan_fst_read", "sfs2d_plan_fst_buffer", "sfs2d_plan_read",
     "sfs2d_plan_bg_buffer", "sfs2d_plan_run_phase", "sfs2d_plan_check", "sfs2d_plan_time",
     "sfs2d_plan_destroy", "sfs2d_scan", "sfs2d_plan_set_timing", "sfs2d_plan_timing_read",
-    "sfs2d_plan_stats", "sfs2d_plan_grids", "sfs2d_plan_attach",
+    "sfs2d_plan_stats", "sfs2d_plan_grids", "sfs2d_plan_attach", "sfs2d_data_synth_sims",
+    "sfs2d_data_read",
 ]
 
 
@@ -40,6 +41,11 @@ class Sfs2dError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"sfs2d error {code}: {msg}")
         self.code = code
+
+
+class SynthParams(C.Structure):   # sfs2d_synth_params
+    _fields_ = [("seed", C.c_uint64), ("generation", C.c_uint32), ("n_replicates", C.c_uint32),
+                ("n_windows", C.c_uint32), ("window_bp", C.c_uint32), ("n1p", C.c_int32), ("n2p", C.c_int32)]
 
 
 class Params(C.Structure):
@@ -99,6 +105,8 @@ def lib():
     L.sfs2d_plan_stats.argtypes = [vp, C.POINTER(C.c_uint32)]
     L.sfs2d_plan_grids.argtypes = [vp, C.POINTER(i64), C.POINTER(i64)]
     L.sfs2d_plan_attach.argtypes = [vp, C.POINTER(Params), C.POINTER(vp)]
+    L.sfs2d_data_synth_sims.argtypes = [vp, C.POINTER(SynthParams), vp, vp, i32, vp, i32, C.POINTER(vp)]
+    L.sfs2d_data_read.argtypes = [vp, vp, vp, i64]
     L.sfs2d_plan_timing_read.argtypes = [vp, C.POINTER(C.c_int)] + [C.POINTER(C.c_double)] * 3
     L.sfs2d_scan.argtypes = [vp, vp, C.POINTER(Params), vp, vp, vp, vp, i64, C.POINTER(i64)]
     _lib = L

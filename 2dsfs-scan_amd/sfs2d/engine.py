@@ -82,6 +82,19 @@ class Engine:
                     chrom_last_pos: np.ndarray) -> "DeviceData":
         return DeviceData(self, None, (d_counts, d_pos, d_ann, n, chrom_off, chrom_last_pos))
 
+    def synth_sims(self, seed: int, generation: int, n_rep: int, n_win: int, window_bp: int, n1p: int, n2p: int,
+                   win_counts: np.ndarray, mt1: np.ndarray, mt2: np.ndarray) -> "DeviceData":
+        """BASELINE config 4: n_rep replicate chromosomes generated in HBM (sfs2d_data_synth_sims)."""
+        sp = L.SynthParams(seed=seed, generation=generation, n_replicates=n_rep, n_windows=n_win,
+                           window_bp=window_bp, n1p=n1p, n2p=n2p)
+        wc = np.ascontiguousarray(win_counts, np.uint16)
+        m1 = np.ascontiguousarray(mt1, np.uint32)
+        m2 = np.ascontiguousarray(mt2, np.uint32)
+        h = C.c_void_p()
+        self.check(self.lib.sfs2d_data_synth_sims(self.h, C.byref(sp), L.ptr(wc), L.ptr(m1), len(m1), L.ptr(m2),
+                                                  len(m2), C.byref(h)))
+        return DeviceData(self, None, dev=h)
+
     def bg_hist(self, data: "DeviceData", cfg: ScanConfig, chrom: int = -1):
         n1, n2 = 2 * cfg.n1p, 2 * cfg.n2p
         h2 = np.zeros((n1 + 1) * (n2 + 1), np.int64)
@@ -112,6 +125,10 @@ class DeviceData:
     def __init__(self, eng: Engine, p: Optional[PackedSNPs], dev=None):
         self.eng = eng
         self.h = C.c_void_p()
+        if isinstance(dev, C.c_void_p):   # a handle the library already created (sfs2d_data_synth_sims)
+            self.packed = None
+            self.h = dev
+            return
         if p is not None:
             self.packed = p
             off = np.ascontiguousarray(p.chrom_off, np.int64)
@@ -125,6 +142,13 @@ class DeviceData:
             eng.check(eng.lib.sfs2d_data_wrap_device(eng.h, C.c_void_p(d_counts), C.c_void_p(d_pos),
                                                      C.c_void_p(d_ann) if d_ann else None, int(n), L.ptr(off),
                                                      L.ptr(lp), len(off) - 1, C.byref(self.h)))
+
+    def read(self, n: int):
+        """(counts, pos) of the data set back on the host (n = its SNP count)."""
+        c = np.zeros(n, np.uint32)
+        p = np.zeros(n, np.uint32)
+        self.eng.check(self.eng.lib.sfs2d_data_read(self.h, L.ptr(c), L.ptr(p), int(n)))
+        return c, p
 
     def close(self):
         if self.h:

@@ -113,6 +113,25 @@ int sfs2d_data_wrap_device(sfs2d_ctx* ctx, const uint32_t* d_counts, const uint3
                            const uint32_t* chrom_last_pos, int32_t nchrom, sfs2d_data** out);
 int sfs2d_data_free(sfs2d_data* data);
 
+/* Synthetic sims replicates generated in HBM (BASELINE config 4: sims_scan.likelihood_scan's
+ * replicate VCFs, sims_scan.py:593-644, at thousands of replicates).  Each replicate is one
+ * chromosome of n_windows fixed windows of window_bp; win_snps[r * n_windows + w] (host) SNPs in
+ * window w of replicate r (the caller draws them, e.g. Poisson(358.5)); per-SNP values from a
+ * counter-based Philox stream keyed by seed and generation (the model is in sfs2d_kernels.hpp;
+ * the host twin sfs2d.synth.sims_host reproduces it bit for bit).  miss_cdf1 / miss_cdf2: u32
+ * inverse-CDF thresholds of the missing-allele counts of each population (nm entries, the last
+ * 0xffffffff).  The data set owns its arrays. */
+typedef struct {
+  uint64_t seed;
+  uint32_t generation, n_replicates, n_windows, window_bp;
+  int32_t n1p, n2p;   /* diploid pop sizes: counts <= 2 * pop size */
+} sfs2d_synth_params;
+int sfs2d_data_synth_sims(sfs2d_ctx* ctx, const sfs2d_synth_params* sp, const uint16_t* win_snps,
+                          const uint32_t* miss_cdf1, int32_t nm1, const uint32_t* miss_cdf2, int32_t nm2,
+                          sfs2d_data** out);
+/* copy a data set's packed counts / positions to host (n = the data set's SNP count; NULL skips) */
+int sfs2d_data_read(const sfs2d_data* data, uint32_t* counts, uint32_t* pos, int64_t n);
+
 /* Background SFS histograms of chromosome `chrom` (-1: all SNPs of the data set), with the
  * params' filters (position, variant_type, fold).  h2d: (2n1p+1)*(2n2p+1) int64, row-major
  * (alt1, alt2); h1a / h1b: UNFOLDED 1D spectra of raw alt counts, 2*pop_size+1 int64 each. */
