@@ -126,7 +126,8 @@ struct sfs2d_plan {
   unsigned long long* d_fsum = nullptr;   // k_prep's per-slot Fst sums (int64 fixed point), cleared by the scan
   int hr = 1;               // k_prep LDS histogram copies per word
   uint64_t runs = 0;        // completed runs (the replica parity of a fused plan)
-  int G = 64;
+  int G = 64;               // 64: k_scan_w; 256: large grids (k_scan_gw when gw, else k_scan_g)
+  bool gw = false;
   bool p16 = true;
   size_t scan_lds = 0, bg_lds = 0, extra_lds = 0;
   int64_t nslots = 0, nrec = 0, extra_rec = -1;
@@ -242,11 +243,23 @@ void launch_scan_g(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
                      pl->ctx->d_lnx, out, bp, pl->d_fsum, pl->d_fst);
 }
 
+template <bool P16, bool FST>
+void launch_scan_gw(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
+  hipExtLaunchKernelGGL((k_scan_gw<P16, FST>), dim3((unsigned)pl->chunks.size()), dim3(WAVE), pl->scan_lds,
+                     pl->ctx->stream, pl->kev[4], pl->kev[5], 0, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
+                     per_chrom, pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, bp, pl->d_repl, pl->d_bcount,
+                     0, pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels, -1, pl->d_fsum, pl->d_fst,
+                     pl->d_ctr, (int)(pl->runs & 1), pl->d_leafsum, pl->d_bg1d, 0);
+}
+
 template <bool P16>
 hipError_t launch_scan(sfs2d_plan* pl, sfs2d_window* out) {
   const int per_chrom = pl->prm.bg_mode == SFS2D_BG_PER_CHROM ? 1 : 0;
   const int bp = pl->prm.window_mode == SFS2D_WINDOW_BP ? 1 : 0;
-  if (pl->G == WAVE) {
+  if (pl->gw) {
+    if (pl->fst) launch_scan_gw<P16, true>(pl, out, per_chrom, bp);
+    else launch_scan_gw<P16, false>(pl, out, per_chrom, bp);
+  } else if (pl->G == WAVE) {
     if (pl->fused) {
       if (pl->fst && !pl->fst_win) launch_scan_w<P16, true, true>(pl, out, per_chrom, bp);
       else launch_scan_w<P16, true, false>(pl, out, per_chrom, bp);
@@ -343,7 +356,8 @@ hipError_t launch_attached(sfs2d_plan* a) {
                        d->nchrom, (uint32_t)a->prm.window, ns, a->d_slots);
   if (a->fst_m)
     hipLaunchKernelGGL(k_fst_agg, g, dim3(256), 0, a->ctx->stream, a->base->d_fsum, a->base->d_slot_base,
-                       a->d_slot_base, d->nchrom, a->fst_m, ns, a->d_fsum);
+                       a->d_slot_base, d->nchrom, a->fst_m, ns,
+                       std::max(0, a->base->K.fst_e - a->K.fst_e), a->d_fsum);
   if (a->fst_win)   // before the scan clears the slots
     hipLaunchKernelGGL(k_fst_win, dim3((unsigned)std::min<uint32_t>(2048u, (ns + 3u) / 4u)), dim3(256), 0,
                        a->ctx->stream, d->counts, a->d_bins, a->d_slots,
@@ -600,6 +614,8 @@ static int make_kparams(sfs2d_ctx* ctx, const sfs2d_params* prm, int nchrom, KPa
   K->ws = (unsigned)prm->window;
   div_magic(K->ws, &K->wmag, &K->wsh1, &K->wsh2);
   K->nchrom = nchrom;
+  K->fst_e = 40;   // plan_create narrows this to the plan's windows
+  K->fst_scale = std::ldexp(1.0, K->fst_e);
   return 0;
 }
 
@@ -650,6 +666,11 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
 
   // LDS strategy: a wavefront per window with u16-packed 2D bins for small grids, a workgroup per
   // window for large ones; u16 bins need < 65536 SNPs of one window in one bin.
+  // (maxsnp: the most SNPs any window can hold, bounding the Fst fixed-point sums)
+  int64_t maxc = 0;
+  for (int c = 0; c < nc; ++c) maxc = std::max<int64_t>(maxc, data->chrom_off[c + 1] - data->chrom_off[c]);
+  int64_t maxsnp = maxc;
+  if (!bp || data->strict) maxsnp = std::min<int64_t>(maxc, prm->window);
   bool p16_ok;
   if (!bp) {
     p16_ok = prm->window <= 65535;
@@ -670,10 +691,18 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
       }
     }
     p16_ok = longest <= 65535;
+    maxsnp = std::min(maxsnp, longest);
   } else {
     p16_ok = false;
   }
   pl->p16 = p16_ok;
+  {
+    // Fst fixed point 2^e: maxsnp terms of |x| <= 1 stay below 2^62 (e = 46 for 20 kb windows)
+    int b = 0;
+    while (b < 62 && (int64_t(1) << b) <= maxsnp) ++b;   // bit length of maxsnp
+    pl->K.fst_e = std::max(8, std::min(FST_E_MAX, 61 - b));
+    pl->K.fst_scale = std::ldexp(1.0, pl->K.fst_e);
+  }
   pl->G = (K.nb2 <= 8192) ? 64 : 256;
   {
     const int core = (pl->p16 ? (K.nb2 + 1) / 2 : K.nb2) + (K.n1p + 1) + (K.n2p + 1);
@@ -687,6 +716,25 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
       pl->scan_lds = sizeof(double) * (size_t)(((K.nt + 1) & ~1) + 2 * LNT) + hist_words * 4;
     } else {
       pl->scan_lds = (size_t)(core + TRASH + 2) * 4 + 32 * 8 + 32 * 8;
+      // k_scan_gw (a wavefront per window, tables from L2) when its one-wave workgroups, whose LDS
+      // holds only the wave's histograms, still leave >= 2 wavefronts per CU (101 x 101: 7);
+      // otherwise k_scan_g (a workgroup per window).  SFS2D_GW=0/1 forces one.
+      const int h2w = pl->p16 ? (((K.nb2 + 1) / 2 + 3) & ~3) : ((K.nb2 + 3) & ~3);
+      const size_t gw_lds = (size_t)(h2w + R1 * (K.n1p + 1) + R1 * (K.n2p + 1) + TRASH) * 4;
+      int occ = 0;
+      if (gw_lds <= 160 * 1024) {
+        const hipFuncAttribute A = hipFuncAttributeMaxDynamicSharedMemorySize;
+        if (gw_lds > 64 * 1024)
+          for (const void* f : {(const void*)k_scan_gw<true, false>, (const void*)k_scan_gw<false, false>,
+                                (const void*)k_scan_gw<true, true>, (const void*)k_scan_gw<false, true>})
+            hipFuncSetAttribute(f, A, (int)gw_lds);
+        const hipError_t oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<true, true>, WAVE, gw_lds)
+                                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<false, true>, WAVE, gw_lds);
+        if (oe != hipSuccess) occ = 0;
+        pl->gw = occ >= 2;   // measured: 201 x 151 (2 per CU) 22 vs 32 us for k_scan_g
+        if (const char* ev = std::getenv("SFS2D_GW")) pl->gw = occ >= 1 && ev[0] == '1';
+      }
+      if (pl->gw) pl->scan_lds = gw_lds;
     }
   }
   if (pl->scan_lds > 160 * 1024) {
@@ -739,11 +787,14 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   // then windows from its chromosome's pool counters until they run dry (windows cost up to ~3x
   // each other, so static chunks left the slowest workgroups 2x behind the median).
   // k_scan_g: two windows per workgroup.
-  if (pl->G == WAVE) {
+  if (pl->G == WAVE || pl->gw) {
     int occ = 0;
     // (the grid is one dispatch wave of resident workgroups: occupancy of the variant that runs)
     hipError_t oe;
-    if (pl->fused)
+    if (pl->gw)
+      oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<true, true>, WAVE, pl->scan_lds)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<false, true>, WAVE, pl->scan_lds);
+    else if (pl->fused)
       oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<true, true, true>, SBLOCK, pl->scan_lds)
                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<false, true, true>, SBLOCK, pl->scan_lds);
     else
@@ -753,13 +804,18 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
     int64_t cap = (int64_t)occ * ctx->ncu;
     if (const char* ev = std::getenv("SFS2D_WGS")) cap = std::max<int64_t>(1, std::atoll(ev));   // tuning
     const double S = (double)std::max<unsigned long long>(1, slot_base[nc] - slot_base[0]);
-    constexpr uint32_t NW = SBLOCK / WAVE;
+    const uint32_t NW = pl->gw ? 1u : (uint32_t)(SBLOCK / WAVE);   // wavefronts per workgroup
     std::vector<double> order;
     for (int c = 0; c < nc; ++c) {
       const uint32_t ns = (uint32_t)(slot_base[c + 1] - slot_base[c]);
       if (!ns) continue;
       const uint32_t wmax = (ns + NW - 1) / NW;
-      const uint32_t nwg = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(wmax, std::llround(cap * (ns / S))));
+      int64_t want = std::llround(cap * (ns / S));
+      // k_scan_gw has no table prologue: many small chromosomes (sims batches: thousands of
+      // replicates) get ~64 windows per workgroup instead of one workgroup each, which would leave
+      // the last dispatch wave's workgroups running alone
+      if (pl->gw) want = std::max<int64_t>(want, (ns + 63) / 64);
+      const uint32_t nwg = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(wmax, want));
       uint32_t npool = std::min<uint32_t>(nwg, CTR_POOLS);
       if (const char* ev = std::getenv("SFS2D_POOLS")) npool = std::max(1u, std::min<uint32_t>(npool, (uint32_t)std::atoi(ev)));   // tuning
       for (uint32_t k = 0; k < nwg; ++k) {
@@ -971,7 +1027,7 @@ int sfs2d_plan_run_phase(sfs2d_plan* pl, int phase, sfs2d_window* out_dev) {
 int sfs2d_plan_grids(const sfs2d_plan* pl, int64_t* prep_threads, int64_t* scan_threads) {
   if (!pl) return SFS2D_E_ARG;
   if (prep_threads) *prep_threads = (int64_t)pl->tiles.size() * BLOCK1;
-  if (scan_threads) *scan_threads = (int64_t)pl->chunks.size() * (pl->G == WAVE ? SBLOCK : BLOCK);
+  if (scan_threads) *scan_threads = (int64_t)pl->chunks.size() * (pl->G == WAVE ? SBLOCK : pl->gw ? WAVE : BLOCK);
   return 0;
 }
 

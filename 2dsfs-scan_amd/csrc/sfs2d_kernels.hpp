@@ -33,7 +33,8 @@
 //   k_scan_w      the hot loop (small grids): one wavefront per window, 8 per workgroup sharing the
 //                 background's log-proportion table and the D / x ln x tables in LDS; bins streamed
 //                 with 16-B loads; one fp64 DPP reduction per spectrum; one 64-B record per window.
-//   k_scan_g      large grids: one workgroup per window (exact evaluation).
+//   k_scan_gw     large grids: k_scan_w's loop in one-wavefront workgroups, tables read from L2.
+//   k_scan_g      grids too large for k_scan_gw: one workgroup per window (exact evaluation).
 //   k_scan_extra  combined_scan's final-window helper (quirk Q9).
 #pragma once
 
@@ -94,6 +95,8 @@ struct KParams {
   unsigned int wmag;     // (p-1)/ws as a multiply-high: q = (t + ((n - t) >> wsh1)) >> wsh2, t = mulhi(n, wmag)
   int wsh1, wsh2;
   int nchrom;
+  int fst_e;             // Fst fixed point: sums of 2^fst_e-scaled terms (|term| <= 1), chosen per plan so
+  double fst_scale;      // that the most SNPs a window can hold cannot overflow int64 (fst_fixed)
 };
 
 struct Tile {   // k_prep work item: SNPs [begin, end) of chromosome chrom = [cb, ce), slots from sbase
@@ -111,7 +114,7 @@ constexpr int CTR_STRIDE = 16;   // one 64-B line per pool counter
 #endif
 constexpr int FST_LDS = SFS2D_FST_LDS;             // k_prep: windows per tile accumulated in LDS (others: global)
 constexpr int FST_R = SFS2D_FST_R;                 // ... in FST_R interleaved copies (lane & 3) to spread same-window atomics
-constexpr double FST_SCALE = 1099511627776.0;   // 2^40: Fst sums as int64 fixed point (deterministic atomics)
+constexpr int FST_E_MAX = 49;   // Fst sums as int64 fixed point (deterministic atomics): at most 2^49 per unit
 
 struct Chunk {  // k_scan work item: window slots [slot_lo, slot_hi) of one chromosome
   uint32_t chrom, slot_lo, slot_hi, wid_lo, cb;
@@ -404,10 +407,11 @@ __device__ __forceinline__ void fst_snp(uint32_t c, bool member, const double2* 
   den = fma(-2.0, m, p1 + p2);
 }
 
-// x * 2^40 rounded to the nearest integer, |x| < 2^11 (the magic-number conversion: 1.5 * 2^52 pins the
-// exponent, the low mantissa bits then hold the integer)
-__device__ __forceinline__ unsigned long long fst_fixed(double x) {
-  const double y = fma(x, FST_SCALE, 6755399441055744.0);
+// x * scale rounded to the nearest integer, |x * scale| < 2^51 (the magic-number conversion:
+// 1.5 * 2^52 pins the exponent, the low mantissa bits then hold the integer); scale <= 2^FST_E_MAX
+// and the Fst terms are within [-1, 1]
+__device__ __forceinline__ unsigned long long fst_fixed(double x, double scale) {
+  const double y = fma(x, scale, 6755399441055744.0);
   return (unsigned long long)(__double_as_longlong(y) - 0x4338000000000000ll);
 }
 
@@ -453,7 +457,7 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
   // fixed-point add of one lane's (num, den) pair into window wid of this chromosome
   const int frep = threadIdx.x & (FST_R - 1);
   auto fst_add = [&](uint32_t wid, double num, double den) {
-    const unsigned long long qn = fst_fixed(num), qd = fst_fixed(den);
+    const unsigned long long qn = fst_fixed(num, P.fst_scale), qd = fst_fixed(den, P.fst_scale);
     if ((qn | qd) == 0ull) return;
     const uint32_t j = wid - wlo;
 #ifdef SFS2D_EXP_NOATOM
@@ -1509,35 +1513,40 @@ __device__ __forceinline__ void fused_table(int nb2, int nh, int nt, int n1p, in
 // per-lane counters give every count, the 2D atomic returns the SNP's rank r in its bin and the
 // SNP adds D(r) - lp_k; the 1D atomics land in lane-&3 replicas; then one lane per 1D bin adds
 // x ln x - x lp; the touched 2D words are cleared; DPP sums; one record.
-template <bool P16, bool FUSED, bool FST>
-__global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_scan_w(KParams P, const uint32_t* __restrict__ bins,
-                                                   const Chunk* __restrict__ chunks, uint2* __restrict__ slots,
-                                                   PL* __restrict__ tab, double* __restrict__ LPg,
-                                                   BgHead* __restrict__ head, int bg_per_chrom,
-                                                   const double* __restrict__ lnx, const double* __restrict__ dfg,
-                                                   sfs2d_window* __restrict__ out, uint32_t* __restrict__ err_word,
-                                                   int mode_bp, uint32_t* __restrict__ repl,
-                                                   uint32_t* __restrict__ bcount, int par,
-                                                   const int2* __restrict__ leaves, int nleaves,
-                                                   const int4* __restrict__ nodes, int nnodes, int nlevels,
-                                                   int write_chrom, unsigned long long* __restrict__ fsum,
-                                                   double* __restrict__ fst_out, uint32_t* __restrict__ ctr,
-                                                   int cpar, const double* __restrict__ leafsum,
-                                                   const Bg1D* __restrict__ bg1d, int sliced) {
-  extern __shared__ double ldsd[];
+// GL (k_scan_gw, grids too large for the table in LDS): one-wavefront workgroups whose LDS holds
+// only the wave's histograms; lp, D and F are read from the global tables (L2-resident: one
+// table per background, read by every window).
+#define SCAN_W_ARGS                                                                                           \
+  KParams P, const uint32_t *__restrict__ bins, const Chunk *__restrict__ chunks, uint2 *__restrict__ slots,  \
+      PL *__restrict__ tab, double *__restrict__ LPg, BgHead *__restrict__ head, int bg_per_chrom,            \
+      const double *__restrict__ lnx, const double *__restrict__ dfg, sfs2d_window *__restrict__ out,          \
+      uint32_t *__restrict__ err_word, int mode_bp, uint32_t *__restrict__ repl, uint32_t *__restrict__ bcount, \
+      int par, const int2 *__restrict__ leaves, int nleaves, const int4 *__restrict__ nodes, int nnodes,       \
+      int nlevels, int write_chrom, unsigned long long *__restrict__ fsum, double *__restrict__ fst_out,       \
+      uint32_t *__restrict__ ctr, int cpar, const double *__restrict__ leafsum, const Bg1D *__restrict__ bg1d, \
+      int sliced
+#define SCAN_W_PASS                                                                                           \
+  P, bins, chunks, slots, tab, LPg, head, bg_per_chrom, lnx, dfg, out, err_word, mode_bp, repl, bcount, par,  \
+      leaves, nleaves, nodes, nnodes, nlevels, write_chrom, fsum, fst_out, ctr, cpar, leafsum, bg1d, sliced
+
+template <bool P16, bool FUSED, bool FST, bool GL>
+__device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
+  static_assert(!(GL && FUSED), "k_scan_gw reads finished tables");
+  constexpr int NT = GL ? WAVE : SBLOCK;   // threads per workgroup
   __shared__ BgHead sh_hb;
   STAMP(10);
   BLK_STAMP(1, 0);
   const int tid = threadIdx.x;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wv = GL ? 0 : __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & (WAVE - 1);
   const Chunk ch = chunks[blockIdx.x];
   const int bg = bg_per_chrom ? (int)ch.chrom : 0;
 
-  double* LPl = ldsd;                            // nt (rounded up to even: the histograms are 16-B aligned)
-  double* Dt = LPl + ((P.nt + 1) & ~1);          // LNT
-  double* Ft = Dt + LNT;                         // LNT
-  uint32_t* HB = reinterpret_cast<uint32_t*>(Ft + LNT);
+  // LDS (!GL): lp table (nt, rounded up to even: the histograms are 16-B aligned) | D | F | histograms
+  double* LPl = GL ? LPg + (size_t)bg * P.nt : ldsd;
+  double* Dt = GL ? const_cast<double*>(dfg) : LPl + ((P.nt + 1) & ~1);   // LNT
+  double* Ft = Dt + LNT;                                                   // LNT
+  uint32_t* HB = GL ? reinterpret_cast<uint32_t*>(ldsd) : reinterpret_cast<uint32_t*>(Ft + LNT);
   const int h2w = P16 ? ((P.nb2 + 1) / 2 + 3) & ~3 : (P.nb2 + 3) & ~3;
   const int h1w = R1 * (P.n1p + 1), h1wb = R1 * (P.n2p + 1);
   const int per = h2w + h1w + h1wb + TRASH;
@@ -1576,13 +1585,16 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) voi
   uint32_t gq = 0;
   if (active && dyn && lane == 0) gq = atomicAdd(myctr, 1u);
   if (blockIdx.x == 0)   // the other parity's counters, for the next run
-    for (int k = tid; k < P.nchrom * CTR_POOLS; k += SBLOCK) ctr[((size_t)(1 - cpar) * P.nchrom * CTR_POOLS + k) * CTR_STRIDE] = 0u;
+    for (int k = tid; k < P.nchrom * CTR_POOLS; k += NT) ctr[((size_t)(1 - cpar) * P.nchrom * CTR_POOLS + k) * CTR_STRIDE] = 0u;
 
-  for (int k = tid; k < 2 * LNT; k += SBLOCK) Dt[k] = dfg[k];
+  if (!GL)
+    for (int k = tid; k < 2 * LNT; k += SBLOCK) Dt[k] = dfg[k];
   BgHead hb;
   const size_t rs = (size_t)P.nchrom * P.nh;     // replica stride
   const uint32_t* Rc = repl + (size_t)par * REPL * rs + (size_t)ch.chrom * P.nh;
-  if (!FUSED) {
+  if (GL) {
+    hb = head[bg];
+  } else if (!FUSED) {
     const double* LP = LPg + (size_t)bg * P.nt;
     for (int k = tid; k < P.nt; k += SBLOCK) LPl[k] = LP[k];
     if (sliced) {
@@ -1636,7 +1648,7 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) voi
     hb = sh_hb;
   }
   for (int k = lane; k < per / 4; k += WAVE) reinterpret_cast<uint4*>(W)[k] = make_uint4(0, 0, 0, 0);
-  if (tid == 0) LPl[0] = 0.0;   // bin 0 ((0,0), never counted): excluded SNPs read it and add 0
+  if (!GL && tid == 0) LPl[0] = 0.0;   // bin 0 ((0,0), never counted): excluded SNPs read it and add 0
   __syncthreads();
   const bool filt = P.ann_want >= 0;
   const bool half1d = P.n1p <= 33 && P.n2p <= 33;
@@ -1654,6 +1666,7 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) voi
       for (int c = tid; c < P.nchrom; c += SBLOCK) bcount[(size_t)(1 - par) * P.nchrom + c] = 0u;
   }
   if (!active) return;
+  const double Dreg = GL ? dfg[lane] : 0.0;     // GL: D(lane)
   const uint32_t one1 = P16 ? 0x10000u : 1u;   // 1D increment (P16: counts in the upper halves)
   uint32_t* const H1a_l = H1a + rep;            // this lane's replica column of the 1D histograms
   uint32_t* const H1b_l = H1b + rep;
@@ -1719,8 +1732,14 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) voi
       double d[2], lp[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        d[q] = Dt[min(rk[q], (uint32_t)LNT - 1u)];   // D[LNT-1] = 0: ranks past the table add 0
+        if (GL) {   // D(r) for r < 64 from the lanes' registers, the global table beyond
+          d[q] = __shfl(Dreg, (int)(rk[q] & 63u));
+          if (rk[q] >= 64u) d[q] = Dt[min(rk[q], (uint32_t)LNT - 1u)];
+        } else {
+          d[q] = Dt[min(rk[q], (uint32_t)LNT - 1u)];   // D[LNT-1] = 0: ranks past the table add 0
+        }
         lp[q] = LPl[kk[q]];
+        if (GL && !kk[q]) lp[q] = 0.0;   // (the global table's bin 0 is not zeroed)
       }
 #pragma unroll
       for (int q = 0; q < 2; ++q) acc2 += d[q] - lp[q];
@@ -1746,6 +1765,9 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) voi
       }
     }
     if (!filt) nvar = nsnp;
+    // GL: the totals' x ln x from the global table, issued now (their latency under the 1D pass)
+    double fn2 = 0.0, fn1a = 0.0, fn1b = 0.0;
+    if (GL) { fn2 = xlnx(n2, Ft, lnx); fn1a = xlnx(n1a, Ft, lnx); fn1b = xlnx(n1b, Ft, lnx); }
     ulonglong2 fq = make_ulonglong2(0ull, 0ull);   // this window's Fst sums (k_prep), used at the end
     if (FST && lane == 0) fq = reinterpret_cast<const ulonglong2*>(fsum)[s];
     const bool ov = nsnp > (uint32_t)(LNT - 1);   // some rank may have passed the D table
@@ -1817,9 +1839,9 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) voi
     }
     WinOut w;
     w.snp_count = nvar; w.n2_all = n2 + nlast; w.n2 = n2; w.n1a = n1a; w.n1b = n1b;
-    w.t2d = 2.0 * (s2 - xlnx(n2, Ft, lnx));
-    w.t1a = 2.0 * (sa - xlnx(n1a, Ft, lnx));
-    w.t1b = 2.0 * (sb - xlnx(n1b, Ft, lnx));
+    w.t2d = 2.0 * (s2 - (GL ? fn2 : xlnx(n2, Ft, lnx)));
+    w.t1a = 2.0 * (sa - (GL ? fn1a : xlnx(n1a, Ft, lnx)));
+    w.t1b = 2.0 * (sb - (GL ? fn1b : xlnx(n1b, Ft, lnx)));
     if (cur.e - cur.b >= 65536u || suspect_zero(w.t2d, n2) || suspect_zero(w.t1a, n1a) ||
         suspect_zero(w.t1b, n1b)) {
       // rare: exact re-evaluation with the bin-by-bin proportionality test (histograms are clean)
@@ -1828,6 +1850,9 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) voi
         w = eval_exact<WAVE, P16, R1>(P, bins, cur.b, cur.e,
                                       TabFused{LPl, Rc, rs, P.nb2, P.n1, P.n2, P.n1p, P.h1a, P.h1b, P.t1a, P.t1b}, hb,
                                       lnx, W, H1a, H1b, nullptr, nullptr);
+      else if (GL)
+        w = eval_exact<WAVE, P16, R1>(P, bins, cur.b, cur.e, TabGlobal{tab + (size_t)bg * P.nt}, hb, lnx, W, H1a,
+                                      H1b, nullptr, nullptr);
       else
         w = eval_exact<WAVE, P16, R1>(P, bins, cur.b, cur.e, TabLocal{tab + (size_t)bg * P.nt, LPl}, hb, lnx, W,
                                       H1a, H1b, nullptr, nullptr);
@@ -1855,6 +1880,19 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) voi
   __builtin_amdgcn_s_barrier();   // diagnostic build only: the block's end is its last active wave's
 #endif
   BLK_STAMP(1, 1);
+}
+
+template <bool P16, bool FUSED, bool FST>
+__global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_scan_w(SCAN_W_ARGS) {
+  extern __shared__ double ldsd[];
+  scan_w_body<P16, FUSED, FST, false>(ldsd, SCAN_W_PASS);
+}
+
+// K3 for large grids, one wavefront per window (LDS: the wave's histograms only)
+template <bool P16, bool FST>
+__global__ __launch_bounds__(WAVE) void k_scan_gw(SCAN_W_ARGS) {
+  extern __shared__ double ldsd[];
+  scan_w_body<P16, false, FST, true>(ldsd, SCAN_W_PASS);
 }
 
 // K3 for large grids: one workgroup per window, exact evaluation.
@@ -2000,7 +2038,7 @@ __global__ __launch_bounds__(256) void k_slots_bp(const uint32_t* __restrict__ p
 __global__ __launch_bounds__(256) void k_fst_agg(const unsigned long long* __restrict__ bsum,
                                                  const uint32_t* __restrict__ bslot_base,
                                                  const uint32_t* __restrict__ slot_base, int nchrom, uint32_t m,
-                                                 uint32_t nslots, unsigned long long* __restrict__ fsum) {
+                                                 uint32_t nslots, int shift, unsigned long long* __restrict__ fsum) {
   const uint32_t s = blockIdx.x * 256u + threadIdx.x;
   if (s >= nslots) return;
   int lo = 0, hi = nchrom;
@@ -2011,10 +2049,12 @@ __global__ __launch_bounds__(256) void k_fst_agg(const unsigned long long* __res
   }
   const uint32_t j = s - slot_base[lo];
   const uint32_t b0 = bslot_base[lo] + j * m, b1 = min(b0 + m, bslot_base[lo + 1]);
+  // the base's sums, rounded to this plan's coarser fixed point (its windows may hold more SNPs)
+  const long long half = shift ? 1ll << (shift - 1) : 0ll;
   unsigned long long qn = 0, qd = 0;
   for (uint32_t b = b0; b < b1; ++b) {
-    qn += bsum[2 * (size_t)b];
-    qd += bsum[2 * (size_t)b + 1];
+    qn += (unsigned long long)(((long long)bsum[2 * (size_t)b] + half) >> shift);
+    qd += (unsigned long long)(((long long)bsum[2 * (size_t)b + 1] + half) >> shift);
   }
   fsum[2 * (size_t)s] = qn;
   fsum[2 * (size_t)s + 1] = qd;

@@ -324,6 +324,52 @@ def test_dynamic_window_pools(monkeypatch, wgs):
         assert outs[0] == outs[1] == outs[2]
 
 
+@pytest.mark.parametrize("gw", ["0", "1"])
+@pytest.mark.parametrize("n1p,n2p", [(50, 50), (100, 75)])
+def test_large_grid_kernels(monkeypatch, gw, n1p, n2p):
+    """Grids > 8192 bins through each large-grid kernel, forced on both grid sizes (by default
+    both take k_scan_gw, a wavefront per window with the tables read from L2; k_scan_g, a
+    workgroup per window, is kept for grids leaving one such wavefront per CU): records of fixed-bp
+    and SNP-count windows over many chromosomes (k_scan_gw's several workgroups per chromosome),
+    Fst, and repeated runs."""
+    from sfs2d import _lib as L
+    from sfs2d.engine import Engine, ScanConfig
+    from sfs2d.synth import synth_genome
+    monkeypatch.setenv("SFS2D_GW", gw)
+    p = synth_genome(9, [700 + 311 * i for i in range(8)] + [3], n1p, n2p, seed=n1p * 3 + int(gw))
+    ocfg = O.Cfg(n1p, n2p)
+    bgs = O.chrom_backgrounds(p, ocfg)
+    for mode, ws in ((L.WINDOW_BP, 30000), (L.WINDOW_SNPS, 90)):
+        cfg = ScanConfig(n1p=n1p, n2p=n2p, window_mode=mode, window=ws)
+        wins = O.snp_windows(p, ws)[0] if mode == L.WINDOW_SNPS else O.bp_windows(p, ws)
+        _records_vs_oracle(p, cfg, ocfg, wins, lambda c: bgs[c])
+    eng = Engine.get(0)
+    dev = eng.upload(p)
+    pl = eng.plan(dev, ScanConfig(n1p=n1p, n2p=n2p, window=30000, fst=True))
+    last = [int(p.pos[p.chrom_off[c + 1] - 1]) for c in range(p.nchrom)]
+    nslots = [(max(x, 1) - 1) // 30000 + 1 for x in last]   # fixed-bp slots per chromosome
+    g_threads = 256 * sum((n + 1) // 2 for n in nslots)   # k_scan_g: two windows per workgroup
+    assert (pl.grids()[1] == g_threads) == (gw == "0")
+    outs = []
+    for _ in range(3):
+        pl.run()
+        pl.check()
+        outs.append((pl.read(), pl.read_fst()))
+    recs, fst = outs[0]
+    live = (recs["flags"][: len(fst)] & L.W_EMPTY) == 0
+    got = fst[live]
+    wins = [(b, e) for (c, s, b, e) in O.bp_windows(p, 30000)]
+    assert len(got) == len(wins)
+    for g, (b, e) in zip(got, wins):
+        assert _fst_close(float(g), O.window_fst(p, np.arange(b, e), ocfg)), (g, b, e)
+    for r, f in outs[1:]:
+        assert np.array_equal(r["snp_count"], recs["snp_count"]) and np.array_equal(f, fst, equal_nan=True)
+        for k in ("t2d", "t1d_p1", "t1d_p2"):
+            a, b = r[k].astype(float), recs[k].astype(float)
+            assert np.allclose(a, b, rtol=1e-12, atol=1e-12, equal_nan=True)
+    pl.close()
+
+
 def test_called_counts_above_sample_size_inside_long_tiles():
     """SNPs whose called allele count r + a exceeds 2 * pop_size without leaving the grid (no fold
     swap, so the 2D key is the alt count): the reference counts them; k_prep routes their steps

@@ -31,8 +31,8 @@ def test_batch_golden(golden, tag):
     extra = synth_genome(2, [4000, 2500], n, n, seed=3, chrom_prefix="1.")
     outs = S.process_windows_batch([rep, extra, rep], *bg, 500000, "p1", "p2", n, n)
     assert not gu.compare_results(outs[0], ref) and not gu.compare_results(outs[2], ref)
-    # (n = 100 takes the workgroup-per-window path, whose fp64 sums follow the order in which lanes win
-    # the histogram take-and-clear: equal within the tolerance, not bit for bit)
+    # (n = 100 takes the large-grid path, whose exact re-evaluations sum in the order in which lanes
+    # win the histogram take-and-clear: equal within the tolerance, not bit for bit)
     assert not gu.compare_results(outs[1], S.process_window(extra, *bg, 500000, "p1", "p2", n, n, None, None, None))
 
 
