@@ -128,6 +128,8 @@ struct sfs2d_plan {
   uint64_t runs = 0;        // completed runs (the replica parity of a fused plan)
   int G = 64;               // 64: k_scan_w; 256: large grids (k_scan_gw when gw, else k_scan_g)
   bool gw = false;
+  uint32_t* d_gscr = nullptr;   // k_scan_gw: nscr u32 histograms (nb2 words) + nscr lock words, for exact re-evaluations
+  int nscr = 0;
   bool p16 = true;
   size_t scan_lds = 0, bg_lds = 0, extra_lds = 0;
   int64_t nslots = 0, nrec = 0, extra_rec = -1;
@@ -214,7 +216,7 @@ void plan_free(sfs2d_plan* p) {
   hipFree(p->d_tiles); hipFree(p->d_chunks); hipFree(p->d_slots); hipFree(p->d_repl); hipFree(p->d_bcount); hipFree(p->d_ctr);
   hipFree(p->d_done); hipFree(p->d_bgval); hipFree(p->d_tab); hipFree(p->d_lp); hipFree(p->d_head);
   hipFree(p->d_bg1d); hipFree(p->d_leafsum); hipFree(p->d_leaves); hipFree(p->d_nodes); hipFree(p->d_slices);
-  hipFree(p->d_out); hipFree(p->d_err); hipFree(p->d_bins); hipFree(p->d_fst); hipFree(p->d_fsum);
+  hipFree(p->d_out); hipFree(p->d_err); hipFree(p->d_bins); hipFree(p->d_fst); hipFree(p->d_fsum); hipFree(p->d_gscr);
   for (auto& e : p->ev) if (e) hipEventDestroy(e);
   for (auto& e : p->tev) if (e) hipEventDestroy(e);
 }
@@ -233,7 +235,7 @@ void launch_scan_w(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
                      per_chrom, pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, bp, pl->d_repl, pl->d_bcount,
                      plan_par(pl), pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels,
                      pl->extra_rec >= 0 ? (int)pl->last_chrom : -1, pl->d_fsum, pl->d_fst, pl->d_ctr,
-                     (int)(pl->runs & 1), pl->d_leafsum, pl->d_bg1d, pl->sliced ? 1 : 0);
+                     (int)(pl->runs & 1), pl->d_leafsum, pl->d_bg1d, pl->sliced ? 1 : 0, nullptr, 0);
 }
 
 template <bool P16, bool FST>
@@ -249,7 +251,7 @@ void launch_scan_gw(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
                      pl->ctx->stream, pl->kev[4], pl->kev[5], 0, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
                      per_chrom, pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, bp, pl->d_repl, pl->d_bcount,
                      0, pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels, -1, pl->d_fsum, pl->d_fst,
-                     pl->d_ctr, (int)(pl->runs & 1), pl->d_leafsum, pl->d_bg1d, 0);
+                     pl->d_ctr, (int)(pl->runs & 1), pl->d_leafsum, pl->d_bg1d, 0, pl->d_gscr, pl->nscr);
 }
 
 template <bool P16>
@@ -719,8 +721,9 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
       // k_scan_gw (a wavefront per window, tables from L2) when its one-wave workgroups, whose LDS
       // holds only the wave's histograms, still leave >= 2 wavefronts per CU (101 x 101: 7);
       // otherwise k_scan_g (a workgroup per window).  SFS2D_GW=0/1 forces one.
-      const int h2w = pl->p16 ? (((K.nb2 + 1) / 2 + 3) & ~3) : ((K.nb2 + 3) & ~3);
-      const size_t gw_lds = (size_t)(h2w + R1 * (K.n1p + 1) + R1 * (K.n2p + 1) + TRASH) * 4;
+      const int h2w = ((K.nb2 + 3) / 4 + 3) & ~3;   // u8-packed 2D bins
+      size_t gw_lds = (size_t)(h2w + R1 * (K.n1p + 1) + R1 * (K.n2p + 1) + TRASH) * 4;
+      if (const char* ev = std::getenv("SFS2D_GW_PAD")) gw_lds += (size_t)std::atoll(ev);   // occupancy experiments
       int occ = 0;
       if (gw_lds <= 160 * 1024) {
         const hipFuncAttribute A = hipFuncAttributeMaxDynamicSharedMemorySize;
@@ -802,6 +805,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<false, false, true>, SBLOCK, pl->scan_lds);
     if (oe != hipSuccess || occ < 1) occ = 1;
     int64_t cap = (int64_t)occ * ctx->ncu;
+    if (pl->gw) pl->nscr = (int)cap;   // one exact-path histogram per resident wavefront
     if (const char* ev = std::getenv("SFS2D_WGS")) cap = std::max<int64_t>(1, std::atoll(ev));   // tuning
     const double S = (double)std::max<unsigned long long>(1, slot_base[nc] - slot_base[0]);
     const uint32_t NW = pl->gw ? 1u : (uint32_t)(SBLOCK / WAVE);   // wavefronts per workgroup
@@ -914,6 +918,8 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   rc = rc ? rc : dalloc(ctx, &pl->d_done, (size_t)pl->nbg);
   const size_t nctr = (size_t)2 * std::max(1, nc) * CTR_POOLS * CTR_STRIDE;
   rc = rc ? rc : dalloc(ctx, &pl->d_ctr, nctr);
+  const size_t ngscr = pl->gw ? (size_t)pl->nscr * (K.nb2 + 1) : 0;
+  if (pl->gw) rc = rc ? rc : dalloc(ctx, &pl->d_gscr, ngscr);
   rc = rc ? rc : dalloc(ctx, &pl->d_bgval, (size_t)pl->nbg * K.nt);
   rc = rc ? rc : dalloc(ctx, &pl->d_tab, (size_t)pl->nbg * K.nt);
   rc = rc ? rc : dalloc(ctx, &pl->d_lp, (size_t)pl->nbg * K.nt);
@@ -943,6 +949,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_bcount, 0, sizeof(uint32_t) * 2 * std::max(1, nc), st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_done, 0, sizeof(uint32_t) * pl->nbg, st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_ctr, 0, sizeof(uint32_t) * nctr, st);
+  if (e == hipSuccess && pl->gw) e = hipMemsetAsync(pl->d_gscr, 0, sizeof(uint32_t) * ngscr, st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_err, 0, 4 * sizeof(uint32_t), st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_bins, 0, sizeof(uint32_t) * nbins, st);
   if (e == hipSuccess && pl->fst) e = hipMemsetAsync(pl->d_fsum, 0, sizeof(unsigned long long) * 2 * ((size_t)pl->nslots + 1), st);

@@ -1220,6 +1220,7 @@ __device__ __forceinline__ WinOut eval_exact(const KParams& P, const uint32_t* _
     if (g1) { ++c1a; atomicAdd(&H1a[g1 * S1], 1u); }
     if (g2) { ++c1b; atomicAdd(&H1b[g2 * S1], 1u); }
   }
+  if (G == WAVE) __threadfence();   // (k_scan_gw passes a histogram in global memory: adds land before the takes)
   group_sync<G>();
   const unsigned long long r0 = group_sum_u64<G>((unsigned long long)c2 | ((unsigned long long)c_last << 32), redu, 0);
   const unsigned long long r1 = group_sum_u64<G>((unsigned long long)c1a | ((unsigned long long)c1b << 32), redu, 1);
@@ -1515,7 +1516,10 @@ __device__ __forceinline__ void fused_table(int nb2, int nh, int nt, int n1p, in
 // x ln x - x lp; the touched 2D words are cleared; DPP sums; one record.
 // GL (k_scan_gw, grids too large for the table in LDS): one-wavefront workgroups whose LDS holds
 // only the wave's histograms; lp, D and F are read from the global tables (L2-resident: one
-// table per background, read by every window).
+// table per background, read by every window).  The 2D bins are u8-packed (101 x 101: 10 KB per
+// wave, 12 waves per CU instead of 7 with u16): a rank of 255 means the byte wrapped, and such a
+// window is re-evaluated exactly on a u32 histogram in global memory (gscr: nscr slots of nb2
+// words, then nscr lock words; a slot is taken with a CAS, so every resident wave finds one).
 #define SCAN_W_ARGS                                                                                           \
   KParams P, const uint32_t *__restrict__ bins, const Chunk *__restrict__ chunks, uint2 *__restrict__ slots,  \
       PL *__restrict__ tab, double *__restrict__ LPg, BgHead *__restrict__ head, int bg_per_chrom,            \
@@ -1524,10 +1528,11 @@ __device__ __forceinline__ void fused_table(int nb2, int nh, int nt, int n1p, in
       int par, const int2 *__restrict__ leaves, int nleaves, const int4 *__restrict__ nodes, int nnodes,       \
       int nlevels, int write_chrom, unsigned long long *__restrict__ fsum, double *__restrict__ fst_out,       \
       uint32_t *__restrict__ ctr, int cpar, const double *__restrict__ leafsum, const Bg1D *__restrict__ bg1d, \
-      int sliced
+      int sliced, uint32_t *__restrict__ gscr, int nscr
 #define SCAN_W_PASS                                                                                           \
   P, bins, chunks, slots, tab, LPg, head, bg_per_chrom, lnx, dfg, out, err_word, mode_bp, repl, bcount, par,  \
-      leaves, nleaves, nodes, nnodes, nlevels, write_chrom, fsum, fst_out, ctr, cpar, leafsum, bg1d, sliced
+      leaves, nleaves, nodes, nnodes, nlevels, write_chrom, fsum, fst_out, ctr, cpar, leafsum, bg1d, sliced,  \
+      gscr, nscr
 
 template <bool P16, bool FUSED, bool FST, bool GL>
 __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
@@ -1547,7 +1552,7 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
   double* Dt = GL ? const_cast<double*>(dfg) : LPl + ((P.nt + 1) & ~1);   // LNT
   double* Ft = Dt + LNT;                                                   // LNT
   uint32_t* HB = GL ? reinterpret_cast<uint32_t*>(ldsd) : reinterpret_cast<uint32_t*>(Ft + LNT);
-  const int h2w = P16 ? ((P.nb2 + 1) / 2 + 3) & ~3 : (P.nb2 + 3) & ~3;
+  const int h2w = GL ? ((P.nb2 + 3) / 4 + 3) & ~3 : P16 ? ((P.nb2 + 1) / 2 + 3) & ~3 : (P.nb2 + 3) & ~3;
   const int h1w = R1 * (P.n1p + 1), h1wb = R1 * (P.n2p + 1);
   const int per = h2w + h1w + h1wb + TRASH;
   uint32_t* W = HB + wv * per;
@@ -1667,7 +1672,8 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
   }
   if (!active) return;
   const double Dreg = GL ? dfg[lane] : 0.0;     // GL: D(lane)
-  const uint32_t one1 = P16 ? 0x10000u : 1u;   // 1D increment (P16: counts in the upper halves)
+  constexpr bool P16H = P16 && !GL;               // u16-packed 2D bins (GL: u8)
+  const uint32_t one1 = P16H ? 0x10000u : 1u;   // 1D increment (P16: counts in the upper halves)
   uint32_t* const H1a_l = H1a + rep;            // this lane's replica column of the 1D histograms
   uint32_t* const H1b_l = H1b + rep;
   uint32_t* const T_l = W + trash;
@@ -1705,6 +1711,7 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
 
     double acc2 = 0.0;
     uint32_t n2 = 0, nlast = 0, n1a = 0, n1b = 0, nvar = 0;
+    bool ovf = false;   // GL: some u8 bin of this lane wrapped
     uint32_t kw[8];   // the 2D words of the first 8 steps, cleared after the window
     auto pair = [&](uint32_t w0, uint32_t w1, int j, bool keep) {
       if (64 * (j + 2) > (int)nsnp) {   // the window's last steps: SNPs past e are excluded
@@ -1720,10 +1727,16 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
         n2 += __popcll(__ballot(k2 != 0u));
         n1a += __popcll(__ballot(g1 != 0u));
         n1b += __popcll(__ballot(g2 != 0u));
-        const uint32_t word = k2 ? (P16 ? (k2 >> 1) : k2) : trash;
-        const uint32_t sh = P16 ? ((k2 & 1u) << 4) : 0u;
+        const uint32_t word = k2 ? (GL ? (k2 >> 2) : P16 ? (k2 >> 1) : k2) : trash;
+        const uint32_t sh = GL ? ((k2 & 3u) << 3) : P16 ? ((k2 & 1u) << 4) : 0u;
         const uint32_t old = atomicAdd(&W[word], k2 ? (1u << sh) : 0u);
-        rk[q] = P16 ? __builtin_amdgcn_ubfe(old, sh, 16) : (k2 ? old : 0u);
+        if (GL) {   // (the trash word's low byte counts 1D increments: excluded SNPs take rank 0)
+          const uint32_t r = __builtin_amdgcn_ubfe(old, sh, 8);
+          rk[q] = k2 ? r : 0u;
+          ovf |= (k2 != 0u) & (r == 255u);
+        } else {
+          rk[q] = P16 ? __builtin_amdgcn_ubfe(old, sh, 16) : (k2 ? old : 0u);
+        }
         kk[q] = k2;
         if (keep) kw[(j + q) & 7] = word;
         atomicAdd(g1 ? H1a_l + g1 * R1 : T_l, one1);
@@ -1770,7 +1783,7 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
     if (GL) { fn2 = xlnx(n2, Ft, lnx); fn1a = xlnx(n1a, Ft, lnx); fn1b = xlnx(n1b, Ft, lnx); }
     ulonglong2 fq = make_ulonglong2(0ull, 0ull);   // this window's Fst sums (k_prep), used at the end
     if (FST && lane == 0) fq = reinterpret_cast<const ulonglong2*>(fsum)[s];
-    const bool ov = nsnp > (uint32_t)(LNT - 1);   // some rank may have passed the D table
+    const bool ov = !GL && nsnp > (uint32_t)(LNT - 1);   // some rank may have passed the D table (GL: ranks < 256)
     if (it == 0) STAMP(12);
     // next window: its slot record is in, issue its first steps now
     Win nxt;
@@ -1780,7 +1793,7 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
     // 1D spectra: one lane per folded inner bin reads (and clears) its R1 replicas; with <= 32 inner
     // bins per population, lanes 0-31 take population 1 and lanes 32-63 population 2 (acca)
     double acca = 0.0, accb = 0.0;
-    constexpr uint32_t S1 = P16 ? 16u : 0u;
+    constexpr uint32_t S1 = P16H ? 16u : 0u;
     if (half1d) {
       const bool pa = lane < 32;
       const int k = 1 + (lane & 31);
@@ -1842,20 +1855,33 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
     w.t2d = 2.0 * (s2 - (GL ? fn2 : xlnx(n2, Ft, lnx)));
     w.t1a = 2.0 * (sa - (GL ? fn1a : xlnx(n1a, Ft, lnx)));
     w.t1b = 2.0 * (sb - (GL ? fn1b : xlnx(n1b, Ft, lnx)));
-    if (cur.e - cur.b >= 65536u || suspect_zero(w.t2d, n2) || suspect_zero(w.t1a, n1a) ||
+    const bool wrapped = GL && __ballot(ovf) != 0ull;
+    if (wrapped || cur.e - cur.b >= 65536u || suspect_zero(w.t2d, n2) || suspect_zero(w.t1a, n1a) ||
         suspect_zero(w.t1b, n1b)) {
       // rare: exact re-evaluation with the bin-by-bin proportionality test (histograms are clean)
       group_sync<WAVE>();
-      if (FUSED)
+      if (FUSED) {
         w = eval_exact<WAVE, P16, R1>(P, bins, cur.b, cur.e,
                                       TabFused{LPl, Rc, rs, P.nb2, P.n1, P.n2, P.n1p, P.h1a, P.h1b, P.t1a, P.t1b}, hb,
                                       lnx, W, H1a, H1b, nullptr, nullptr);
-      else if (GL)
-        w = eval_exact<WAVE, P16, R1>(P, bins, cur.b, cur.e, TabGlobal{tab + (size_t)bg * P.nt}, hb, lnx, W, H1a,
-                                      H1b, nullptr, nullptr);
-      else
+      } else if (GL) {
+        // a u32 histogram in global memory: take a free slot (nscr >= resident waves)
+        uint32_t* lock = gscr + (size_t)nscr * P.nb2;
+        uint32_t slot = blockIdx.x % (uint32_t)nscr;
+        for (;;) {
+          uint32_t got = 1u;
+          if (lane == 0) got = atomicCAS(&lock[slot], 0u, 1u);
+          if (__builtin_amdgcn_readfirstlane(got) == 0u) break;
+          slot = slot + 1u == (uint32_t)nscr ? 0u : slot + 1u;
+        }
+        w = eval_exact<WAVE, false, R1>(P, bins, cur.b, cur.e, TabGlobal{tab + (size_t)bg * P.nt}, hb, lnx,
+                                        gscr + (size_t)slot * P.nb2, H1a, H1b, nullptr, nullptr);
+        __threadfence();   // the slot's words are clean again before it is released
+        if (lane == 0) atomicExch(&lock[slot], 0u);
+      } else {
         w = eval_exact<WAVE, P16, R1>(P, bins, cur.b, cur.e, TabLocal{tab + (size_t)bg * P.nt, LPl}, hb, lnx, W,
                                       H1a, H1b, nullptr, nullptr);
+      }
       if (lane == 0) atomicAdd(err_word + 1, 1u);   // statistics: windows that took the exact path
     } else {
       if (nan2) w.t2d = __builtin_nan("");

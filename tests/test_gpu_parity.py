@@ -370,6 +370,32 @@ def test_large_grid_kernels(monkeypatch, gw, n1p, n2p):
     pl.close()
 
 
+@pytest.mark.parametrize("n1p,n2p", [(50, 50), (100, 75)])
+def test_large_grid_u8_bins_wrap(n1p, n2p):
+    """k_scan_gw counts 2D bins in bytes: windows with >= 256 SNPs in one bin wrap a byte and are
+    re-evaluated exactly on global-memory histograms (many waves at once: every window of the
+    first chromosome wraps).  Records of fixed-bp and SNP-count windows against the oracle."""
+    from sfs2d import _lib as L
+    from sfs2d.engine import ScanConfig
+    from sfs2d.pack import PackedSNPs, pack_counts
+    from sfs2d.synth import synth_genome
+    p = synth_genome(3, [9000, 4000, 700], n1p, n2p, seed=77)
+    r1, a1 = (p.counts & 0xff).astype(np.int64), ((p.counts >> 8) & 0xff).astype(np.int64)
+    r2, a2 = ((p.counts >> 16) & 0xff).astype(np.int64), (p.counts >> 24).astype(np.int64)
+    same = np.zeros(p.n, bool)
+    same[: p.chrom_off[1]] = True                                   # chromosome 0: one 2D bin only
+    same[p.chrom_off[1]: p.chrom_off[1] + 1500] = np.arange(1500) % 3 != 0   # chromosome 1: 2 in 3
+    r1 = np.where(same, 2 * n1p - 1, r1); a1 = np.where(same, 1, a1)
+    r2 = np.where(same, 2 * n2p - 2, r2); a2 = np.where(same, 2, a2)
+    q = PackedSNPs(pack_counts(r1, a1, r2, a2), p.pos, p.chrom_off, p.chrom_names, p.ann_id, p.ann_names)
+    ocfg = O.Cfg(n1p, n2p)
+    bgs = O.chrom_backgrounds(q, ocfg)
+    for mode, ws in ((L.WINDOW_BP, 60000), (L.WINDOW_SNPS, 700)):
+        wins = O.snp_windows(q, ws)[0] if mode == L.WINDOW_SNPS else O.bp_windows(q, ws)
+        _records_vs_oracle(q, ScanConfig(n1p=n1p, n2p=n2p, window_mode=mode, window=ws), ocfg, wins,
+                           lambda c: bgs[c])
+
+
 def test_called_counts_above_sample_size_inside_long_tiles():
     """SNPs whose called allele count r + a exceeds 2 * pop_size without leaving the grid (no fold
     swap, so the 2D key is the alt count): the reference counts them; k_prep routes their steps
