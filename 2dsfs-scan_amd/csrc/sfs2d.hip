@@ -210,6 +210,8 @@ void plan_free(sfs2d_plan* p) {
     p->d_bcount = nullptr;
     if (p->sliced) {
       p->d_tab = nullptr; p->d_lp = nullptr; p->d_head = nullptr; p->d_leafsum = nullptr; p->d_bg1d = nullptr;
+    } else if (p->do_bg && p->G != WAVE) {
+      p->d_tab = nullptr; p->d_lp = nullptr; p->d_head = nullptr;
     }
   }
   hipFree(p->d_slot_base);
@@ -1222,8 +1224,9 @@ int sfs2d_plan_attach(sfs2d_plan* base, const sfs2d_params* prm, sfs2d_plan** ou
   sfs2d_ctx* ctx = base->ctx;
   *out = nullptr;
   if (base->base) return set_err(ctx, SFS2D_E_ARG, "attach to a base plan, not to an attached one");
-  if (!base->fused && !base->sliced)
-    return set_err(ctx, SFS2D_E_ARG, "attached plans need a per-chromosome-background base plan on the small-grid path");
+  const bool large = base->do_bg && base->G != WAVE;   // tables from the base's k_bg_slice (with its tail)
+  if (!base->fused && !base->sliced && !large)
+    return set_err(ctx, SFS2D_E_ARG, "attached plans need a per-chromosome-background base plan");
   const sfs2d_params& b = base->prm;
   if (prm->n1p != b.n1p || prm->n2p != b.n2p || (prm->fold != 0) != (b.fold != 0) || prm->bg_mode != b.bg_mode ||
       prm->ann_want != b.ann_want || prm->has_start != b.has_start || prm->has_end != b.has_end ||
@@ -1260,6 +1263,11 @@ int sfs2d_plan_attach(sfs2d_plan* base, const sfs2d_params* prm, sfs2d_plan** ou
     a->d_head = base->d_head;
     a->d_leafsum = base->d_leafsum;
     a->d_bg1d = base->d_bg1d;
+  } else if (large) {   // the base's finished per-chromosome tables
+    hipFree(a->d_tab); hipFree(a->d_lp); hipFree(a->d_head);
+    a->d_tab = base->d_tab;
+    a->d_lp = base->d_lp;
+    a->d_head = base->d_head;
   }
   a->base = base;
   a->fst_m = m;

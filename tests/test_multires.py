@@ -52,6 +52,22 @@ def test_matches_single_plans(seed):
         _same(res[f"{S}snps"], obj.scan_perChr_bySNPs(p, S))
 
 
+def test_large_grid_matches_single_plans():
+    """Attached plans on the large-grid path (101 x 101: k_scan_gw with its own exact-path slots)."""
+    from sfs2d.synth import synth_genome
+    p = synth_genome(3, [30000, 12000, 5000], 50, 50, seed=9)
+    obj = _obj(50, 50)
+    res = obj.multi_scan(p, [20000, 100000, 500000], [400], fst=True)
+    for ws in (20000, 100000, 500000):
+        _same(res[ws], obj.combined_scan(p, ws))
+        single = obj.window_fst(p, window_size=ws)
+        assert list(res["fst"][ws]) == list(single)
+        for k, v in single.items():
+            w = res["fst"][ws][k]
+            assert (v is None and w is None) or abs(w - v) <= 1e-9 * max(1.0, abs(v)), (ws, k, w, v)
+    _same(res["400snps"], obj.scan_perChr_bySNPs(p, 400))
+
+
 def test_repeated_runs_identical():
     from sfs2d import _lib as L
     from sfs2d.engine import Engine, ScanConfig
