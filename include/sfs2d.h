@@ -185,7 +185,7 @@ int sfs2d_plan_check(sfs2d_plan* plan);
 int sfs2d_plan_set_timing(sfs2d_plan* plan, int max_runs);   /* = sampled(plan, max_runs, 1) */
 int sfs2d_plan_set_timing_sampled(sfs2d_plan* plan, int max_samples, int every);
 /* average device time per kernel over the sampled runs (synchronises): k1 = k_prep, k2 = k_bg_slice
- * (0 when the plan does not launch it), k3 = the window scan kernel (k_scan_w / k_scan_g) */
+ * (0 when the plan does not launch it), k3 = the window scan kernel (k_scan_w / k_scan_gw / k_scan_g) */
 int sfs2d_plan_timing_read(sfs2d_plan* plan, int* nruns, double* ms_k1, double* ms_k2, double* ms_k3);
 /* standalone timing loop: average device time per kernel over `iters` runs */
 int sfs2d_plan_time(sfs2d_plan* plan, int iters, double* ms_per_run, double* ms_k1, double* ms_k2, double* ms_k3);
