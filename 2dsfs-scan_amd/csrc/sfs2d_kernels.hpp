@@ -58,7 +58,7 @@ constexpr int LNX_N = 1 << 20;    // ln(k) table for k < LNX_N (bin counts / win
 constexpr int LNT = 512;          // D(r) and x ln x tables staged in LDS by k_scan_w
 constexpr int RCPN = 512;         // (1/k, 1/(k(k-1))) for k < 512 (Fst: called allele counts ref + alt <= 510), after the LNT tables
 constexpr int REPL = 4;           // replicas of the per-chromosome background histograms
-constexpr int PW_MAX_LEAVES = 256;
+constexpr int PW_MAX_LEAVES = 1024;  // numpy pairwise leaves (64-128 values each): grids up to 255 x 255 (u8 counts)
 constexpr int LEAVES_PER_SLICE = 4;
 constexpr int FIN_LDS_BINS = 12288;  // backgrounds with nt <= this keep values / proportions in LDS
 constexpr int TRASH = WAVE;       // lane-private scratch words after each wave's histograms
@@ -862,7 +862,7 @@ __global__ __launch_bounds__(KBLOCK) void k_bg_slice(KParams P, uint32_t* __rest
   // tail == 0: no last-block combination -- the scan kernel combines the leaf sums itself (its
   // prologue), and bcount is a per-run parity buffer cleared by the scan kernel
   __shared__ double pv[4 * 128 + 8];
-  __shared__ double acc8[KBLOCK];
+  __shared__ double acc8[KBLOCK > 2 * PW_MAX_LEAVES ? KBLOCK : 2 * PW_MAX_LEAVES];   // (also the tail's leaf tree)
   __shared__ uint32_t u1[2 * 256 + 2];
   __shared__ double red[KBLOCK / WAVE][2];
   __shared__ int last_blk;

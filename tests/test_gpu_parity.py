@@ -396,6 +396,23 @@ def test_large_grid_u8_bins_wrap(n1p, n2p):
                            lambda c: bgs[c])
 
 
+@pytest.mark.parametrize("gw", ["0", "1"])
+def test_largest_grid(monkeypatch, gw):
+    """The largest grid the u8 allele counts allow (pop_size 127: 255 x 255 = 65,025 bins, 16-bit 2D
+    keys, 7-bit folded 1D keys): both large-grid kernels against the oracle."""
+    from sfs2d import _lib as L
+    from sfs2d.engine import ScanConfig
+    from sfs2d.synth import synth_genome
+    monkeypatch.setenv("SFS2D_GW", gw)
+    p = synth_genome(2, [5000, 1200], 127, 127, seed=127)
+    ocfg = O.Cfg(127, 127)
+    bgs = O.chrom_backgrounds(p, ocfg)
+    for mode, ws in ((L.WINDOW_BP, 50000), (L.WINDOW_SNPS, 300)):
+        wins = O.snp_windows(p, ws)[0] if mode == L.WINDOW_SNPS else O.bp_windows(p, ws)
+        _records_vs_oracle(p, ScanConfig(n1p=127, n2p=127, window_mode=mode, window=ws), ocfg, wins,
+                           lambda c: bgs[c])
+
+
 def test_called_counts_above_sample_size_inside_long_tiles():
     """SNPs whose called allele count r + a exceeds 2 * pop_size without leaving the grid (no fold
     swap, so the 2D key is the alt count): the reference counts them; k_prep routes their steps
