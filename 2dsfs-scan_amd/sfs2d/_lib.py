@@ -33,7 +33,8 @@ EXPORTS = [
     "sfs2d_plan_bg_buffer", "sfs2d_plan_run_phase", "sfs2d_plan_check", "sfs2d_plan_time",
     "sfs2d_plan_destroy", "sfs2d_scan", "sfs2d_plan_set_timing", "sfs2d_plan_timing_read",
     "sfs2d_plan_stats", "sfs2d_plan_grids", "sfs2d_plan_attach", "sfs2d_data_synth_sims",
-    "sfs2d_data_read",
+    "sfs2d_data_read", "sfs2d_dist_unique_id", "sfs2d_dist_create", "sfs2d_dist_scan_gather",
+    "sfs2d_dist_destroy",
 ]
 
 
@@ -107,6 +108,10 @@ def lib():
     L.sfs2d_plan_attach.argtypes = [vp, C.POINTER(Params), C.POINTER(vp)]
     L.sfs2d_data_synth_sims.argtypes = [vp, C.POINTER(SynthParams), vp, vp, i32, vp, i32, C.POINTER(vp)]
     L.sfs2d_data_read.argtypes = [vp, vp, vp, i64]
+    L.sfs2d_dist_unique_id.argtypes = [vp]
+    L.sfs2d_dist_create.argtypes = [vp, vp, i32, i32, C.POINTER(vp)]
+    L.sfs2d_dist_scan_gather.argtypes = [vp, vp, vp, vp, vp, vp, i64, i64, C.c_int, vp]
+    L.sfs2d_dist_destroy.argtypes = [vp]
     L.sfs2d_plan_timing_read.argtypes = [vp, C.POINTER(C.c_int)] + [C.POINTER(C.c_double)] * 3
     L.sfs2d_scan.argtypes = [vp, vp, C.POINTER(Params), vp, vp, vp, vp, i64, C.POINTER(i64)]
     _lib = L

@@ -78,6 +78,15 @@ class Engine:
     def upload(self, p: PackedSNPs) -> "DeviceData":
         return DeviceData(self, p)
 
+    def dist_unique_id(self) -> bytes:
+        """RCCL communicator id (rank 0 makes it, the caller broadcasts it): sfs2d_dist_unique_id."""
+        buf = (C.c_uint8 * 128)()
+        self.check(self.lib.sfs2d_dist_unique_id(buf))
+        return bytes(buf)
+
+    def dist(self, uid: bytes, rank: int, world: int) -> "Dist":
+        return Dist(self, uid, rank, world)
+
     def wrap_device(self, d_counts: int, d_pos: int, d_ann: Optional[int], n: int, chrom_off: np.ndarray,
                     chrom_last_pos: np.ndarray) -> "DeviceData":
         return DeviceData(self, None, (d_counts, d_pos, d_ann, n, chrom_off, chrom_last_pos))
@@ -256,6 +265,40 @@ class Plan:
                 self.base.attached.remove(self)
             self.eng.lib.sfs2d_plan_destroy(self.h)
             self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Dist:
+    """One rank's RCCL communicator in the native library (sfs2d_dist_*): back-to-back scans of a
+    plan, each all-gathering the fixed-stride window tables of every rank, enqueued
+    from C so that the host loop is not the bottleneck."""
+
+    def __init__(self, eng: Engine, uid: bytes, rank: int, world: int):
+        if len(uid) != 128:
+            raise ValueError("RCCL unique id must be 128 bytes")
+        self.eng = eng
+        h = C.c_void_p()
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        eng.check(eng.lib.sfs2d_dist_create(eng.h, buf, rank, world, C.byref(h)))
+        self.h = h
+
+    def scan_gather(self, plan: "Plan", outs, gathered, rows: int, first_step: int, nsteps: int,
+                    comm_stream: Optional[int]):
+        """outs / gathered: two device pointers each (rows x 64 B per rank / world x rows x 64 B);
+        comm_stream None: gathers serial on the library's stream."""
+        self.eng.check(self.eng.lib.sfs2d_dist_scan_gather(
+            self.h, plan.h, C.c_void_p(outs[0]), C.c_void_p(outs[1]), C.c_void_p(gathered[0]),
+            C.c_void_p(gathered[1]), rows, first_step, nsteps, C.c_void_p(comm_stream) if comm_stream else None))
+
+    def close(self):
+        if self.h:
+            self.eng.lib.sfs2d_dist_destroy(self.h)
+            self.h = None
 
     def __del__(self):
         try:

@@ -126,6 +126,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-hbm-stream", action="store_true")
+    ap.add_argument("--dist-loop", action="store_true",
+                    help="diagnostic: the N>1 step loop (scan + RCCL all-gather per step) even on one rank")
+    ap.add_argument("--py-loop", action="store_true", help="diagnostic: the Python N>1 step loop instead of the native one")
     args = ap.parse_args()
 
     import torch
@@ -135,8 +138,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    if world > 1:
+    dl = world > 1 or args.dist_loop   # the distributed step loop
+    if dl:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
         dist.init_process_group("nccl", rank=rank, world_size=world)
 
     from sfs2d import _lib as L
@@ -153,7 +158,7 @@ def main():
     pl = eng.plan(dev, ScanConfig(n1p=POP, n2p=POP, window=WS, fst=True))
     nrec = pl.nrec
     cdev = f"cuda:{local}"
-    if world > 1:
+    if dl:
         # shards differ in window count: tables are padded to the largest (unused rows flagged empty)
         c = torch.tensor([nrec], dtype=torch.int64, device=cdev)
         dist.all_reduce(c, op=dist.ReduceOp.MAX)
@@ -163,7 +168,23 @@ def main():
     outs = [torch.zeros((rows, 64), dtype=torch.uint8, device=cdev) for _ in range(2)]
     for o in outs:
         o[nrec:, 39] = 0x80   # padding rows: flags = SFS2D_W_EMPTY
-    gathered = [torch.empty((world * rows, 64), dtype=torch.uint8, device=cdev) for _ in range(2)] if world > 1 else None
+    gathered = [torch.empty((world * rows, 64), dtype=torch.uint8, device=cdev) for _ in range(2)] if dl else None
+    # the step loop runs in the native library (sfs2d_dist_scan_gather: its own RCCL communicator, the
+    # scans and all-gathers enqueued from C); the Python loop below is the fallback
+    nat = None
+    if dl:
+        hdr = torch.zeros(129, dtype=torch.uint8)
+        if rank == 0:
+            try:
+                hdr[1:] = torch.tensor(list(eng.dist_unique_id()), dtype=torch.uint8)
+                hdr[0] = 1
+            except Exception as e:  # noqa: BLE001
+                print(f"[bench] RCCL id unavailable ({e}): Python step loop", file=sys.stderr)
+        hdr = hdr.to(cdev)
+        dist.broadcast(hdr, 0)
+        hdr = hdr.cpu()
+        if int(hdr[0]) == 1 and not args.py_loop:
+            nat = eng.dist(bytes(hdr[1:].tolist()), rank, world)
     ev_scan = [torch.cuda.Event() for _ in range(2)]
     ev_comm = [torch.cuda.Event() for _ in range(2)]
     for e in ev_comm:
@@ -185,7 +206,27 @@ def main():
     out = outs[0]
     pl.run(out.data_ptr())
     pl.check()
-    if world > 1:
+    optrs = [o.data_ptr() for o in outs]
+    gptrs = [g.data_ptr() for g in gathered] if dl else None
+    gather_on = None
+    if nat is not None:
+        # the warmup times both gather placements (overlapped on the comm stream with events, or
+        # serial on the scan stream) and every rank keeps the faster by the max over ranks
+        def timed(cs, first, n):
+            torch.cuda.synchronize()
+            dist.barrier()
+            t = time.perf_counter()
+            nat.scan_gather(pl, optrs, gptrs, rows, first, n, cs)
+            torch.cuda.synchronize()
+            tt = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=cdev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            return float(tt.item())
+        wh = max(4, args.warmup // 2)
+        t_ov = timed(comm_s.cuda_stream, 0, wh)
+        t_se = timed(None, wh, wh)
+        gather_on = comm_s.cuda_stream if t_ov < t_se else None
+        first_timed = 2 * wh
+    elif dl:
         for i in range(args.warmup):
             step(i)
     else:
@@ -193,20 +234,22 @@ def main():
     # HIP events around each kernel of every 8th timed run, on the stream the kernels run on (sampled:
     # an event pair costs several microseconds of queue time, 1/8 of it is ~1 us per step)
     pl.set_timing(args.steps, every=8)
-    if world > 1:
+    if dl:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if world == 1:
+    if not dl:
         pl.run_many(args.steps, out.data_ptr())   # enqueued from C: no host work between steps
+    elif nat is not None:
+        nat.scan_gather(pl, optrs, gptrs, rows, first_timed, args.steps, gather_on)
     else:
         for i in range(args.steps):
             step(i)
     torch.cuda.synchronize()
-    if world > 1:
+    if dl:
         dist.barrier()
     dt = time.perf_counter() - t0
-    if world > 1:
+    if dl:
         t = torch.tensor([dt], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
@@ -237,7 +280,10 @@ def main():
                        "snps_per_gpu": p.n, "windows_per_gpu": nwin_rank, "window_bp": WS,
                        "stats": "T2D, T1D_p1, T1D_p2 (reference semantics) + Hudson Fst (DESIGN.md; not in the "
                                 "reference, parity vs its own oracle restatement)",
-                       "parallelism": f"windows sharded by chromosome over {world} GPU(s); RCCL all-gather"},
+                       "parallelism": f"windows sharded by chromosome over {world} GPU(s); RCCL all-gather"
+                                      + (f" per step ({'native' if nat is not None else 'Python'} step loop"
+                                         + ("" if nat is None else ", gathers " + ("overlapped on a comm stream" if gather_on else "serial on the scan stream"))
+                                         + ")" if dl else "")},
             "kernels_ms": {"k_prep": k1, "k_bg_slice": k2, "k_scan_w": k3, "timed_runs": nr,
                            "exact_path_windows": pl.stats()},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -256,9 +302,11 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(p)
         print(json.dumps(line), flush=True)
+    if nat is not None:
+        nat.close()
     pl.close()
     dev.close()
-    if world > 1:
+    if dl:
         dist.destroy_process_group()
 
 

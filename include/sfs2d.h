@@ -191,6 +191,25 @@ int sfs2d_plan_timing_read(sfs2d_plan* plan, int* nruns, double* ms_k1, double* 
 int sfs2d_plan_time(sfs2d_plan* plan, int iters, double* ms_per_run, double* ms_k1, double* ms_k2, double* ms_k3);
 int sfs2d_plan_destroy(sfs2d_plan* plan);
 
+/* ---- multi-GPU: one process per GPU, windows sharded by chromosome (sfs2d/dist.py), one RCCL
+ * all-gather of the fixed-stride window tables per scan (replaces the reference's
+ * single-process loop over every window, twoDSFS_class.py:787-991).  RCCL is loaded at the first
+ * call (dlopen librccl.so.1: the copy torch already loaded, else the ROCm one).
+ * sfs2d_dist_unique_id: rank 0 makes the 128-byte communicator id the caller broadcasts;
+ * sfs2d_dist_create: every rank joins (blocks until all `world` ranks have called it);
+ * sfs2d_dist_scan_gather: `nsteps` back-to-back scans of `plan`, step s writing its records into
+ * outs[s & 1] on the library stream, then all-gathering `rows` 64-B records from every rank into
+ * gathered[s & 1] on `comm_stream` while the next step scans (the scan of step s + 2 waits for the
+ * gather of step s); comm_stream NULL: each gather follows its scan on the library's stream (no
+ * cross-stream events).  Steps are numbered from `first_step`.  Enqueue only: synchronise the
+ * streams to wait; synchronise before switching between the two modes. */
+typedef struct sfs2d_dist sfs2d_dist;
+int sfs2d_dist_unique_id(uint8_t* id128);
+int sfs2d_dist_create(sfs2d_ctx* ctx, const uint8_t* id128, int rank, int world, sfs2d_dist** out);
+int sfs2d_dist_scan_gather(sfs2d_dist* d, sfs2d_plan* plan, void* out0, void* out1, void* gathered0,
+                           void* gathered1, int64_t rows, int64_t first_step, int nsteps, void* comm_stream);
+int sfs2d_dist_destroy(sfs2d_dist* d);
+
 /* one-shot convenience: plan + run + read (+ supplied background when bg2d != NULL) */
 int sfs2d_scan(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* params, const double* bg2d,
                const double* bg1a, const double* bg1b, sfs2d_window* out_host, int64_t cap, int64_t* nrec_out);

@@ -1,0 +1,44 @@
+"""The native multi-GPU step loop (sfs2d_dist_*, include/sfs2d.h): RCCL loaded at run time, one
+communicator per rank, scans and all-gathers of the window tables enqueued from C.  On the one-GPU
+box: a one-rank communicator (the gather is a copy) -- the tables gathered after back-to-back
+steps equal the plan's own records.  N > 1 runs are the driver's (bench.py --gpus N)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_single_rank_scan_gather():
+    import torch
+    from sfs2d import _lib as L
+    from sfs2d.engine import Engine, ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(2, [30000, 9000], 25, 25, seed=21)
+    eng = Engine.get(0)
+    dev = eng.upload(p)
+    pl = eng.plan(dev, ScanConfig(n1p=25, n2p=25, window=20000, fst=True))
+    pl.run()
+    pl.check()
+    ref = pl.read()
+    rows = pl.nrec + 3   # padded like bench.py's shards
+    outs = [torch.zeros((rows, 64), dtype=torch.uint8, device="cuda:0") for _ in range(2)]
+    gath = [torch.full((rows, 64), 7, dtype=torch.uint8, device="cuda:0") for _ in range(2)]
+    comm = torch.cuda.Stream(device=0)
+    d = eng.dist(eng.dist_unique_id(), 0, 1)
+    try:
+        for first, n, cs in ((0, 5, comm.cuda_stream), (5, 4, None)):   # overlapped gathers, then serial
+            for g in gath:
+                g.fill_(7)
+            d.scan_gather(pl, [o.data_ptr() for o in outs], [g.data_ptr() for g in gath], rows, first, n, cs)
+            torch.cuda.synchronize()
+            pl.check()
+            for o, g in zip(outs, gath):
+                assert torch.equal(o, g)
+                recs = np.frombuffer(o[: pl.nrec].cpu().numpy().tobytes(), dtype=L.WINDOW_DTYPE)
+                assert recs.tobytes() == ref.tobytes()
+        with pytest.raises(L.Sfs2dError):   # rows must cover the plan's records
+            d.scan_gather(pl, [o.data_ptr() for o in outs], [g.data_ptr() for g in gath], pl.nrec - 1, 0, 1,
+                          comm.cuda_stream)
+    finally:
+        d.close()
+        pl.close()
