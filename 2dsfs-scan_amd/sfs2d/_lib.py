@@ -75,6 +75,14 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise Sfs2dError(E_ARG, f"HIP library not built: {os.path.abspath(LIB_PATH)} missing "
                                 "(run __graft_entry__.build() or make -C 2dsfs-scan_amd/csrc)")
+    # one HIP runtime per process: torch's wheel bundles libamdhip64 (soname libamdhip64.so.7, which
+    # torch itself needs as "libamdhip64.so"); if this library loaded /opt/rocm's copy first, a later
+    # torch import would bring a second runtime that finds no GPU.  Loaded after torch, this
+    # library's libamdhip64.so.7 resolves to torch's copy.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(os.path.abspath(LIB_PATH))
     vp, i32, i64, u32p = C.c_void_p, C.c_int32, C.c_int64, C.POINTER(C.c_uint32)
     L.sfs2d_abi_version.restype = C.c_int
