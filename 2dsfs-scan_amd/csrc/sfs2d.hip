@@ -876,7 +876,12 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
         pl->tiles.push_back(t);
       }
   }
-  pl->hr = (size_t)K.nh * 4 * 4 <= 64 * 1024 ? 4 : 1;
+  // one LDS copy per histogram word: four interleaved copies (lane & 3, fewer same-address atomics)
+  // cost more in zeroing and flushing than they saved (k_prep config 2 10.3 vs 10.9 us, config 3
+  // 183 vs 187 us); SFS2D_HR=4 restores them where they fit
+  pl->hr = 1;
+  if (const char* ev = std::getenv("SFS2D_HR"))
+    if (ev[0] == '4' && (size_t)K.nh * 4 * 4 <= 64 * 1024) pl->hr = 4;
   pl->bg_lds = ((size_t)K.nh * pl->hr + WAVE) * 4;   // + 64 lane trash words
   pl->lds_hist = pl->bg_lds <= 150 * 1024;
   if (pl->lds_hist && pl->bg_lds > 64 * 1024) {
