@@ -906,8 +906,10 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   pl->nnodes = (int)pw.nodes.size();
   pl->nlevels = pw.nlevels;
   if (pl->nleaves > PW_MAX_LEAVES) { delete pl; return set_err(ctx, SFS2D_E_ARG, "grid too large for the pairwise plan"); }
-  for (int j = 0; j < pl->nleaves; j += LEAVES_PER_SLICE) {
-    const int jl = std::min(pl->nleaves, j + LEAVES_PER_SLICE);
+  int lps = LEAVES_PER_SLICE;
+  if (const char* ev = std::getenv("SFS2D_LPS")) lps = std::max(1, std::min(LEAVES_PER_SLICE, std::atoi(ev)));   // tuning
+  for (int j = 0; j < pl->nleaves; j += lps) {
+    const int jl = std::min(pl->nleaves, j + lps);
     const int kb = j == 0 ? 0 : 1 + pw.leaves[j].x;
     const int ke = jl == pl->nleaves ? K.nb2 : 1 + pw.leaves[jl].x;
     pl->slices.push_back(make_int4(kb, ke, j, jl));
