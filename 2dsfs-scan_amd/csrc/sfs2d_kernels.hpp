@@ -872,8 +872,15 @@ __global__ __launch_bounds__(KBLOCK) void k_bg_slice(KParams P, uint32_t* __rest
   const int lane = tid & (WAVE - 1);
   if (s > nslices) {   // the extra workgroups (background 0's row only): Fst per window, using the
                        // GPU while this kernel's table blocks wait on memory
-    if (b == 0) fst_windows(counts, bins, slots, rt, fst_out, nslots, (uint32_t)(s - nslices - 1) * (KBLOCK / WAVE) + (tid >> 6),
-                            (uint32_t)nfst * (KBLOCK / WAVE));
+    if (b == 0) {
+      // the (1/n, 1/(n(n-1))) table in LDS (acc8 is free here): its look-ups follow each SNP's count
+      // load, and L2 round trips there were on the window's critical path
+      double2* rl = reinterpret_cast<double2*>(acc8);
+      for (int k = tid; k < RCPN; k += KBLOCK) rl[k] = rt[k];
+      __syncthreads();
+      fst_windows(counts, bins, slots, rl, fst_out, nslots, (uint32_t)(s - nslices - 1) * (KBLOCK / WAVE) + (tid >> 6),
+                  (uint32_t)nfst * (KBLOCK / WAVE));
+    }
     return;
   }
   const size_t rstride = (size_t)P.nchrom * P.nh;
