@@ -775,7 +775,10 @@ __device__ __forceinline__ void fst_windows(const uint32_t* __restrict__ counts,
 __global__ __launch_bounds__(256) void k_fst_win(const uint32_t* __restrict__ counts, const uint32_t* __restrict__ bins,
                                                  const uint2* __restrict__ slots, const double2* __restrict__ rt,
                                                  double* __restrict__ fst_out, uint32_t nslots) {
-  fst_windows(counts, bins, slots, rt, fst_out, nslots, blockIdx.x * 4u + (threadIdx.x >> 6), gridDim.x * 4u);
+  __shared__ double2 rl[RCPN];   // the (1/n, 1/(n(n-1))) table in LDS, as in k_bg_slice's Fst workgroups
+  for (int k = threadIdx.x; k < RCPN; k += 256) rl[k] = rt[k];
+  __syncthreads();
+  fst_windows(counts, bins, slots, rl, fst_out, nslots, blockIdx.x * 4u + (threadIdx.x >> 6), gridDim.x * 4u);
 }
 
 // ------------------------------------------------------------------------------------------ K2
