@@ -180,6 +180,15 @@ __device__ unsigned long long g_wv[4096 * 8][2];   // k_scan_w per wavefront: en
   } while (0)
 #endif
 
+// Diagnostic build only (-DSFS2D_MARK): assembly comments delimiting regions of the scan loop
+#ifdef SFS2D_MARK
+#define MARK(n) asm volatile("; MARK " #n)
+#else
+#define MARK(n) \
+  do {          \
+  } while (0)
+#endif
+
 // ------------------------------------------------------------------------------------------ helpers
 
 __device__ __forceinline__ uint32_t wid_of(uint32_t p, uint32_t ws) { return p ? (p - 1u) / ws : 0u; }
@@ -197,8 +206,12 @@ __device__ __forceinline__ uint32_t div_fast(const KParams& P, uint32_t n) {
   return (t + ((n - t) >> P.wsh1)) >> P.wsh2;
 }
 
+// ln x for counts past the table (>= 2^20 SNPs in one bin): out of line, so that log's constants
+// are not kept in registers across the loops that can reach it
+__device__ __noinline__ double log_u32(uint32_t x) { return log((double)x); }
+
 __device__ __forceinline__ double lnx_of(const double* lnx, uint32_t x) {
-  return x < (uint32_t)LNX_N ? lnx[x] : log((double)x);
+  return x < (uint32_t)LNX_N ? lnx[x] : log_u32(x);
 }
 
 __device__ __forceinline__ double wave_sum_d(double v) {
@@ -1918,10 +1931,534 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
   BLK_STAMP(1, 1);
 }
 
+// fp64 wave sums on the DPP path without update_dpp's old-value copies (every lane of these
+// patterns has a source lane); the rounding order of wave_sum_dpp / wave_sum_dpp_halves
+template <int CTRL>
+__device__ __forceinline__ double mdpp_d(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(u & 0xffffffffull), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double((long long)(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+__device__ __forceinline__ void wave_sum2_halves(double a, double b, double& s2, double& sa, double& sb) {
+  a += mdpp_d<0xB1>(a);  b += mdpp_d<0xB1>(b);
+  a += mdpp_d<0x4E>(a);  b += mdpp_d<0x4E>(b);
+  a += mdpp_d<0x141>(a); b += mdpp_d<0x141>(b);
+  a += mdpp_d<0x140>(a); b += mdpp_d<0x140>(b);
+  s2 = (readlane_d(a, 0) + readlane_d(a, 16)) + (readlane_d(a, 32) + readlane_d(a, 48));
+  sa = readlane_d(b, 0) + readlane_d(b, 16);
+  sb = readlane_d(b, 32) + readlane_d(b, 48);
+}
+__device__ __forceinline__ double wave_sum1(double v) {
+  v += mdpp_d<0xB1>(v);
+  v += mdpp_d<0x4E>(v);
+  v += mdpp_d<0x141>(v);
+  v += mdpp_d<0x140>(v);
+  return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+}
+
+// fp64 wave sums replicated in every lane: the row sums by DPP, then across rows and halves by the
+// gfx950 lane swaps (v_permlane16_swap / v_permlane32_swap); a fixed tree, so deterministic
+__device__ __forceinline__ double swap16_d(double v, bool upper) {
+  const unsigned long long u = __double_as_longlong(v);
+  const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)(u & 0xffffffffull), (uint32_t)(u & 0xffffffffull), false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32), false, false);
+  const uint32_t l = upper ? lo[1] : lo[0], h = upper ? hi[1] : hi[0];
+  return __longlong_as_double((long long)(((unsigned long long)h << 32) | l));
+}
+__device__ __forceinline__ double swap32_d(double v, bool upper) {
+  const unsigned long long u = __double_as_longlong(v);
+  const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)(u & 0xffffffffull), (uint32_t)(u & 0xffffffffull), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32), false, false);
+  const uint32_t l = upper ? lo[1] : lo[0], h = upper ? hi[1] : hi[0];
+  return __longlong_as_double((long long)(((unsigned long long)h << 32) | l));
+}
+// row (16-lane) sums in every lane of the row
+__device__ __forceinline__ double row_sum_d(double v) {
+  v += mdpp_d<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += mdpp_d<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += mdpp_d<0x141>(v);   // row_half_mirror
+  v += mdpp_d<0x140>(v);   // row_mirror
+  return v;
+}
+// (permlane16_swap(v, v): result 0 holds the even rows' values in both rows of a pair, result 1 the odd
+// rows'; permlane32_swap(v, v): result 0 the lower half's in both halves, result 1 the upper half's)
+__device__ __forceinline__ double wave_sum_all(double v) {
+  v = row_sum_d(v);
+  v = swap16_d(v, false) + swap16_d(v, true);
+  return swap32_d(v, false) + swap32_d(v, true);
+}
+// sums of lanes 0-31 (a) and 32-63 (b), both in every lane
+__device__ __forceinline__ void wave_sum_halves_all(double v, double& a, double& b) {
+  v = row_sum_d(v);
+  v = swap16_d(v, false) + swap16_d(v, true);
+  a = swap32_d(v, false);
+  b = swap32_d(v, true);
+}
+
+// v_writelane_b32 (the LLVM intrinsic: this clang has no builtin for it): lane l (uniform) of `old`
+// takes the uniform value v; the compiler puts the lane select in M0
+extern "C" __device__ int sfs2d_llvm_writelane(int v, int l, int old) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ uint32_t wlane(uint32_t v, int l, uint32_t old) {
+  return (uint32_t)sfs2d_llvm_writelane((int)__builtin_amdgcn_readfirstlane((int)v), l, (int)old);
+}
+
+
+// dst[0, n) = src[0, n) into LDS by the whole workgroup, eight 8-B loads of a thread in flight at once
+__device__ __forceinline__ void lds_copy_d(double* dst, const double* __restrict__ src, int n) {
+  constexpr int U = 8;
+  for (int k0 = threadIdx.x; k0 < n; k0 += U * SBLOCK) {
+    double v[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) v[j] = k0 + j * SBLOCK < n ? src[k0 + j * SBLOCK] : 0.0;
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (k0 + j * SBLOCK < n) dst[k0 + j * SBLOCK] = v[j];
+  }
+}
+
+// K3 for small grids (nb2 <= 8192: the background table in LDS).  Workgroup: 8 wavefronts sharing
+// one chromosome's table (prologue: copied from k_bg_slice's output and finished -- "sliced" -- or
+// built from this run's replicas -- "fused"); each wavefront scans one window at a time: a static
+// first window, then windows from the chromosome's pool counters (the atomic one window ahead of
+// its use), the next window's slot record and first 8 rows of bins in flight while the current one
+// is finished.  Per window only the per-SNP work and the wave sums run; what is wave-uniform -- the
+// T values, the zero / NaN rules, the Fst value, the 64-B record -- is evaluated per lane for a
+// batch of windows at once (flush), the rare exact re-evaluations included.  (Measured on config 3:
+// the loop is VALU-issue and LDS-latency bound at 4 waves per SIMD; the batched finish took it from
+// 405 to ~330 VALU instructions per window.)
+template <bool P16, bool FUSED, bool FST>
+__device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
+  constexpr int NWV = SBLOCK / WAVE;
+  constexpr int SB = 4;    // windows per batch (see flush; LDS-limited)
+  __shared__ BgHead sh_hb;
+  __shared__ double sh_bd[NWV][3][SB];      // batch: the three sums of window j
+  __shared__ uint32_t sh_bu[NWV][5][SB];    // batch: slot, begin, n2 | n2_all, n1a | n1b, nsnp | nvar
+  __shared__ unsigned long long sh_bf[NWV][FST ? 2 : 1][SB];   // batch (FST): k_prep's Fst sums of the slot
+  STAMP(10);
+  BLK_STAMP(1, 0);
+  const int tid = threadIdx.x;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & (WAVE - 1);
+  const Chunk ch = chunks[blockIdx.x];
+  const int bg = bg_per_chrom ? (int)ch.chrom : 0;
+
+  // LDS: lp table (nt, rounded up to even: the histograms are 16-B aligned) | D | F | histograms
+  double* LPl = ldsd;
+  double* Dt = LPl + ((P.nt + 1) & ~1);   // LNT
+  double* Ft = Dt + LNT;                  // LNT
+  uint32_t* HB = reinterpret_cast<uint32_t*>(Ft + LNT);
+  const int h2w = P16 ? ((P.nb2 + 1) / 2 + 3) & ~3 : (P.nb2 + 3) & ~3;
+  const int h1w = R1 * (P.n1p + 1), h1wb = R1 * (P.n2p + 1);
+  const int per = h2w + h1w + h1wb + TRASH;
+  uint32_t* W = HB + wv * per;
+  uint32_t* H1a = W + h2w;
+  uint32_t* H1b = H1a + h1w;
+  const uint32_t rep = lane & (R1 - 1);
+
+  auto bounds = [&](uint32_t s, uint2 sr, Win& w) {
+    if (mode_bp) {
+      w.has = sr.x != 0u;
+      w.b = sr.x - 1u;
+      w.e = sr.y;
+    } else {
+      w.has = true;
+      w.b = ch.cb + (ch.wid_lo + (s - ch.slot_lo)) * P.ws;
+      w.e = w.b + P.ws;
+    }
+    if (w.has) {   // the bins buffer has SCAN_PAD readable words past n; masked in the last step
+      const uint32_t* q = bins + w.b + lane;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w.u[j] = q[64 * j];
+    }
+  };
+  // window schedule: one static window per wavefront, then the chromosome's pool counters (an
+  // atomic is always one window ahead of its use, so its latency hides under a window's work)
+  uint32_t s = ch.slot_lo + ch.first + wv;
+  const bool active = s < ch.slot_hi;
+  const uint2 sr0 = (active && mode_bp) ? slots[s] : make_uint2(0, 0);   // in flight during the table work
+  const uint32_t npool = ch.pool & 0xffffu, pool = ch.pool >> 16;
+  const bool dyn = ch.slot_lo + ch.nstatic < ch.slot_hi;
+  const uint32_t dbase = ch.slot_lo + ch.nstatic + pool;
+  uint32_t* myctr = ctr + (((size_t)cpar * P.nchrom + ch.chrom) * CTR_POOLS + pool) * CTR_STRIDE;
+  uint32_t gq = 0;
+  if (active && dyn && lane == 0) gq = atomicAdd(myctr, 1u);
+  if (blockIdx.x == 0)   // the other parity's counters, for the next run
+    for (int k = tid; k < P.nchrom * CTR_POOLS; k += SBLOCK) ctr[((size_t)(1 - cpar) * P.nchrom * CTR_POOLS + k) * CTR_STRIDE] = 0u;
+
+  // table copies with every load of a thread in flight at once (a load-wait-store loop paid one
+  // L2/MALL round trip per element: ~4 us of config 2's ~10)
+  lds_copy_d(Dt, dfg, 2 * LNT);
+  BgHead hb;
+  const size_t rs = (size_t)P.nchrom * P.nh;     // replica stride
+  const uint32_t* Rc = repl + (size_t)par * REPL * rs + (size_t)ch.chrom * P.nh;
+  if (!FUSED) {
+    lds_copy_d(LPl, LPg + (size_t)bg * P.nt, P.nt);
+    if (sliced) {
+      // this run's per-chromosome table from k_bg_slice (proportions, logs, 1D part final) and its
+      // leaf sums: numpy's tree over the leaves, then scipy's p[-1] rule on the 2D table -- the
+      // combination k_bg_slice's last block would do, here in every workgroup (no grid-wide
+      // completion step between the kernels).  Scratch: the histogram area (zeroed below).
+      const bool writer = ch.first == 0 && (int)ch.chrom == write_chrom;
+      double* lsum = reinterpret_cast<double*>(HB);
+      if (tid < nleaves) lsum[tid] = leafsum[(size_t)bg * nleaves + tid];
+      const int4 my_node = tid < nnodes ? nodes[tid] : make_int4(0, 0, -1, 0);
+      __syncthreads();
+      for (int l = 0; l < nlevels; ++l) {
+        if (my_node.z == l) lsum[nleaves + tid] = lsum[my_node.x] + lsum[my_node.y];
+        __syncthreads();
+      }
+      if (tid == 0) {
+        const double B2 = (double)bcount[(size_t)par * P.nchrom + bg];
+        const Bg1D o = bg1d[bg];
+        uint32_t flags = o.flags;
+        if (B2 == 0.0) flags |= BGF_B2_ZERO;
+        const int M2 = P.nb2 - 2;
+        if (M2 >= 1 && B2 != 0.0) {
+          const double S = (nleaves + nnodes) ? lsum[nleaves + nnodes - 1] : 0.0;
+          const double padj = 1.0 - S;
+          if (padj < -1e-15) {
+            flags |= BGF_NAN2;
+          } else if (fabs(padj) > 1e-15) {
+            const double l2 = log(padj);
+            LPl[M2] = l2;
+            if (writer) { tab[(size_t)bg * P.nt + M2].lp = l2; LPg[(size_t)bg * P.nt + M2] = l2; }
+          }
+        }
+        BgHead h;
+        h.B2 = B2; h.B1a = o.B1a; h.B1b = o.B1b; h.flags = flags; h.pad = 0;
+        sh_hb = h;
+        if (writer) head[bg] = h;
+      }
+      if (blockIdx.x == 0)   // the other parity's inner sums, for the next run
+        for (int c = tid; c < P.nchrom; c += SBLOCK) bcount[(size_t)(1 - par) * P.nchrom + c] = 0u;
+      __syncthreads();
+      hb = sh_hb;
+    } else {
+      hb = head[bg];
+    }
+  } else {
+    fused_table(P.nb2, P.nh, P.nt, P.n1p, P.n2p, P.n1, P.n2, P.t1a, P.t1b, P.nchrom, ch.chrom,
+                ch.first == 0 && (int)ch.chrom == write_chrom, bg,
+                Rc, rs, repl, bcount, par, tab, LPg, head, LPl, HB, leaves, nleaves, nodes, nnodes, nlevels, lnx,
+                &sh_hb);
+    hb = sh_hb;
+  }
+  for (int k = lane; k < per / 4; k += WAVE) reinterpret_cast<uint4*>(W)[k] = make_uint4(0, 0, 0, 0);
+  if (tid == 0) LPl[0] = 0.0;   // bin 0 ((0,0), never counted): SNPs outside the 2D SFS read it and add 0
+  __syncthreads();
+  if (FUSED) {
+    // the other parity's replicas and inner sums: zeroed for the next run, a slice per workgroup
+    // (after the last barrier: nothing waits for these stores)
+    uint32_t* Ro = repl + (size_t)(1 - par) * REPL * rs;
+    const size_t tot = (size_t)REPL * rs, share = (tot + gridDim.x - 1) / gridDim.x;
+    const size_t lo = (size_t)blockIdx.x * share, hi = lo + share < tot ? lo + share : tot;
+    for (size_t k = lo + tid; k < hi; k += SBLOCK) Ro[k] = 0u;
+    if (blockIdx.x == 0)
+      for (int c = tid; c < P.nchrom; c += SBLOCK) bcount[(size_t)(1 - par) * P.nchrom + c] = 0u;
+  }
+  if (!active) return;
+  const bool filt = P.ann_want >= 0;
+  const bool half1d = P.n1p <= 33 && P.n2p <= 33;
+  const uint32_t zflags = bg_zero_flags(hb);
+  const bool nan2 = hb.flags & BGF_NAN2, nan1a = hb.flags & BGF_NAN1A, nan1b = hb.flags & BGF_NAN1B;
+  uint32_t* const H1a_l = H1a + rep;   // this lane's replica column of the 1D histograms
+  uint32_t* const H1b_l = H1b + rep;
+  const uint32_t trash = (uint32_t)(h2w + h1w + h1wb + lane);   // the lane's trash word (index from W)
+  uint32_t* const T_l = W + trash;
+  const uint32_t one1 = P16 ? 0x10000u : 1u;   // 1D increment (P16: upper halves, see the window loop)
+  // ---- batched finish.  Lane j of the B* registers holds the j-th window this wavefront has
+  // scanned since the last flush (slot, SNP range, counts, the three sums); per window only the
+  // sums' wave reductions run, and the T values, the zero / NaN rules, the Fst value and the 64-B
+  // record of up to 64 windows are computed per lane, in one pass (flush)
+  uint32_t jb = 0;
+  auto flush = [&]() {
+    MARK(30);
+    // (the lane id and the batch addresses recomputed here: kept live across the window loop they
+    // were spilled, and their scratch reloads put an L2 round trip in front of every flush)
+    uint32_t ln = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    asm volatile("" : "+v"(ln));
+    const bool mine = ln < jb;
+    const int jl = ln & (SB - 1);
+    const double B2 = sh_bd[wv][0][jl], Ba = sh_bd[wv][1][jl], Bb = sh_bd[wv][2][jl];
+    const uint32_t Bs = sh_bu[wv][0][jl], Bsb = sh_bu[wv][1][jl], Bn2 = sh_bu[wv][2][jl], Bn1 = sh_bu[wv][3][jl],
+                   Bnv = sh_bu[wv][4][jl];
+    const uint32_t nsnp = Bnv & 0xffffu;
+    const bool empty = nsnp == 0u;   // a slot with no SNP
+    const uint32_t wid = ch.wid_lo + (Bs - ch.slot_lo);
+    const uint32_t Bse = Bsb + nsnp;
+    WinOut w;
+    w.snp_count = Bnv >> 16; w.n2 = Bn2 & 0xffffu; w.n2_all = Bn2 >> 16; w.n1a = Bn1 & 0xffffu; w.n1b = Bn1 >> 16;
+    w.t2d = 2.0 * (B2 - xlnx(w.n2, Ft, lnx));
+    w.t1a = 2.0 * (Ba - xlnx(w.n1a, Ft, lnx));
+    w.t1b = 2.0 * (Bb - xlnx(w.n1b, Ft, lnx));
+    // |T| this small may be an exactly proportional window: the exact evaluation below
+    const bool exact = mine && !empty &&
+                       (nsnp == 0xffffu || suspect_zero(w.t2d, w.n2) || suspect_zero(w.t1a, w.n1a) ||
+                        suspect_zero(w.t1b, w.n1b));
+    if (nan2) w.t2d = __builtin_nan("");
+    if (nan1a) w.t1a = __builtin_nan("");
+    if (nan1b) w.t1b = __builtin_nan("");
+    if (empty) { w.t2d = 0.0; w.t1a = 0.0; w.t1b = 0.0; }   // (counts 0: write_empty's record)
+    if (mine && !exact)
+      write_rec(out + Bs, ch.chrom, wid, empty ? 0u : Bsb, empty ? 0u : Bse, w, empty ? SFS2D_W_EMPTY : zflags);
+    if (mine) {
+      if (FST) {   // k_prep's fixed-point sums of the slot (read in the window), cleared for the next run
+        const long long fx = (long long)sh_bf[wv][0][jl], fy = (long long)sh_bf[wv][FST ? 1 : 0][jl];
+        fst_out[Bs] = fy != 0 ? (double)fx / (double)fy : __builtin_nan("");
+        reinterpret_cast<ulonglong2*>(fsum)[Bs] = make_ulonglong2(0ull, 0ull);
+      }
+      if (mode_bp) {   // the slot table is left clean for the next run
+        uint32_t z = 0u;
+        asm volatile("" : "+v"(z));   // (a literal 0 here was taken from a spilled register)
+        slots[Bs] = make_uint2(z, z);
+      }
+    }
+    MARK(31);
+    // rare: exact re-evaluation with the bin-by-bin proportionality test (the histograms are clean)
+    for (unsigned long long m = __ballot(exact); m; m &= m - 1) {
+      const int l = __builtin_ctzll(m);
+      const uint32_t xs = __builtin_amdgcn_readlane(Bs, l), xb = __builtin_amdgcn_readlane(Bsb, l);
+      // (a saturated size: the window's end from its slot record, still in place)
+      const uint32_t xn = __builtin_amdgcn_readlane(Bnv, l) & 0xffffu;
+      const uint32_t xe = xn != 0xffffu ? xb + xn : (mode_bp ? slots[xs].y : xb + P.ws);
+      WinOut x;
+      if (FUSED)
+        x = eval_exact<WAVE, P16, R1>(P, bins, xb, xe,
+                                      TabFused{LPl, Rc, rs, P.nb2, P.n1, P.n2, P.n1p, P.h1a, P.h1b, P.t1a, P.t1b}, hb,
+                                      lnx, W, H1a, H1b, nullptr, nullptr);
+      else
+        x = eval_exact<WAVE, P16, R1>(P, bins, xb, xe, TabLocal{tab + (size_t)bg * P.nt, LPl}, hb, lnx, W, H1a, H1b,
+                                      nullptr, nullptr);
+      if (lane == 0) {
+        write_rec(out + xs, ch.chrom, ch.wid_lo + (xs - ch.slot_lo), xb, xe, x, zflags);
+        atomicAdd(err_word + 1, 1u);   // statistics: windows that took the exact path
+      }
+      group_sync<WAVE>();
+    }
+    jb = 0;
+  };
+  // window jb of the batch (lane 0 stores it; the values are wave-uniform)
+  auto put = [&](uint32_t slot, uint32_t b, uint32_t nsnp, uint32_t n2, uint32_t n1a, uint32_t n1b, uint32_t nvar,
+                 uint32_t nlast, double s2, double sa, double sb, ulonglong2 fq) {
+    if (lane == 0) {
+      sh_bd[wv][0][jb] = s2; sh_bd[wv][1][jb] = sa; sh_bd[wv][2][jb] = sb;
+      if (FST) { sh_bf[wv][0][jb] = fq.x; sh_bf[wv][FST ? 1 : 0][jb] = fq.y; }
+      sh_bu[wv][0][jb] = slot;
+      sh_bu[wv][1][jb] = b;
+      sh_bu[wv][2][jb] = min(n2, 0xffffu) | (min(n2 + nlast, 0xffffu) << 16);
+      sh_bu[wv][3][jb] = min(n1a, 0xffffu) | (min(n1b, 0xffffu) << 16);
+      sh_bu[wv][4][jb] = min(nsnp, 0xffffu) | (min(nvar, 0xffffu) << 16);
+    }
+  };
+
+
+  Win cur;
+  bounds(s, sr0, cur);
+  STAMP(11);
+  int it = 0;
+  uint32_t sn = ch.slot_hi;
+  uint2 srn = make_uint2(0, 0);
+  for (;;) {
+  while (s < ch.slot_hi) {
+    // the batch's last window prefetches nothing: the flush after it (with the rare exact
+    // evaluations) then runs with no rows in flight and no row registers live
+    const bool fill = jb + 1u < (uint32_t)SB;
+    sn = ch.slot_hi;
+    if (dyn) {
+      const uint32_t j = __builtin_amdgcn_readfirstlane(gq);
+      sn = dbase + npool * j < ch.slot_hi ? dbase + npool * j : ch.slot_hi;
+      if (sn < ch.slot_hi && lane == 0) gq = atomicAdd(myctr, 1u);
+    }
+    const bool more = sn < ch.slot_hi;
+    srn = (mode_bp && more) ? slots[sn] : make_uint2(0, 0);
+    if (!cur.has) {
+      put(s, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0.0, 0.0, 0.0, make_ulonglong2(0ull, 0ull));   // (no SNP: no Fst sums)
+      ++jb;
+      Win nxt;
+      nxt.has = false;
+      if (more && fill) bounds(sn, srn, nxt);
+      cur = nxt;
+      s = sn;
+      if (!fill) break;
+      continue;
+    }
+    // SNP j of this lane is b + lane + 64 j: rows of 64 SNPs in pairs, the first 8 rows from the
+    // prefetched registers (a row wholly past e is skipped; SNPs past e are w = 0, outside every
+    // spectrum).  Per SNP: the 2D LDS atomic (u16 halves) returns the SNP's rank r in its bin and the
+    // SNP adds D(r) - lp_k (telescoping: sum_k x_k ln x_k = sum_i D(r_i)); the folded 1D bins are
+    // counted in lane & 3 replicas.  An SNP outside a spectrum adds to the lane's own trash word
+    // (shared words instead -- bin (0,0), the folded bin 0 -- cost 60% more LDS bank-conflict cycles):
+    // 0 for the 2D spectrum, so the word's low half stays 0 and gives rank 0, D(0) = 0, LPl[0] = 0;
+    // 0x10000 for the 1D spectra, whose counts live in the upper u16 halves.  Counts are wave-uniform
+    // ballot counts.
+    const uint32_t nsnp = cur.e - cur.b;
+    const int lim = (int)nsnp - lane;
+    const bool clampd = nsnp > (uint32_t)(LNT - 1);   // some rank may pass the D table
+    double acc2 = 0.0;
+    uint32_t n2 = 0, n1a = 0, n1b = 0, nlast = 0, nvar = 0;
+    uint32_t kw[8];   // the 2D words of the first 8 rows, cleared after the window
+    auto pair = [&](uint32_t w0, uint32_t w1, int j, bool keep) {
+      if (64 * (j + 2) > (int)nsnp) {   // the window's last rows
+        w0 = 64 * j < lim ? w0 : 0u;
+        w1 = 64 * (j + 1) < lim ? w1 : 0u;
+      }
+      const uint32_t ww[2] = {w0, w1};
+      uint32_t rk[2], kk[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const uint32_t w = ww[q];
+        const uint32_t k2 = bin_k2(w), g1 = bin_g1(w), g2 = bin_g2(w);
+        n2 += __popcll(__ballot(k2 != 0u));
+        n1a += __popcll(__ballot(g1 != 0u));
+        n1b += __popcll(__ballot(g2 != 0u));
+        const uint32_t x = w << 4;   // low five bits: (k2 & 1) << 4, the u16 half's shift
+        const uint32_t word = k2 ? (P16 ? (k2 >> 1) : k2) : trash;
+        const uint32_t old = atomicAdd(&W[word], k2 ? (P16 ? (1u << (x & 31u)) : 1u) : 0u);
+        rk[q] = P16 ? __builtin_amdgcn_ubfe(old, x & 31u, 16) : (k2 ? old : 0u);
+        kk[q] = k2;
+        if (keep) kw[(j + q) & 7] = word;
+        atomicAdd(g1 ? H1a_l + g1 * R1 : T_l, one1);
+        atomicAdd(g2 ? H1b_l + g2 * R1 : T_l, one1);
+      }
+      double d[2], lp[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        d[q] = Dt[clampd ? min(rk[q], (uint32_t)LNT - 1u) : rk[q]];   // D[LNT-1] = 0: ranks past the table add 0
+        lp[q] = LPl[kk[q]];
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) acc2 += d[q] - lp[q];
+    };
+    MARK(19);
+#pragma unroll
+    for (int j = 0; j < 8; j += 2)
+      if (64 * j < (int)nsnp) pair(cur.u[j], cur.u[j + 1], j, true);
+    MARK(20);
+    if (nsnp > 8 * WAVE) {   // rows 8 on (windows of > 512 SNPs), streamed one pair ahead
+      const uint32_t* qb = bins + cur.b + lane;
+      uint32_t x0 = 64 * 8 < lim ? qb[64 * 8] : 0u, x1 = 64 * 9 < lim ? qb[64 * 9] : 0u;
+      for (int j = 8; 64 * j < (int)nsnp; j += 2) {
+        const uint32_t w0 = x0, w1 = x1;
+        x0 = 64 * (j + 2) < lim ? qb[64 * (j + 2)] : 0u;
+        x1 = 64 * (j + 3) < lim ? qb[64 * (j + 3)] : 0u;
+        pair(w0, w1, j, false);
+      }
+    }
+    MARK(22);
+    if (!P.fold || filt) {   // rare settings: unfolded (SNPs in the excluded last 2D bin), variant_type filter
+      for (uint32_t i0 = cur.b; i0 < cur.e; i0 += WAVE) {   // wave-uniform trip count
+        const uint32_t w = i0 + lane < cur.e ? bins[i0 + lane] : 0u;
+        nlast += __popcll(__ballot((w & B_LAST) != 0u));
+        nvar += __popcll(__ballot((w & B_VAR) != 0u));
+      }
+    }
+    if (!filt) nvar = nsnp;
+    ulonglong2 fq = make_ulonglong2(0ull, 0ull);   // this window's Fst sums (k_prep): their latency under the window
+    if (FST && lane == 0) fq = reinterpret_cast<const ulonglong2*>(fsum)[s];
+    if (it == 0) STAMP(12);
+    MARK(23);
+    group_sync<WAVE>();
+    // bins with x > LNT-1 SNPs: the ranks from LNT-1 on add F(x) - F(LNT-1) (read before the clear)
+    if (clampd) {
+      constexpr uint32_t L1 = LNT - 1;
+      const double fl = Ft[L1];
+      for (int k = lane; k < h2w; k += WAVE) {
+        const uint32_t v = W[k];
+        const uint32_t xa = P16 ? (v & 0xffffu) : v, xb = P16 ? (v >> 16) : 0u;
+        if (xa > L1) acc2 += (double)xa * lnx_of(lnx, xa) - fl;
+        if (xb > L1) acc2 += (double)xb * lnx_of(lnx, xb) - fl;
+      }
+    }
+    // clear the 2D words this window counted: its rows are then dead
+    if (nsnp <= 8 * WAVE) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (64 * j < (int)nsnp) W[kw[j]] = 0u;
+    } else {
+      uint4* q = reinterpret_cast<uint4*>(W);
+      for (int k = lane; k < h2w / 4; k += WAVE) q[k] = make_uint4(0, 0, 0, 0);
+    }
+    // next window: its slot record is in, issue its first rows now (under the 1D pass and the sums);
+    // the record is wave-uniform: in SGPRs it survives the batch's flush without a VGPR spill
+    srn.x = __builtin_amdgcn_readfirstlane(srn.x);
+    srn.y = __builtin_amdgcn_readfirstlane(srn.y);
+    Win nxt;
+    nxt.has = false;
+    if (more && fill) bounds(sn, srn, nxt);
+    MARK(24);
+    // 1D spectra: one lane per folded inner bin reads (and clears) its R1 replicas; with <= 32 inner
+    // bins per population, lanes 0-31 take population 1 and lanes 32-63 population 2 (acca)
+    double acca = 0.0, accb = 0.0;
+    constexpr uint32_t S1 = P16 ? 16u : 0u;
+    if (half1d) {
+      const bool pa = lane < 32;
+      const int k = 1 + (lane & 31);
+      if (k <= (pa ? P.n1p : P.n2p) - 1) {
+        uint4* q = reinterpret_cast<uint4*>((pa ? H1a : H1b) + k * R1);
+        const uint4 v = *q;
+        *q = make_uint4(0, 0, 0, 0);
+        const uint32_t x = (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
+        acca = x ? xlnx(x, Ft, lnx) - (double)x * LPl[(pa ? P.t1a : P.t1b) + k] : 0.0;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int k = 1 + lane + WAVE * j;
+        if (k <= P.n1p - 1) {
+          uint4* q = reinterpret_cast<uint4*>(H1a + k * R1);
+          const uint4 v = *q;
+          *q = make_uint4(0, 0, 0, 0);
+          const uint32_t x = (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
+          acca += x ? xlnx(x, Ft, lnx) - (double)x * LPl[P.t1a + k] : 0.0;
+        }
+        if (k <= P.n2p - 1) {
+          uint4* q = reinterpret_cast<uint4*>(H1b + k * R1);
+          const uint4 v = *q;
+          *q = make_uint4(0, 0, 0, 0);
+          const uint32_t x = (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
+          accb += x ? xlnx(x, Ft, lnx) - (double)x * LPl[P.t1b + k] : 0.0;
+        }
+      }
+    }
+    if (it == 0) STAMP(13);
+    MARK(25);
+    // the sums, replicated in every lane (fixed trees: deterministic), into lane jb of the batch
+    const double s2 = wave_sum_all(acc2);
+    double sa, sb;
+    if (half1d) {
+      wave_sum_halves_all(acca, sa, sb);
+    } else {
+      sa = wave_sum_all(acca);
+      sb = wave_sum_all(accb);
+    }
+    MARK(26);
+    put(s, cur.b, nsnp, n2, n1a, n1b, nvar, nlast, s2, sa, sb, fq);
+    ++jb;
+    group_sync<WAVE>();
+    if (it == 0) STAMP(14);
+    MARK(28);
+    ++it;
+    cur = nxt;
+    s = sn;
+    if (!fill) break;
+  }
+  if (jb) flush();   // (a full batch, or the wavefront's last windows)
+  if (s >= ch.slot_hi) break;
+  bounds(s, srn, cur);   // the next batch's first window
+  }
+  STAMP(15);
+  WV_STAMP(it);
+#ifdef SFS2D_STAMPS
+  __builtin_amdgcn_s_barrier();   // diagnostic build only: the block's end is its last active wave's
+#endif
+  BLK_STAMP(1, 1);
+}
+
 template <bool P16, bool FUSED, bool FST>
 __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_scan_w(SCAN_W_ARGS) {
   extern __shared__ double ldsd[];
-  scan_w_body<P16, FUSED, FST, false>(ldsd, SCAN_W_PASS);
+  scan_w_small<P16, FUSED, FST>(ldsd, SCAN_W_PASS);
 }
 
 // K3 for large grids, one wavefront per window (LDS: the wave's histograms only)
