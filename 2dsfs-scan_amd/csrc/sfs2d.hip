@@ -883,18 +883,36 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   if (const char* ev = std::getenv("SFS2D_HR"))
     if (ev[0] == '4' && (size_t)K.nh * 4 * 4 <= 64 * 1024) pl->hr = 4;
   pl->bg_lds = ((size_t)K.nh * pl->hr + WAVE) * 4;   // + 64 lane trash words
-  pl->lds_hist = pl->bg_lds <= 150 * 1024;
+  {
+    // the LDS histogram must fit beside the static LDS of the k_prep variant that will run: the Fst
+    // variant (Fst not taken from k_bg_slice) holds ~20 KB of window sums and reciprocals, so e.g.
+    // pop_size 95 / 95 (148 KB of histogram) takes the global-atomic histogram with Fst
+    const bool kfst = (prm->flags & SFS2D_F_FST) && !pl->fst_win;
+    hipFuncAttributes fa{};
+    const hipError_t ae = kfst ? hipFuncGetAttributes(&fa, (const void*)k_prep<true, true, true, true, false, true>)
+                               : hipFuncGetAttributes(&fa, (const void*)k_prep<true, true, true, true, false, false>);
+    const size_t stat = ae == hipSuccess ? fa.sharedSizeBytes : (kfst ? 24 * 1024 : 1024);
+    pl->lds_hist = pl->bg_lds + stat <= 160 * 1024;
+  }
   if (pl->lds_hist && pl->bg_lds > 64 * 1024) {
     const hipFuncAttribute A = hipFuncAttributeMaxDynamicSharedMemorySize;
     const int lds = (int)pl->bg_lds;
-    hipFuncSetAttribute((const void*)k_prep<true, true, true, true, false, false>, A, lds);
-    hipFuncSetAttribute((const void*)k_prep<true, false, true, true, false, false>, A, lds);
-    hipFuncSetAttribute((const void*)k_prep<true, true, true, true, true, false>, A, lds);
-    hipFuncSetAttribute((const void*)k_prep<true, false, true, true, true, false>, A, lds);
-    hipFuncSetAttribute((const void*)k_prep<true, true, true, true, false, true>, A, lds);
-    hipFuncSetAttribute((const void*)k_prep<true, false, true, true, false, true>, A, lds);
-    hipFuncSetAttribute((const void*)k_prep<true, true, true, true, true, true>, A, lds);
-    hipFuncSetAttribute((const void*)k_prep<true, false, true, true, true, true>, A, lds);
+    hipError_t e = hipSuccess;
+    auto set = [&](const void* f) { if (e == hipSuccess) e = hipFuncSetAttribute(f, A, lds); };
+    set((const void*)k_prep<true, true, true, true, false, false>);
+    set((const void*)k_prep<true, false, true, true, false, false>);
+    set((const void*)k_prep<true, true, true, true, true, false>);
+    set((const void*)k_prep<true, false, true, true, true, false>);
+    set((const void*)k_prep<true, true, true, true, false, true>);
+    set((const void*)k_prep<true, false, true, true, false, true>);
+    set((const void*)k_prep<true, true, true, true, true, true>);
+    set((const void*)k_prep<true, false, true, true, true, true>);
+    set((const void*)k_prep<true, false, true, false, false, false>);   // (the histogram-only pass)
+    set((const void*)k_prep<true, false, true, false, true, false>);
+    if (e != hipSuccess) {   // the large dynamic LDS was refused: the global-atomic histogram instead
+      (void)hipGetLastError();
+      pl->lds_hist = false;
+    }
   }
   hipFuncSetAttribute((const void*)k_bg_finalize, hipFuncAttributeMaxDynamicSharedMemorySize,
                       (int)(sizeof(double) * FIN_LDS_BINS));

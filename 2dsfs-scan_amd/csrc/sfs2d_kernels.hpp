@@ -114,7 +114,10 @@ constexpr int CTR_STRIDE = 16;   // one 64-B line per pool counter
 #endif
 constexpr int FST_LDS = SFS2D_FST_LDS;             // k_prep: windows per tile accumulated in LDS (others: global)
 constexpr int FST_R = SFS2D_FST_R;                 // ... in FST_R interleaved copies (lane & 3) to spread same-window atomics
-constexpr int FST_E_MAX = 49;   // Fst sums as int64 fixed point (deterministic atomics): at most 2^49 per unit
+constexpr int FST_E_MAX = 48;   // Fst sums as int64 fixed point (deterministic atomics): at most 2^48 per unit
+// k_prep's fast path converts a lane's sum of up to 4 SNP terms (|term| <= 1) at once: fst_fixed's
+// |x * scale| < 2^51 must hold for that sum
+static_assert(4.0 * (double)(1ll << FST_E_MAX) < (double)(1ll << 51), "fst_fixed range: 4 terms at the largest scale");
 
 struct Chunk {  // k_scan work item: window slots [slot_lo, slot_hi) of one chromosome
   uint32_t chrom, slot_lo, slot_hi, wid_lo, cb;

@@ -135,6 +135,21 @@ def test_records_per_chrom_snps(S):
                        lambda c: bgs[c])
 
 
+def test_records_large_histogram_with_fst():
+    """pop_size 95 / 95 with Fst: the background histogram (148 KB) no longer fits the LDS beside the
+    Fst k_prep's static window sums; the plan must still run (global-atomic histogram) and match the
+    oracle's records."""
+    from sfs2d import _lib as L
+    from sfs2d.engine import ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(2, [3000, 1700], 95, 95, seed=9595)
+    ocfg = O.Cfg(95, 95)
+    bgs = O.chrom_backgrounds(p, ocfg)
+    wins, _ = O.snp_windows(p, 400)
+    _records_vs_oracle(p, ScanConfig(n1p=95, n2p=95, window_mode=L.WINDOW_SNPS, window=400, fst=True), ocfg, wins,
+                       lambda c: bgs[c])
+
+
 def test_config2_full_size_self_consistency():
     """BASELINE config 2 (1e6 SNPs, n1=n2=50 haploid, 20 kb): every window's counts partition the
     stream, the 2D/1D totals equal the background totals, and a 200-window sample matches the
@@ -268,10 +283,12 @@ def _fst_close(a, b):
 
 
 @pytest.mark.parametrize("n1p,n2p,mode,ws", [(25, 25, "bp", 20000), (18, 14, "bp", 7000), (25, 25, "snps", 500),
-                                             (100, 75, "snps", 500)])
+                                             (100, 75, "snps", 500), (95, 95, "snps", 400), (95, 95, "bp", 20000)])
 def test_fst_vs_oracle(n1p, n2p, mode, ws):
     """Hudson Fst per window (k_scan_w fast path, k_scan_g for the 201x151 grid) against
-    oracle.window_fst (parity of Fst itself is unpinned: the reference has no Fst)."""
+    oracle.window_fst (parity of Fst itself is unpinned: the reference has no Fst).  95 x 95: a
+    background histogram (148 KB) that fits the LDS alone but not beside the Fst k_prep's static
+    sums, which then takes the global-atomic histogram."""
     from sfs2d import _lib as L
     from sfs2d.engine import Engine, ScanConfig
     from sfs2d.synth import synth_genome
