@@ -33,6 +33,8 @@ print(which, "K3 blk0: prologue %.2f  2D pass(1st) %.2f  1D+clear %.2f  reduce+s
     d(10, 11), d(11, 12), d(12, 13), d(13, 14), d(14, 15)))
 print(which, "K3 fused prologue: replicas %.2f  1D+leaves %.2f  tree %.2f  logs %.2f  zero %.2f us" % (
     d(10, 16), d(16, 17), d(17, 18), d(18, 19), d(19, 11)))
+print(which, "K3 sliced prologue: D/F copy %.2f  lp copy %.2f  leaf tree %.2f  head %.2f  zero %.2f us" % (
+    d(10, 24), d(24, 25), d(25, 26), d(26, 27), d(27, 11)))
 print(which, "gaps: K1end->K2start %.2f  K2end->K3start %.2f us" % (d(23, 0), d(4, 10)))
 
 # per-block spans (us) of the last run: k_prep = 0, k_scan_w = 1
