@@ -164,6 +164,7 @@ struct sfs2d_plan {
   std::vector<hipEvent_t> tev;   // 6 per sampled run (start / end of k_prep, k_bg_slice, the scan)
   int tcount = 0;
   int tevery = 1;                // sample every tevery-th run
+  int tmask = 7;                 // kernels with events: bit 0 k_prep, 1 k_bg_slice, 2 the scan kernel
   int64_t tseen = 0;             // runs since timing was set
   // events of the run being enqueued: k_prep start/stop, scan start/stop (null: not sampled).  They
   // go into the kernels' own dispatch packets (hipExtLaunchKernelGGL), so they stamp the kernel's
@@ -1026,9 +1027,9 @@ int sfs2d_plan_run_phase(sfs2d_plan* pl, int phase, sfs2d_window* out_dev) {
     return set_err(ctx, SFS2D_E_ARG, "supplied-background plan run before sfs2d_plan_set_background");
   // sampled runs: each kernel carries its start / end events in its own dispatch packet; a kernel
   // this run does not launch gets both events recorded in the stream instead (duration ~0)
-  for (int k = 0; k < 6; ++k) pl->kev[k] = te ? te[k] : nullptr;
+  for (int k = 0; k < 6; ++k) pl->kev[k] = (te && ((pl->tmask >> (k / 2)) & 1)) ? te[k] : nullptr;
   auto mark = [&](int k) -> int {
-    if (te) {
+    if (te && ((pl->tmask >> (k / 2)) & 1)) {
       HIPCHK(ctx, hipEventRecord(te[k], ctx->stream));
       HIPCHK(ctx, hipEventRecord(te[k + 1], ctx->stream));
     }
@@ -1068,8 +1069,13 @@ int sfs2d_plan_grids(const sfs2d_plan* pl, int64_t* prep_threads, int64_t* scan_
 int sfs2d_plan_set_timing(sfs2d_plan* pl, int max_runs) { return sfs2d_plan_set_timing_sampled(pl, max_runs, 1); }
 
 int sfs2d_plan_set_timing_sampled(sfs2d_plan* pl, int max_runs, int every) {
-  if (!pl || max_runs < 0 || every < 1) return SFS2D_E_ARG;
+  return sfs2d_plan_set_timing_kernels(pl, max_runs, every, 7);
+}
+
+int sfs2d_plan_set_timing_kernels(sfs2d_plan* pl, int max_runs, int every, int kernel_mask) {
+  if (!pl || max_runs < 0 || every < 1 || (kernel_mask & ~7) || !kernel_mask) return SFS2D_E_ARG;
   pl->tevery = every;
+  pl->tmask = kernel_mask;
   pl->tseen = 0;
   sfs2d_ctx* ctx = pl->ctx;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
@@ -1085,10 +1091,12 @@ int sfs2d_plan_timing_read(sfs2d_plan* pl, int* nruns, double* ms_k1, double* ms
   if (!pl || !nruns) return SFS2D_E_ARG;
   sfs2d_ctx* ctx = pl->ctx;
   double t[3] = {0, 0, 0};
+  const int klast = (pl->tmask & 4) ? 2 : (pl->tmask & 2) ? 1 : 0;   // the run's last recorded event pair
   for (int r = 0; r < pl->tcount; ++r) {
     hipEvent_t* te = &pl->tev[(size_t)r * 6];
-    HIPCHK(ctx, hipEventSynchronize(te[5]));
+    HIPCHK(ctx, hipEventSynchronize(te[2 * klast + 1]));
     for (int k = 0; k < 3; ++k) {
+      if (!((pl->tmask >> k) & 1)) continue;
       float ms = 0;
       HIPCHK(ctx, hipEventElapsedTime(&ms, te[2 * k], te[2 * k + 1]));
       t[k] += ms;

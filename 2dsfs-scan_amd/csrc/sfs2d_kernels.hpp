@@ -2070,9 +2070,11 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       w.e = w.b + P.ws;
     }
     if (w.has) {   // the bins buffer has SCAN_PAD readable words past n; masked in the last step
-      const uint32_t* q = bins + w.b + lane;
+      // (uniform base + a 32-bit lane offset: no per-lane 64-bit pointer stays live, which the exact
+      // path's registers pushed to scratch -- 512 B of stores per wavefront)
+      const uint32_t* q = bins + w.b;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) w.u[j] = q[64 * j];
+      for (int j = 0; j < 8; ++j) w.u[j] = q[(uint32_t)lane + 64u * j];
     }
   };
   // window schedule: one static window per wavefront, then the chromosome's pool counters (an
@@ -2339,12 +2341,14 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       if (64 * j < (int)nsnp) pair(cur.u[j], cur.u[j + 1], j, true);
     MARK(20);
     if (nsnp > 8 * WAVE) {   // rows 8 on (windows of > 512 SNPs), streamed one pair ahead
-      const uint32_t* qb = bins + cur.b + lane;
-      uint32_t x0 = 64 * 8 < lim ? qb[64 * 8] : 0u, x1 = 64 * 9 < lim ? qb[64 * 9] : 0u;
+      const uint32_t* qb = bins + cur.b;
+      uint32_t ln = (uint32_t)lane;
+      asm volatile("" : "+v"(ln));   // (else bins + lane is hoisted out of the window loop and spilled)
+      uint32_t x0 = 64 * 8 < lim ? qb[ln + 64 * 8] : 0u, x1 = 64 * 9 < lim ? qb[ln + 64 * 9] : 0u;
       for (int j = 8; 64 * j < (int)nsnp; j += 2) {
         const uint32_t w0 = x0, w1 = x1;
-        x0 = 64 * (j + 2) < lim ? qb[64 * (j + 2)] : 0u;
-        x1 = 64 * (j + 3) < lim ? qb[64 * (j + 3)] : 0u;
+        x0 = 64 * (j + 2) < lim ? qb[ln + 64u * (j + 2)] : 0u;
+        x1 = 64 * (j + 3) < lim ? qb[ln + 64u * (j + 3)] : 0u;
         pair(w0, w1, j, false);
       }
     }

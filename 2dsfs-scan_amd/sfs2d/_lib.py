@@ -29,6 +29,7 @@ EXPORTS = [
     "sfs2d_abi_version", "sfs2d_ctx_create", "sfs2d_ctx_destroy", "sfs2d_last_error", "sfs2d_ctx_set_stream",
     "sfs2d_data_upload", "sfs2d_data_wrap_device", "sfs2d_data_free", "sfs2d_bg_hist", "sfs2d_plan_create",
     "sfs2d_plan_num_records", "sfs2d_plan_set_background", "sfs2d_plan_run", "sfs2d_plan_run_many", "sfs2d_plan_set_timing_sampled",
+    "sfs2d_plan_set_timing_kernels",
     "sfs2d_plan_fst_read", "sfs2d_plan_fst_buffer", "sfs2d_plan_read",
     "sfs2d_plan_bg_buffer", "sfs2d_plan_run_phase", "sfs2d_plan_check", "sfs2d_plan_time",
     "sfs2d_plan_destroy", "sfs2d_scan", "sfs2d_plan_set_timing", "sfs2d_plan_timing_read",
@@ -102,6 +103,7 @@ def lib():
     L.sfs2d_plan_run.argtypes = [vp, vp]
     L.sfs2d_plan_run_many.argtypes = [vp, C.c_int, vp]
     L.sfs2d_plan_set_timing_sampled.argtypes = [vp, C.c_int, C.c_int]
+    L.sfs2d_plan_set_timing_kernels.argtypes = [vp, C.c_int, C.c_int, C.c_int]
     L.sfs2d_plan_fst_read.argtypes = [vp, vp, i64]
     L.sfs2d_plan_fst_buffer.argtypes = [vp, C.POINTER(vp), C.POINTER(i64)]
     L.sfs2d_plan_run_phase.argtypes = [vp, C.c_int, vp]

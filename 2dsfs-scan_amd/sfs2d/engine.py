@@ -246,9 +246,10 @@ class Plan:
         self.eng.check(self.eng.lib.sfs2d_plan_stats(self.h, C.byref(v)))
         return int(v.value)
 
-    def set_timing(self, max_runs: int, every: int = 1):
-        """Record HIP events around each kernel of every `every`-th following run (<= max_runs samples)."""
-        self.eng.check(self.eng.lib.sfs2d_plan_set_timing_sampled(self.h, int(max_runs), int(every)))
+    def set_timing(self, max_runs: int, every: int = 1, kernels: int = 7):
+        """Record HIP events around each kernel of every `every`-th following run (<= max_runs samples);
+        `kernels`: bit 0 k_prep, bit 1 k_bg_slice, bit 2 the scan kernel (the others read 0)."""
+        self.eng.check(self.eng.lib.sfs2d_plan_set_timing_kernels(self.h, int(max_runs), int(every), int(kernels)))
 
     def timing_read(self):
         n = C.c_int()

@@ -235,9 +235,13 @@ def main():
             step(i)
     else:
         pl.run_many(args.warmup, out.data_ptr())
-    # HIP events around each kernel of every 8th timed run, on the stream the kernels run on (sampled:
-    # an event pair costs several microseconds of queue time, 1/8 of it is ~1 us per step)
-    pl.set_timing(args.steps, every=8)
+    # HIP events around the scan kernel (the roofline's) and k_bg_slice of every 8th timed run, on the
+    # stream the kernels run on, carried in their dispatch packets.  An event pair costs queue time:
+    # events around all three kernels of every 8th run cost ~2 us per step, these two ~1 us
+    # (tools/timing_overhead.py); the scan kernel's start event needs the end event of the kernel
+    # before it (alone it also counts that kernel's drain: 10.8-11.4 vs 9.6 us).  k_prep is timed in
+    # an untimed pass after the timed loop.
+    pl.set_timing(args.steps, every=8, kernels=6)
     if dl:
         dist.barrier()
     torch.cuda.synchronize()
@@ -257,7 +261,11 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    nr, (k1, k2, k3) = pl.timing_read()
+    nr, (_, k2, k3) = pl.timing_read()
+    pl.set_timing(16, every=1)   # k_prep (and the other two again), outside the timed region
+    pl.run_many(16, out.data_ptr())
+    _, (k1, _, k3_untimed) = pl.timing_read()
+    pl.set_timing(0)
     pl.check()
     recs = np.frombuffer(out[:nrec].cpu().numpy().tobytes(), dtype=L.WINDOW_DTYPE)
     nwin_rank = int(((recs["flags"] & L.W_EMPTY) == 0).sum())
@@ -288,8 +296,10 @@ def main():
                                       + (f" per step ({'native' if nat is not None else 'Python'} step loop"
                                          + ("" if nat is None else ", gathers " + ("overlapped on a comm stream" if gather_on else "serial on the scan stream"))
                                          + ")" if dl else "")},
-            "kernels_ms": {"k_prep": k1, "k_bg_slice": k2, "k_scan_w": k3, "timed_runs": nr,
-                           "exact_path_windows": pl.stats()},
+            "kernels_ms": {"k_prep": k1, "k_bg_slice": k2, "k_scan_w": k3, "k_scan_w_untimed_pass": k3_untimed,
+                           "timed_runs_sampled": nr, "exact_path_windows": pl.stats(),
+                           "note": "k_bg_slice / k_scan_w: events in every 8th timed run; k_prep: 16 runs after "
+                                   "the timed loop"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_scan_w", "ms": k3, "algorithmic_bytes": b3,

@@ -184,6 +184,10 @@ int sfs2d_plan_check(sfs2d_plan* plan);
  * between kernels.  sfs2d_plan_timing_read averages the sampled runs' per-kernel durations */
 int sfs2d_plan_set_timing(sfs2d_plan* plan, int max_runs);   /* = sampled(plan, max_runs, 1) */
 int sfs2d_plan_set_timing_sampled(sfs2d_plan* plan, int max_samples, int every);
+/* the same for a subset of the kernels: bit 0 k_prep, bit 1 k_bg_slice, bit 2 the scan kernel (an event
+ * pair costs queue time: the bench times only the scan kernel inside its timed loop); the kernels
+ * left out read 0 in sfs2d_plan_timing_read */
+int sfs2d_plan_set_timing_kernels(sfs2d_plan* plan, int max_samples, int every, int kernel_mask);
 /* average device time per kernel over the sampled runs (synchronises): k1 = k_prep, k2 = k_bg_slice
  * (0 when the plan does not launch it), k3 = the window scan kernel (k_scan_w / k_scan_gw / k_scan_g) */
 int sfs2d_plan_timing_read(sfs2d_plan* plan, int* nruns, double* ms_k1, double* ms_k2, double* ms_k3);
