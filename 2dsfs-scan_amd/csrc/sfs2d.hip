@@ -866,11 +866,15 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
     const int64_t Tmax = (prm->flags & SFS2D_F_FST) ? 32768 : 65536;
     int64_t T = std::max<int64_t>(4096, std::min<int64_t>(Tmax, (n / 768 + 4095) / 4096 * 4096));
     if (const char* ev = std::getenv("SFS2D_TILE")) T = std::max<int64_t>(2048, std::atoll(ev) & ~int64_t(3));   // tuning
+    // tile edges on absolute multiples of 4 SNPs (T is): only a chromosome's first and last step
+    // take k_prep's masked edge path, every interior step of every tile the fast one
     for (int c = 0; c < nc; ++c)
-      for (int64_t s = data->chrom_off[c]; s < data->chrom_off[c + 1]; s += T) {
+      for (int64_t s = data->chrom_off[c]; s < data->chrom_off[c + 1];) {
+        const int64_t e = std::min<int64_t>((s & ~int64_t(3)) + T, data->chrom_off[c + 1]);
         Tile t{};
         t.chrom = (uint32_t)c; t.begin = (uint32_t)s;
-        t.end = (uint32_t)std::min<int64_t>(s + T, data->chrom_off[c + 1]);
+        t.end = (uint32_t)e;
+        s = e;
         t.cb = (uint32_t)data->chrom_off[c]; t.ce = (uint32_t)data->chrom_off[c + 1];
         t.sbase = (uint32_t)slot_base[c];
         t.nslots = (uint32_t)(slot_base[c + 1] - slot_base[c]);
@@ -1340,10 +1344,13 @@ int sfs2d_bg_hist(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* pr
   const int c0 = chrom < 0 ? 0 : chrom, c1 = chrom < 0 ? data->nchrom : chrom + 1;
   const int64_t T = 16384;
   for (int c = c0; c < c1; ++c)
-    for (int64_t s = data->chrom_off[c]; s < data->chrom_off[c + 1]; s += T) {
+    for (int64_t s = data->chrom_off[c]; s < data->chrom_off[c + 1];) {   // (edges on multiples of 4, as plans)
+      const int64_t e = std::min<int64_t>((s & ~int64_t(3)) + T, data->chrom_off[c + 1]);
       Tile t{};
-      t.chrom = 0; t.begin = (uint32_t)s; t.end = (uint32_t)std::min<int64_t>(s + T, data->chrom_off[c + 1]);
+      t.chrom = 0; t.begin = (uint32_t)s; t.end = (uint32_t)e;
+      t.cb = (uint32_t)data->chrom_off[c]; t.ce = (uint32_t)data->chrom_off[c + 1];
       pl.tiles.push_back(t);
+      s = e;
     }
   // chrom_off for pseudo-chromosome 0 is only read by segmentation (disabled)
   std::vector<uint32_t> hist((size_t)REPL * K.nh, 0);

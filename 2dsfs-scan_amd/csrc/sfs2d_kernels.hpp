@@ -692,8 +692,10 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
     auto nc2 = [](uint32_t c) { return __builtin_amdgcn_udot4(c, 0x01010000u, 0u, false); };
     const bool bad = (max(max(nc1(ca.x), nc1(ca.y)), max(nc1(ca.z), nc1(ca.w))) > (uint32_t)P.n1) |
                      (max(max(nc2(ca.x), nc2(ca.y)), max(nc2(ca.z), nc2(ca.w))) > (uint32_t)P.n2);
-    // a tile's first and last steps hold its edges, the chromosome's first / last SNP included
-    const bool edge = base == ab || base + STEP >= t.end;   // block-uniform
+    // the masked edge path: a step reaching outside the tile (only a chromosome's first / last tile
+    // has unaligned ends: the host puts tile edges on multiples of 4 SNPs) or holding the
+    // chromosome's first or last SNP (window starts / ends there whatever the neighbours' ids)
+    const bool edge = base < t.begin || base + STEP > t.end || base <= t.cb || base + STEP >= t.ce;   // block-uniform
     using T_ = std::true_type;
     using F_ = std::false_type;
     if (!FASTOK || edge || __ballot(bad)) process(T_{}, F_{}, ia, ca, pa, aav, wpa, wna);   // exact, masked
