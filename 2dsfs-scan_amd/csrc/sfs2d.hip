@@ -1424,6 +1424,7 @@ struct RcclApi {
   decltype(&ncclCommInitRank) init_rank = nullptr;
   decltype(&ncclCommDestroy) destroy = nullptr;
   decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclGather) gather = nullptr;   // (optional: an RCCL extension)
   decltype(&ncclGetErrorString) errstr = nullptr;
 };
 
@@ -1438,6 +1439,7 @@ RcclApi& rccl() {
     a.init_rank = reinterpret_cast<decltype(a.init_rank)>(dlsym(h, "ncclCommInitRank"));
     a.destroy = reinterpret_cast<decltype(a.destroy)>(dlsym(h, "ncclCommDestroy"));
     a.all_gather = reinterpret_cast<decltype(a.all_gather)>(dlsym(h, "ncclAllGather"));
+    a.gather = reinterpret_cast<decltype(a.gather)>(dlsym(h, "ncclGather"));
     a.errstr = reinterpret_cast<decltype(a.errstr)>(dlsym(h, "ncclGetErrorString"));
     a.ok = a.get_id && a.init_rank && a.destroy && a.all_gather && a.errstr;
     if (!a.ok) a.err = "librccl.so.1 lacks the expected symbols";
@@ -1451,6 +1453,7 @@ struct sfs2d_dist {
   sfs2d_ctx* ctx = nullptr;
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
+  bool to_root = false;   // ncclGather to rank 0 (else ncclAllGather)
   hipEvent_t ev_scan[2] = {nullptr, nullptr}, ev_comm[2] = {nullptr, nullptr};
 };
 
@@ -1477,6 +1480,8 @@ int sfs2d_dist_create(sfs2d_ctx* ctx, const uint8_t* id128, int rank, int world,
   std::memcpy(id.internal, id128, NCCL_UNIQUE_ID_BYTES);
   sfs2d_dist* d = new sfs2d_dist();
   d->ctx = ctx; d->rank = rank; d->world = world;
+  d->to_root = r.gather != nullptr;
+  if (const char* ev = std::getenv("SFS2D_GATHER")) d->to_root = d->to_root && std::strcmp(ev, "all") != 0;
   const ncclResult_t e = r.init_rank(&d->comm, world, id, rank);
   if (e != ncclSuccess) { delete d; return set_err(ctx, SFS2D_E_HIP, std::string("ncclCommInitRank: ") + r.errstr(e)); }
   for (int b = 0; b < 2; ++b) {
@@ -1514,10 +1519,20 @@ int sfs2d_dist_scan_gather(sfs2d_dist* d, sfs2d_plan* pl, void* out0, void* out1
       HIPCHK(ctx, hipEventRecord(d->ev_scan[b], ctx->stream));
       HIPCHK(ctx, hipStreamWaitEvent(cs, d->ev_scan[b], 0));
     }
-    const ncclResult_t e = r.all_gather(outs[b], gath[b], (size_t)rows * sizeof(sfs2d_window), ncclUint8, d->comm, cs);
-    if (e != ncclSuccess) return set_err(ctx, SFS2D_E_HIP, std::string("ncclAllGather: ") + r.errstr(e));
+    const size_t bytes = (size_t)rows * sizeof(sfs2d_window);
+    const ncclResult_t e = d->to_root ? r.gather(outs[b], gath[b], bytes, ncclUint8, 0, d->comm, cs)
+                                      : r.all_gather(outs[b], gath[b], bytes, ncclUint8, d->comm, cs);
+    if (e != ncclSuccess)
+      return set_err(ctx, SFS2D_E_HIP, std::string(d->to_root ? "ncclGather: " : "ncclAllGather: ") + r.errstr(e));
     if (overlap) HIPCHK(ctx, hipEventRecord(d->ev_comm[b], cs));
   }
+  return 0;
+}
+
+int sfs2d_dist_set_gather(sfs2d_dist* d, int to_root) {
+  if (!d) return SFS2D_E_ARG;
+  if (to_root && !rccl().gather) return set_err(d->ctx, SFS2D_E_ARG, "the loaded RCCL has no ncclGather");
+  d->to_root = to_root != 0;
   return 0;
 }
 

@@ -276,8 +276,9 @@ class Plan:
 
 class Dist:
     """One rank's RCCL communicator in the native library (sfs2d_dist_*): back-to-back scans of a
-    plan, each all-gathering the fixed-stride window tables of every rank, enqueued
-    from C so that the host loop is not the bottleneck."""
+    plan, each gathering the fixed-stride window tables of every rank to rank 0 (ncclGather; or
+    all-gathering them into every rank, set_gather(False)), enqueued from C so that
+    the host loop is not the bottleneck."""
 
     def __init__(self, eng: Engine, uid: bytes, rank: int, world: int):
         if len(uid) != 128:
@@ -295,6 +296,10 @@ class Dist:
         self.eng.check(self.eng.lib.sfs2d_dist_scan_gather(
             self.h, plan.h, C.c_void_p(outs[0]), C.c_void_p(outs[1]), C.c_void_p(gathered[0]),
             C.c_void_p(gathered[1]), rows, first_step, nsteps, C.c_void_p(comm_stream) if comm_stream else None))
+
+    def set_gather(self, to_root: bool):
+        """True: ncclGather to rank 0 (the default where RCCL has it); False: ncclAllGather."""
+        self.eng.check(self.eng.lib.sfs2d_dist_set_gather(self.h, 1 if to_root else 0))
 
     def close(self):
         if self.h:

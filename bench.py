@@ -172,6 +172,7 @@ def main():
     # the step loop runs in the native library (sfs2d_dist_scan_gather: its own RCCL communicator, the
     # scans and all-gathers enqueued from C); the Python loop below is the fallback
     nat = None
+    gather_root = False
     if dl:
         hdr = torch.zeros(129, dtype=torch.uint8)
         if rank == 0:
@@ -185,6 +186,18 @@ def main():
         hdr = hdr.cpu()
         if int(hdr[0]) == 1 and not args.py_loop:
             nat = eng.dist(bytes(hdr[1:].tolist()), rank, world)
+            # one ncclGather of the window tables to rank 0 per step (their one consumer),
+            # ncclAllGather where the loaded RCCL lacks it or SFS2D_GATHER=all; the same on every rank
+            to_root = os.environ.get("SFS2D_GATHER", "root") != "all"
+            ok = torch.tensor([1 if to_root else 0], dtype=torch.int32, device=f"cuda:{local}")
+            if to_root:
+                try:
+                    nat.set_gather(True)
+                except Exception:  # noqa: BLE001
+                    ok.zero_()
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            gather_root = bool(int(ok.item()))
+            nat.set_gather(gather_root)
     ev_scan = [torch.cuda.Event() for _ in range(2)]
     ev_comm = [torch.cuda.Event() for _ in range(2)]
     for e in ev_comm:
@@ -226,10 +239,21 @@ def main():
         pre = 4
         nat.scan_gather(pl, optrs, gptrs, rows, 0, pre, None)
         wh = max(20, args.warmup)
-        t_se = timed(None, pre, wh)
-        t_ov = timed(comm_s.cuda_stream, pre + wh, wh)
+        step_no = pre
+        if gather_root:
+            # gather to rank 0 vs all-gather, both serial: the faster one stays (on one rank the
+            # ncclGather's grouped send / receive cost 37 vs 30 us per step; at N > 1 it moves 1/N
+            # of the all-gather's bytes)
+            t_root = timed(None, step_no, wh)
+            nat.set_gather(False)
+            t_all = timed(None, step_no + wh, wh)
+            step_no += 2 * wh
+            gather_root = t_root < t_all
+            nat.set_gather(gather_root)
+        t_se = timed(None, step_no, wh)
+        t_ov = timed(comm_s.cuda_stream, step_no + wh, wh)
         gather_on = comm_s.cuda_stream if t_ov < 0.9 * t_se else None
-        first_timed = pre + 2 * wh
+        first_timed = step_no + 2 * wh
     elif dl:
         for i in range(args.warmup):
             step(i)
@@ -292,7 +316,8 @@ def main():
                        "snps_per_gpu": p.n, "windows_per_gpu": nwin_rank, "window_bp": WS,
                        "stats": "T2D, T1D_p1, T1D_p2 (reference semantics) + Hudson Fst (DESIGN.md; not in the "
                                 "reference, parity vs its own oracle restatement)",
-                       "parallelism": f"windows sharded by chromosome over {world} GPU(s); RCCL all-gather"
+                       "parallelism": f"windows sharded by chromosome over {world} GPU(s); RCCL "
+                                      + ("gather to rank 0" if gather_root else "all-gather")
                                       + (f" per step ({'native' if nat is not None else 'Python'} step loop"
                                          + ("" if nat is None else ", gathers " + ("overlapped on a comm stream" if gather_on else "serial on the scan stream"))
                                          + ")" if dl else "")},

@@ -206,12 +206,17 @@ int sfs2d_plan_destroy(sfs2d_plan* plan);
  * gathered[s & 1] on `comm_stream` while the next step scans (the scan of step s + 2 waits for the
  * gather of step s); comm_stream NULL: each gather follows its scan on the library's stream (no
  * cross-stream events).  Steps are numbered from `first_step`.  Enqueue only: synchronise the
- * streams to wait; synchronise before switching between the two modes. */
+ * streams to wait; synchronise before switching between the two modes.
+ * sfs2d_dist_set_gather: 1 (the default when RCCL has it) = one ncclGather to rank 0 per step (the
+ * reference's results have one consumer; only rank 0's `gathered` buffers are written, the other
+ * ranks' are left alone), 0 = ncclAllGather into every rank's buffers.  SFS2D_E_ARG for 1 when the
+ * loaded RCCL lacks ncclGather. */
 typedef struct sfs2d_dist sfs2d_dist;
 int sfs2d_dist_unique_id(uint8_t* id128);
 int sfs2d_dist_create(sfs2d_ctx* ctx, const uint8_t* id128, int rank, int world, sfs2d_dist** out);
 int sfs2d_dist_scan_gather(sfs2d_dist* d, sfs2d_plan* plan, void* out0, void* out1, void* gathered0,
                            void* gathered1, int64_t rows, int64_t first_step, int nsteps, void* comm_stream);
+int sfs2d_dist_set_gather(sfs2d_dist* d, int to_root);
 int sfs2d_dist_destroy(sfs2d_dist* d);
 
 /* one-shot convenience: plan + run + read (+ supplied background when bg2d != NULL) */

@@ -1,6 +1,6 @@
 """The native multi-GPU step loop (sfs2d_dist_*, include/sfs2d.h): RCCL loaded at run time, one
 communicator per rank, scans and all-gathers of the window tables enqueued from C.  On the one-GPU
-box: a one-rank communicator (the gather is a copy) -- the tables gathered after back-to-back
+box: a one-rank communicator (gather and all-gather are copies) -- the tables gathered after back-to-back
 steps equal the plan's own records.  N > 1 runs are the driver's (bench.py --gpus N)."""
 import numpy as np
 import pytest
@@ -26,7 +26,9 @@ def test_single_rank_scan_gather():
     comm = torch.cuda.Stream(device=0)
     d = eng.dist(eng.dist_unique_id(), 0, 1)
     try:
-        for first, n, cs in ((0, 5, comm.cuda_stream), (5, 4, None)):   # overlapped gathers, then serial
+        # overlapped gathers to the root, serial gathers to the root, serial all-gathers
+        for first, n, cs, root in ((0, 5, comm.cuda_stream, True), (5, 4, None, True), (9, 3, None, False)):
+            d.set_gather(root)
             for g in gath:
                 g.fill_(7)
             d.scan_gather(pl, [o.data_ptr() for o in outs], [g.data_ptr() for g in gath], rows, first, n, cs)
