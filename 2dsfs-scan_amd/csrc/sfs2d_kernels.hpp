@@ -2174,6 +2174,12 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   const uint32_t trash = (uint32_t)(h2w + h1w + h1wb + lane);   // the lane's trash word (index from W)
   uint32_t* const T_l = W + trash;
   const uint32_t one1 = P16 ? 0x10000u : 1u;   // 1D increment (P16: upper halves, see the window loop)
+  // the 1D atomics' LDS byte addresses: per-lane bases kept opaque, so that a bin's address is one
+  // v_lshl_add (the compiler otherwise re-splits base + replica + bin into three operations)
+  typedef __attribute__((address_space(3))) uint32_t lds_u32;
+  uint32_t a1b = (uint32_t)(uintptr_t)((lds_u32*)H1a_l), a2b = (uint32_t)(uintptr_t)((lds_u32*)H1b_l);
+  uint32_t atr = (uint32_t)(uintptr_t)((lds_u32*)T_l);
+  asm volatile("" : "+v"(a1b), "+v"(a2b), "+v"(atr));
   // ---- batched finish.  Lane j of the B* registers holds the j-th window this wavefront has
   // scanned since the last flush (slot, SNP range, counts, the three sums); per window only the
   // sums' wave reductions run, and the T values, the zero / NaN rules, the Fst value and the 64-B
@@ -2306,10 +2312,10 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     uint32_t n2 = 0, n1a = 0, n1b = 0, nlast = 0, nvar = 0;
     uint32_t kw[8];   // the 2D words of the first 8 rows, cleared after the window
     auto pair = [&](uint32_t w0, uint32_t w1, int j, bool keep) {
-      if (64 * (j + 2) > (int)nsnp) {   // the window's last rows
-        w0 = 64 * j < lim ? w0 : 0u;
-        w1 = 64 * (j + 1) < lim ? w1 : 0u;
-      }
+      // SNPs past the window's end: w = 0 (unconditional: a guard on the window's last rows cost
+      // more selects than the masking itself)
+      w0 = 64 * j < lim ? w0 : 0u;
+      w1 = 64 * (j + 1) < lim ? w1 : 0u;
       const uint32_t ww[2] = {w0, w1};
       uint32_t rk[2], kk[2];
 #pragma unroll
@@ -2321,17 +2327,23 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
         n1b += __popcll(__ballot(g2 != 0u));
         const uint32_t x = w << 4;   // low five bits: (k2 & 1) << 4, the u16 half's shift
         const uint32_t word = k2 ? (P16 ? (k2 >> 1) : k2) : trash;
-        const uint32_t old = atomicAdd(&W[word], k2 ? (P16 ? (1u << (x & 31u)) : 1u) : 0u);
-        rk[q] = P16 ? __builtin_amdgcn_ubfe(old, x & 31u, 16) : (k2 ? old : 0u);
+        // (v_lshlrev_b32 / v_bfe_u32 read the shift's low five bits: no mask; C's << would need one)
+        uint32_t one2 = 1u;
+        if (P16) asm("v_lshlrev_b32 %0, %1, 1" : "=v"(one2) : "v"(x));
+        const uint32_t old = atomicAdd(&W[word], k2 ? one2 : 0u);
+        rk[q] = P16 ? __builtin_amdgcn_ubfe(old, x, 16) : (k2 ? old : 0u);
         kk[q] = k2;
         if (keep) kw[(j + q) & 7] = word;
-        atomicAdd(g1 ? H1a_l + g1 * R1 : T_l, one1);
-        atomicAdd(g2 ? H1b_l + g2 * R1 : T_l, one1);
+        const uint32_t u1 = g1 ? a1b + g1 * (4u * R1) : atr, u2 = g2 ? a2b + g2 * (4u * R1) : atr;
+        __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u1, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u2, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       double d[2], lp[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        d[q] = Dt[clampd ? min(rk[q], (uint32_t)LNT - 1u) : rk[q]];   // D[LNT-1] = 0: ranks past the table add 0
+        // D[LNT-1] = 0: ranks past the table add 0 (clampd windows); elsewhere rank < nsnp <= LNT-1 and
+        // the min is a no-op, cheaper than selecting it per window
+        d[q] = Dt[min(rk[q], (uint32_t)LNT - 1u)];
         lp[q] = LPl[kk[q]];
       }
 #pragma unroll
