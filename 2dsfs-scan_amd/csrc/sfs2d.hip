@@ -319,7 +319,7 @@ hipError_t launch_bg_slices(sfs2d_plan* pl) {
   hipExtLaunchKernelGGL(k_bg_slice, dim3((unsigned)pl->slices.size() + 1 + (unsigned)pl->nfst, (unsigned)pl->nbg), dim3(KBLOCK), 0,
                      pl->ctx->stream, pl->kev[2], pl->kev[3], 0, pl->K, pl->d_repl, pl->d_bcount + (size_t)plan_par(pl) * pl->K.nchrom, pl->d_tab,
                      pl->d_lp, pl->d_head, pl->d_leafsum, pl->d_bg1d, pl->d_done, pl->d_slices, (int)pl->slices.size(),
-                     pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->sliced ? 0 : 1, pl->nfst,
+                     pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels, pl->sliced ? 0 : 1, pl->nfst,
                      pl->data->counts, pl->d_bins, pl->d_slots, reinterpret_cast<const double2*>(pl->ctx->d_df + 2 * LNT),
                      pl->d_fst, (uint32_t)pl->nslots);
   return hipGetLastError();

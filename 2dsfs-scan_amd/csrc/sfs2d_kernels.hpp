@@ -163,6 +163,10 @@ __device__ unsigned long long g_blk[2][4096][2];   // per-block start / end (k_p
   do {                                                                                           \
     if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[i] = __builtin_amdgcn_s_memrealtime();     \
   } while (0)
+#define TSTAMP(i)   /* thread 0 of whichever block runs it (a kernel's one tail block) */       \
+  do {                                                                                           \
+    if (threadIdx.x == 0) g_stamps[i] = __builtin_amdgcn_s_memrealtime();                        \
+  } while (0)
 __device__ unsigned long long g_wv[4096 * 8][2];   // k_scan_w per wavefront: end, windows scanned
 #define WV_STAMP(n)                                                                              \
   do {                                                                                           \
@@ -177,6 +181,9 @@ __device__ unsigned long long g_wv[4096 * 8][2];   // k_scan_w per wavefront: en
   } while (0)
 #define STAMP(i) \
   do {           \
+  } while (0)
+#define TSTAMP(i) \
+  do {            \
   } while (0)
 #define BLK_STAMP(k, e) \
   do {                  \
@@ -875,7 +882,7 @@ __global__ __launch_bounds__(KBLOCK) void k_bg_slice(KParams P, uint32_t* __rest
                                                      double* __restrict__ leafsum, Bg1D* __restrict__ bg1d,
                                                      uint32_t* __restrict__ done, const int4* __restrict__ slices,
                                                      int nslices, const int2* __restrict__ leaves, int nleaves,
-                                                     const int4* __restrict__ nodes, int nnodes, int tail,
+                                                     const int4* __restrict__ nodes, int nnodes, int nlevels, int tail,
                                                      int nfst, const uint32_t* __restrict__ counts,
                                                      const uint32_t* __restrict__ bins, const uint2* __restrict__ slots,
                                                      const double2* __restrict__ rt, double* __restrict__ fst_out,
@@ -1014,20 +1021,36 @@ __global__ __launch_bounds__(KBLOCK) void k_bg_slice(KParams P, uint32_t* __rest
   __syncthreads();
   if (!last_blk) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  STAMP(3);
+  TSTAMP(3);
+  // numpy's tree over the leaf sums, by the whole block: leaves and nodes loaded in parallel, then
+  // one level per barrier (children before parents; each node = left + right, the serial order's
+  // sums exactly).  (One thread walking leaves and nodes took 18.6 us on a 201 x 151 grid.)
+  double* node = acc8;   // leaves then internal nodes (<= 2 * PW_MAX_LEAVES entries)
+  static_assert(2 * PW_MAX_LEAVES <= 4 * KBLOCK, "tree nodes per thread");
+  uint32_t bc = 0u;
+  Bg1D o1{};
+  if (tid == 0) { bc = bcount[b]; o1 = bg1d[b]; }
+  int4 nd[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = tid + r * KBLOCK;
+    nd[r] = i < nnodes ? nodes[i] : make_int4(0, 0, -1, 0);
+    if (i < nleaves) node[i] = leafsum[(size_t)b * nleaves + i];
+  }
+  __syncthreads();
+  for (int l = 0; l < nlevels; ++l) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (nd[r].z == l) node[nleaves + tid + r * KBLOCK] = node[nd[r].x] + node[nd[r].y];
+    __syncthreads();
+  }
   if (tid == 0) {
-    const double B2 = (double)bcount[b];
-    const Bg1D o = bg1d[b];
+    const double B2 = (double)bc;
+    const Bg1D o = o1;
     uint32_t flags = o.flags;
     if (B2 == 0.0) flags |= BGF_B2_ZERO;
     const int M2 = P.nb2 - 2;
     if (M2 >= 1 && B2 != 0.0) {
-      double* node = acc8;   // leaves then internal nodes (<= 2 * PW_MAX_LEAVES entries)
-      for (int j = 0; j < nleaves; ++j) node[j] = leafsum[(size_t)b * nleaves + j];
-      for (int i = 0; i < nnodes; ++i) {
-        const int4 ab = nodes[i];
-        node[nleaves + i] = node[ab.x] + node[ab.y];
-      }
       const double S = (nleaves + nnodes) ? node[nleaves + nnodes - 1] : 0.0;
       flags |= adjust_last(T, LP, M2, 1.0 - S, BGF_NAN2);
     }
@@ -1036,7 +1059,7 @@ __global__ __launch_bounds__(KBLOCK) void k_bg_slice(KParams P, uint32_t* __rest
     head[b] = h;
     bcount[b] = 0u;
     done[b] = 0u;
-    STAMP(4);
+    TSTAMP(4);
   }
 }
 

@@ -13,10 +13,15 @@ from sfs2d.engine import Engine, ScanConfig  # noqa: E402
 from sfs2d.synth import synth_genome  # noqa: E402
 
 which = sys.argv[1] if len(sys.argv) > 1 else "config2"
-p = synth_genome(1 if which == "config2" else 32, 1_000_000 if which == "config2" else 1_562_500, 25, 25, seed=1)
+if which == "config5":   # 201 x 151 grid, 500-SNP windows (large-grid kernels, k_bg_slice with its tail)
+    p = synth_genome(1, 1_000_000, 100, 75, seed=55)
+    cfg = ScanConfig(n1p=100, n2p=75, window_mode=L.WINDOW_SNPS, window=500)
+else:
+    p = synth_genome(1 if which == "config2" else 32, 1_000_000 if which == "config2" else 1_562_500, 25, 25, seed=1)
+    cfg = ScanConfig(n1p=25, n2p=25, window=20000, fst=True)
 eng = Engine.get(0)
 dev = eng.upload(p)
-pl = eng.plan(dev, ScanConfig(n1p=25, n2p=25, window=20000, fst=True))
+pl = eng.plan(dev, cfg)
 for _ in range(3):
     pl.run()
 pl.check()
