@@ -1728,6 +1728,11 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
   uint32_t* const H1a_l = H1a + rep;            // this lane's replica column of the 1D histograms
   uint32_t* const H1b_l = H1b + rep;
   uint32_t* const T_l = W + trash;
+  // the 1D atomics' LDS byte addresses from opaque per-lane bases (one v_lshl_add per bin)
+  typedef __attribute__((address_space(3))) uint32_t lds_u32;
+  uint32_t a1b = (uint32_t)(uintptr_t)((lds_u32*)H1a_l), a2b = (uint32_t)(uintptr_t)((lds_u32*)H1b_l);
+  uint32_t atr = (uint32_t)(uintptr_t)((lds_u32*)T_l);
+  asm volatile("" : "+v"(a1b), "+v"(a2b), "+v"(atr));
   Win cur;
   bounds(s, sr0, cur);
   STAMP(11);
@@ -1765,10 +1770,8 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
     bool ovf = false;   // GL: some u8 bin of this lane wrapped
     uint32_t kw[8];   // the 2D words of the first 8 steps, cleared after the window
     auto pair = [&](uint32_t w0, uint32_t w1, int j, bool keep) {
-      if (64 * (j + 2) > (int)nsnp) {   // the window's last steps: SNPs past e are excluded
-        w0 = 64 * j < lim ? w0 : 0u;
-        w1 = 64 * (j + 1) < lim ? w1 : 0u;
-      }
+      w0 = 64 * j < lim ? w0 : 0u;   // SNPs past e are excluded (unconditional: cheaper than a guard)
+      w1 = 64 * (j + 1) < lim ? w1 : 0u;
       const uint32_t ww[2] = {w0, w1};
       uint32_t rk[2], kk[2];
 #pragma unroll
@@ -1779,8 +1782,12 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
         n1a += __popcll(__ballot(g1 != 0u));
         n1b += __popcll(__ballot(g2 != 0u));
         const uint32_t word = k2 ? (GL ? (k2 >> 2) : P16 ? (k2 >> 1) : k2) : trash;
-        const uint32_t sh = GL ? ((k2 & 3u) << 3) : P16 ? ((k2 & 1u) << 4) : 0u;
-        const uint32_t old = atomicAdd(&W[word], k2 ? (1u << sh) : 0u);
+        // the byte / half's shift: the hardware reads shift operands' low five bits, so w << 3 (GL)
+        // or w << 4 serves without a mask
+        const uint32_t sh = GL ? (w << 3) : P16 ? (w << 4) : 0u;
+        uint32_t one2 = 1u;
+        if (GL || P16) asm("v_lshlrev_b32 %0, %1, 1" : "=v"(one2) : "v"(sh));
+        const uint32_t old = atomicAdd(&W[word], k2 ? one2 : 0u);
         if (GL) {   // (the trash word's low byte counts 1D increments: excluded SNPs take rank 0)
           const uint32_t r = __builtin_amdgcn_ubfe(old, sh, 8);
           rk[q] = k2 ? r : 0u;
@@ -1790,8 +1797,9 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
         }
         kk[q] = k2;
         if (keep) kw[(j + q) & 7] = word;
-        atomicAdd(g1 ? H1a_l + g1 * R1 : T_l, one1);
-        atomicAdd(g2 ? H1b_l + g2 * R1 : T_l, one1);
+        const uint32_t u1 = g1 ? a1b + g1 * (4u * R1) : atr, u2 = g2 ? a2b + g2 * (4u * R1) : atr;
+        __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u1, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u2, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       double d[2], lp[2];
 #pragma unroll
