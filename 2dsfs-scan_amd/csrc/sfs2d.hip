@@ -725,7 +725,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
       // holds only the wave's histograms, still leave >= 2 wavefronts per CU (101 x 101: 7);
       // otherwise k_scan_g (a workgroup per window).  SFS2D_GW=0/1 forces one.
       const int h2w = ((K.nb2 + 3) / 4 + 3) & ~3;   // u8-packed 2D bins
-      size_t gw_lds = (size_t)(h2w + R1 * (K.n1p + 1) + R1 * (K.n2p + 1) + TRASH) * 4;
+      size_t gw_lds = (size_t)(h2w + R1GW * (K.n1p + 1) + R1GW * (K.n2p + 1) + TRASH) * 4;
       if (const char* ev = std::getenv("SFS2D_GW_PAD")) gw_lds += (size_t)std::atoll(ev);   // occupancy experiments
       int occ = 0;
       if (gw_lds <= 160 * 1024) {

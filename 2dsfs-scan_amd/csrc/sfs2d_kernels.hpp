@@ -63,6 +63,32 @@ constexpr int LEAVES_PER_SLICE = 4;
 constexpr int FIN_LDS_BINS = 12288;  // backgrounds with nt <= this keep values / proportions in LDS
 constexpr int TRASH = WAVE;       // lane-private scratch words after each wave's histograms
 constexpr int R1 = 4;             // replicas of the folded 1D window histograms (lane & 3)
+#ifndef SFS2D_GW_R1
+#define SFS2D_GW_R1 1
+#endif
+// ... in k_scan_gw: one copy (less LDS per wavefront, more of them per CU; measured 1 / 2 / 4:
+// sims scan kernel 1.55 / 1.56 / 1.63 ms per 500 replicates, config 5 13.8 / 17.7 / 14.4 us)
+constexpr int R1GW = SFS2D_GW_R1;
+
+// sum (and clear) the RR replicas of one 1D bin word group (RR consecutive words, 4 * RR-B aligned)
+template <int RR>
+__device__ __forceinline__ uint32_t take_replicas(uint32_t* p, uint32_t shift) {
+  if (RR == 4) {
+    uint4* q = reinterpret_cast<uint4*>(p);
+    const uint4 v = *q;
+    *q = make_uint4(0, 0, 0, 0);
+    return (v.x >> shift) + (v.y >> shift) + (v.z >> shift) + (v.w >> shift);
+  } else if (RR == 2) {
+    uint2* q = reinterpret_cast<uint2*>(p);
+    const uint2 v = *q;
+    *q = make_uint2(0, 0);
+    return (v.x >> shift) + (v.y >> shift);
+  } else {
+    const uint32_t v = *p;
+    *p = 0u;
+    return v >> shift;
+  }
+}
 constexpr int FUSED_VCNT = 2 * (1536 + 256) + 16;   // k_scan_w fused prologue: word offset of the counts
 
 enum : uint32_t { ERR_KEY = 1u, ERR_GRID = 2u };
@@ -1604,13 +1630,14 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
   double* Ft = Dt + LNT;                                                   // LNT
   uint32_t* HB = GL ? reinterpret_cast<uint32_t*>(ldsd) : reinterpret_cast<uint32_t*>(Ft + LNT);
   const int h2w = GL ? ((P.nb2 + 3) / 4 + 3) & ~3 : P16 ? ((P.nb2 + 1) / 2 + 3) & ~3 : (P.nb2 + 3) & ~3;
-  const int h1w = R1 * (P.n1p + 1), h1wb = R1 * (P.n2p + 1);
+  constexpr int RG = GL ? R1GW : R1;   // 1D replicas
+  const int h1w = RG * (P.n1p + 1), h1wb = RG * (P.n2p + 1);
   const int per = h2w + h1w + h1wb + TRASH;
   uint32_t* W = HB + wv * per;
   uint32_t* H1a = W + h2w;
   uint32_t* H1b = H1a + h1w;
   const uint32_t trash = (uint32_t)(h2w + h1w + h1wb + lane);   // word offset from W
-  const uint32_t rep = lane & (R1 - 1);
+  const uint32_t rep = lane & (RG - 1);
 
   // the first window's slot record is fetched before the table work
   auto bounds = [&](uint32_t s, uint2 sr, Win& w) {
@@ -1797,7 +1824,7 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
         }
         kk[q] = k2;
         if (keep) kw[(j + q) & 7] = word;
-        const uint32_t u1 = g1 ? a1b + g1 * (4u * R1) : atr, u2 = g2 ? a2b + g2 * (4u * R1) : atr;
+        const uint32_t u1 = g1 ? a1b + g1 * (4u * RG) : atr, u2 = g2 ? a2b + g2 * (4u * RG) : atr;
         __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u1, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u2, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -1857,10 +1884,7 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
       const bool pa = lane < 32;
       const int k = 1 + (lane & 31);
       if (k <= (pa ? P.n1p : P.n2p) - 1) {
-        uint4* q = reinterpret_cast<uint4*>((pa ? H1a : H1b) + k * R1);
-        const uint4 v = *q;
-        *q = make_uint4(0, 0, 0, 0);
-        const uint32_t x = (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
+        const uint32_t x = take_replicas<RG>((pa ? H1a : H1b) + k * RG, S1);
         acca = x ? xlnx(x, Ft, lnx) - (double)x * LPl[(pa ? P.t1a : P.t1b) + k] : 0.0;
       }
     } else
@@ -1868,17 +1892,11 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
     for (int j = 0; j < 2; ++j) {
       const int k = 1 + lane + WAVE * j;
       if (k <= P.n1p - 1) {
-        uint4* q = reinterpret_cast<uint4*>(H1a + k * R1);
-        const uint4 v = *q;
-        *q = make_uint4(0, 0, 0, 0);
-        const uint32_t x = (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
+        const uint32_t x = take_replicas<RG>(H1a + k * RG, S1);
         acca += x ? xlnx(x, Ft, lnx) - (double)x * LPl[P.t1a + k] : 0.0;
       }
       if (k <= P.n2p - 1) {
-        uint4* q = reinterpret_cast<uint4*>(H1b + k * R1);
-        const uint4 v = *q;
-        *q = make_uint4(0, 0, 0, 0);
-        const uint32_t x = (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
+        const uint32_t x = take_replicas<RG>(H1b + k * RG, S1);
         accb += x ? xlnx(x, Ft, lnx) - (double)x * LPl[P.t1b + k] : 0.0;
       }
     }
@@ -1920,7 +1938,7 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
       // rare: exact re-evaluation with the bin-by-bin proportionality test (histograms are clean)
       group_sync<WAVE>();
       if (FUSED) {
-        w = eval_exact<WAVE, P16, R1>(P, bins, cur.b, cur.e,
+        w = eval_exact<WAVE, P16, RG>(P, bins, cur.b, cur.e,
                                       TabFused{LPl, Rc, rs, P.nb2, P.n1, P.n2, P.n1p, P.h1a, P.h1b, P.t1a, P.t1b}, hb,
                                       lnx, W, H1a, H1b, nullptr, nullptr);
       } else if (GL) {
@@ -1933,12 +1951,12 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
           if (__builtin_amdgcn_readfirstlane(got) == 0u) break;
           slot = slot + 1u == (uint32_t)nscr ? 0u : slot + 1u;
         }
-        w = eval_exact<WAVE, false, R1>(P, bins, cur.b, cur.e, TabGlobal{tab + (size_t)bg * P.nt}, hb, lnx,
+        w = eval_exact<WAVE, false, RG>(P, bins, cur.b, cur.e, TabGlobal{tab + (size_t)bg * P.nt}, hb, lnx,
                                         gscr + (size_t)slot * P.nb2, H1a, H1b, nullptr, nullptr);
         __threadfence();   // the slot's words are clean again before it is released
         if (lane == 0) atomicExch(&lock[slot], 0u);
       } else {
-        w = eval_exact<WAVE, P16, R1>(P, bins, cur.b, cur.e, TabLocal{tab + (size_t)bg * P.nt, LPl}, hb, lnx, W,
+        w = eval_exact<WAVE, P16, RG>(P, bins, cur.b, cur.e, TabLocal{tab + (size_t)bg * P.nt, LPl}, hb, lnx, W,
                                       H1a, H1b, nullptr, nullptr);
       }
       if (lane == 0) atomicAdd(err_word + 1, 1u);   // statistics: windows that took the exact path
