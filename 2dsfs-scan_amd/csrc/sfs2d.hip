@@ -1125,6 +1125,30 @@ int sfs2d_plan_run_many(sfs2d_plan* pl, int nruns, sfs2d_window* out_dev) {
   return 0;
 }
 
+int sfs2d_plan_run_streams(sfs2d_plan* const* plans, void* const* streams, sfs2d_window* const* outs, int nplans,
+                           int nruns) {
+  if (!plans || !streams || nplans < 1 || nruns < 0) return SFS2D_E_ARG;
+  sfs2d_ctx* ctx = plans[0] ? plans[0]->ctx : nullptr;
+  if (!ctx) return SFS2D_E_ARG;
+  for (int k = 0; k < nplans; ++k) {
+    if (!plans[k] || plans[k]->ctx != ctx) return set_err(ctx, SFS2D_E_ARG, "plans must share one ctx");
+    for (int j = 0; j < k; ++j)
+      if (plans[j] == plans[k]) return set_err(ctx, SFS2D_E_ARG, "a plan may appear once (its per-run state is not shareable)");
+  }
+  // run i: plan i % nplans on stream i % nplans.  The plans' per-run state (bins, replicas, slots,
+  // counters) is their own, so consecutive runs on different streams overlap; the ctx stream is
+  // switched per run and restored
+  hipStream_t saved = ctx->stream;
+  int rc = 0;
+  for (int i = 0; i < nruns && !rc; ++i) {
+    const int k = i % nplans;
+    ctx->stream = streams[k] ? (hipStream_t)streams[k] : ctx->own;
+    rc = sfs2d_plan_run_phase(plans[k], 0, outs ? outs[k] : nullptr);
+  }
+  ctx->stream = saved;
+  return rc;
+}
+
 int sfs2d_plan_bg_buffer(sfs2d_plan* pl, void** dev_ptr, int64_t* nbytes) {
   if (!pl || !dev_ptr || !nbytes) return SFS2D_E_ARG;
   // the replica buffer the next run's k_prep accumulates into (fused plans alternate two)

@@ -35,7 +35,7 @@ EXPORTS = [
     "sfs2d_plan_destroy", "sfs2d_scan", "sfs2d_plan_set_timing", "sfs2d_plan_timing_read",
     "sfs2d_plan_stats", "sfs2d_plan_grids", "sfs2d_plan_attach", "sfs2d_data_synth_sims",
     "sfs2d_data_read", "sfs2d_dist_unique_id", "sfs2d_dist_create", "sfs2d_dist_scan_gather",
-    "sfs2d_dist_destroy", "sfs2d_dist_set_gather",
+    "sfs2d_dist_destroy", "sfs2d_dist_set_gather", "sfs2d_plan_run_streams",
 ]
 
 
@@ -102,6 +102,7 @@ def lib():
     L.sfs2d_plan_set_background.argtypes = [vp, vp, vp, vp]
     L.sfs2d_plan_run.argtypes = [vp, vp]
     L.sfs2d_plan_run_many.argtypes = [vp, C.c_int, vp]
+    L.sfs2d_plan_run_streams.argtypes = [vp, vp, vp, C.c_int, C.c_int]
     L.sfs2d_plan_set_timing_sampled.argtypes = [vp, C.c_int, C.c_int]
     L.sfs2d_plan_set_timing_kernels.argtypes = [vp, C.c_int, C.c_int, C.c_int]
     L.sfs2d_plan_fst_read.argtypes = [vp, vp, i64]

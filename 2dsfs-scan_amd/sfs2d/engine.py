@@ -215,6 +215,18 @@ class Plan:
         self.eng.check(self.eng.lib.sfs2d_plan_run_many(self.h, int(nruns),
                                                         C.c_void_p(out_dev_ptr) if out_dev_ptr else None))
 
+    @staticmethod
+    def run_streams(plans, streams, nruns: int, out_dev_ptrs=None):
+        """Enqueue `nruns` runs round-robin over distinct plans of one engine, run i on
+        streams[i % len(plans)] (HIP stream handles; 0/None = the engine's stream)
+        (sfs2d_plan_run_streams: independent scans overlap across the streams)."""
+        k = len(plans)
+        ph = (C.c_void_p * k)(*[p.h.value for p in plans])
+        sh = (C.c_void_p * k)(*[s or None for s in streams])
+        oh = (C.c_void_p * k)(*[o or None for o in out_dev_ptrs]) if out_dev_ptrs else None
+        eng = plans[0].eng
+        eng.check(eng.lib.sfs2d_plan_run_streams(ph, sh, oh, k, int(nruns)))
+
     def check(self):
         self.eng.check(self.eng.lib.sfs2d_plan_check(self.h))
 

@@ -132,7 +132,8 @@ def hbm_stream_roofline(eng, steps=5):
            "pipeline_bytes_note": "SURVEY 8(d): 12 B/SNP + 64 B/window per run over the wall time of back-to-back runs",
            "windows": nwin, "windows_per_s": nwin / tk,
            "workload": "config 3 stream on 1 GPU: 32 chrom x 1.5625e6 SNPs, 20 kb, per-chromosome bg"}
-    pl.close()
+    for q in plans[::-1]:
+        q.close()
     dev.close()
     return out
 
@@ -147,6 +148,9 @@ def main():
     ap.add_argument("--dist-loop", action="store_true",
                     help="diagnostic: the N>1 step loop (scan + RCCL all-gather per step) even on one rank")
     ap.add_argument("--py-loop", action="store_true", help="diagnostic: the Python N>1 step loop instead of the native one")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="N=1: consecutive steps round-robin over this many plans, each on its own HIP stream "
+                         "(independent passes overlap; sfs2d_plan_run_streams)")
     args = ap.parse_args()
 
     import torch
@@ -163,7 +167,7 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world)
 
     from sfs2d import _lib as L
-    from sfs2d.engine import Engine, ScanConfig
+    from sfs2d.engine import Engine, Plan, ScanConfig
     from sfs2d.synth import synth_genome
 
     p = synth_genome(1, N_SNP, POP, POP, seed=12345 + rank)
@@ -183,7 +187,10 @@ def main():
         rows = int(c.item())
     else:
         rows = nrec
-    outs = [torch.zeros((rows, 64), dtype=torch.uint8, device=cdev) for _ in range(2)]
+    ns = 1 if dl else max(1, args.streams)
+    plans = [pl] + [eng.plan(dev, ScanConfig(n1p=POP, n2p=POP, window=WS, fst=True)) for _ in range(ns - 1)]
+    sstreams = [scan_s.cuda_stream] + [torch.cuda.Stream(device=local).cuda_stream for _ in range(ns - 1)]
+    outs = [torch.zeros((rows, 64), dtype=torch.uint8, device=cdev) for _ in range(max(2, ns))]
     for o in outs:
         o[nrec:, 39] = 0x80   # padding rows: flags = SFS2D_W_EMPTY
     gathered = [torch.empty((world * rows, 64), dtype=torch.uint8, device=cdev) for _ in range(2)] if dl else None
@@ -275,6 +282,8 @@ def main():
     elif dl:
         for i in range(args.warmup):
             step(i)
+    elif ns > 1:
+        Plan.run_streams(plans, sstreams, args.warmup * ns, optrs[:ns])
     else:
         pl.run_many(args.warmup, out.data_ptr())
     # HIP events around the scan kernel (the roofline's) and k_bg_slice of every 8th timed run, on the
@@ -288,7 +297,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if not dl:
+    if ns > 1:
+        Plan.run_streams(plans, sstreams, args.steps, optrs[:ns])   # run i: plan i % ns on stream i % ns
+    elif not dl:
         pl.run_many(args.steps, out.data_ptr())   # enqueued from C: no host work between steps
     elif nat is not None:
         nat.scan_gather(pl, optrs, gptrs, rows, first_timed, args.steps, gather_on)
@@ -309,6 +320,10 @@ def main():
     _, (k1, _, k3_untimed) = pl.timing_read()
     pl.set_timing(0)
     pl.check()
+    for k in range(1, ns):   # every plan's last pass wrote the same records (independent per-run state)
+        plans[k].check()
+        if not torch.equal(outs[k][:nrec], out[:nrec]):
+            raise RuntimeError(f"plan {k} on stream {k} disagrees with plan 0")
     recs = np.frombuffer(out[:nrec].cpu().numpy().tobytes(), dtype=L.WINDOW_DTYPE)
     nwin_rank = int(((recs["flags"] & L.W_EMPTY) == 0).sum())
     total_windows = nwin_rank
@@ -338,7 +353,9 @@ def main():
                                       + ("gather to rank 0" if gather_root else "all-gather")
                                       + (f" per step ({'native' if nat is not None else 'Python'} step loop"
                                          + ("" if nat is None else ", gathers " + ("overlapped on a comm stream" if gather_on else "serial on the scan stream"))
-                                         + ")" if dl else "")},
+                                         + ")" if dl else "")
+                                      + (f"; {ns} plans on {ns} HIP streams, steps round-robin (passes overlap)"
+                                         if ns > 1 else "")},
             "kernels_ms": {"k_prep": k1, "k_bg_slice": k2, "k_scan_w": k3, "k_scan_w_untimed_pass": k3_untimed,
                            "timed_runs_sampled": nr, "exact_path_windows": pl.stats(),
                            "note": "k_bg_slice / k_scan_w: events in every 8th timed run; k_prep: 16 runs after "
@@ -361,7 +378,8 @@ def main():
         print(json.dumps(line), flush=True)
     if nat is not None:
         nat.close()
-    pl.close()
+    for q in plans[::-1]:
+        q.close()
     dev.close()
     if dl:
         dist.destroy_process_group()

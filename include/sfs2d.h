@@ -151,6 +151,12 @@ int sfs2d_plan_set_background(sfs2d_plan* plan, const double* bg2d, const double
 int sfs2d_plan_run(sfs2d_plan* plan, sfs2d_window* out_dev);
 /* enqueue `nruns` back-to-back runs (no host work in between; benchmarks and batch replays) */
 int sfs2d_plan_run_many(sfs2d_plan* plan, int nruns, sfs2d_window* out_dev);
+/* enqueue `nruns` runs round-robin over `nplans` distinct plans of one ctx: run i is plans[i % nplans]
+ * on streams[i % nplans] (NULL = the ctx's own stream) into outs[i % nplans] (outs NULL or an entry
+ * NULL = plan-owned).  Independent scans (replicates, data sets, repeated passes) overlap across the
+ * streams; each plan's own runs stay ordered on its stream.  The ctx stream is restored after. */
+int sfs2d_plan_run_streams(sfs2d_plan* const* plans, void* const* streams, sfs2d_window* const* outs, int nplans,
+                           int nruns);
 /* copy the last run's records to host (synchronises the stream) */
 int sfs2d_plan_read(sfs2d_plan* plan, sfs2d_window* out_host, int64_t cap, int64_t* nrec_out);
 /* device pointers of the plan's per-chromosome background histogram replicas (uint32), for a

@@ -196,6 +196,41 @@ def test_plan_replay_is_deterministic():
     pl.close()
 
 
+@pytest.mark.parametrize("fst", [False, True])
+def test_run_streams_overlapped_plans(fst):
+    """sfs2d_plan_run_streams: passes round-robin over plans on their own HIP streams (overlapping)
+    write the same records and Fst as one plan run alone; argument errors are reported."""
+    import torch
+    from sfs2d import _lib as L
+    from sfs2d.engine import Engine, Plan, ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(1, 200000, 25, 25, seed=4242)
+    eng = Engine.get(0)
+    dev = eng.upload(p)
+    cfg = ScanConfig(n1p=25, n2p=25, window=20000, fst=fst)
+    ref = eng.plan(dev, cfg)
+    ref.run()
+    ref.check()
+    want = ref.read()
+    want_f = ref.read_fst() if fst else None
+    plans = [eng.plan(dev, cfg) for _ in range(3)]
+    streams = [torch.cuda.Stream(device=0).cuda_stream for _ in range(3)]
+    outs = [torch.zeros((plans[0].nrec, 64), dtype=torch.uint8, device="cuda:0") for _ in range(3)]
+    Plan.run_streams(plans, streams, 3 * 5 + 1, [o.data_ptr() for o in outs])
+    torch.cuda.synchronize()
+    for k, q in enumerate(plans):
+        q.check()
+        got = np.frombuffer(outs[k].cpu().numpy().tobytes(), dtype=L.WINDOW_DTYPE)
+        assert got.tobytes() == want.tobytes(), k
+        if fst:
+            assert np.array_equal(q.read_fst(), want_f, equal_nan=True), k
+    with pytest.raises(L.Sfs2dError):
+        Plan.run_streams([plans[0], plans[0]], streams[:2], 2)
+    for q in plans + [ref]:
+        q.close()
+    dev.close()
+
+
 def test_key_error_on_counts_above_sample_size():
     import twoDSFS_class as T
     d = {"c-1": {"calls": {"uv": (0, 3), "bv": (2, 0)}, "annotation": "x"},
