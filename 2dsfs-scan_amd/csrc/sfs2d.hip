@@ -1553,6 +1553,42 @@ int sfs2d_dist_scan_gather(sfs2d_dist* d, sfs2d_plan* pl, void* out0, void* out1
   return 0;
 }
 
+int sfs2d_dist_scan_gather_streams(sfs2d_dist* const* dists, sfs2d_plan* const* plans, void* const* streams,
+                                   void* const* outs, void* const* gathered, int nplans, int64_t rows, int nsteps) {
+  if (!dists || !plans || !streams || !outs || !gathered || nplans < 1 || nsteps < 0 || !dists[0])
+    return SFS2D_E_ARG;
+  sfs2d_ctx* ctx = dists[0]->ctx;
+  for (int k = 0; k < nplans; ++k) {
+    if (!dists[k] || !plans[k] || !outs[k] || !gathered[k] || dists[k]->ctx != ctx || plans[k]->ctx != ctx ||
+        rows < plans[k]->nrec)
+      return set_err(ctx, SFS2D_E_ARG, "bad argument (one ctx; rows must cover every plan's records)");
+    for (int j = 0; j < k; ++j)
+      if (plans[j] == plans[k] || dists[j] == dists[k] || streams[j] == streams[k])
+        return set_err(ctx, SFS2D_E_ARG, "plans, communicators and streams must be distinct");
+  }
+  RcclApi& r = rccl();
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  // step i: plan k = i % nplans scans into outs[k] and its table is gathered through communicator k,
+  // both on streams[k]: each stream is a serial scan -> gather chain of its own (no cross-stream
+  // event), and every communicator sees its collectives in the same order on every rank
+  hipStream_t saved = ctx->stream;
+  const size_t bytes = (size_t)rows * sizeof(sfs2d_window);
+  int rc = 0;
+  for (int i = 0; i < nsteps && !rc; ++i) {
+    const int k = i % nplans;
+    hipStream_t st = streams[k] ? (hipStream_t)streams[k] : ctx->own;
+    ctx->stream = st;
+    if ((rc = sfs2d_plan_run(plans[k], static_cast<sfs2d_window*>(outs[k])))) break;
+    sfs2d_dist* d = dists[k];
+    const ncclResult_t e = d->to_root ? r.gather(outs[k], gathered[k], bytes, ncclUint8, 0, d->comm, st)
+                                      : r.all_gather(outs[k], gathered[k], bytes, ncclUint8, d->comm, st);
+    if (e != ncclSuccess)
+      rc = set_err(ctx, SFS2D_E_HIP, std::string(d->to_root ? "ncclGather: " : "ncclAllGather: ") + r.errstr(e));
+  }
+  ctx->stream = saved;
+  return rc;
+}
+
 int sfs2d_dist_set_gather(sfs2d_dist* d, int to_root) {
   if (!d) return SFS2D_E_ARG;
   if (to_root && !rccl().gather) return set_err(d->ctx, SFS2D_E_ARG, "the loaded RCCL has no ncclGather");

@@ -36,6 +36,7 @@ EXPORTS = [
     "sfs2d_plan_stats", "sfs2d_plan_grids", "sfs2d_plan_attach", "sfs2d_data_synth_sims",
     "sfs2d_data_read", "sfs2d_dist_unique_id", "sfs2d_dist_create", "sfs2d_dist_scan_gather",
     "sfs2d_dist_destroy", "sfs2d_dist_set_gather", "sfs2d_plan_run_streams",
+    "sfs2d_dist_scan_gather_streams",
 ]
 
 
@@ -123,6 +124,7 @@ def lib():
     L.sfs2d_dist_create.argtypes = [vp, vp, i32, i32, C.POINTER(vp)]
     L.sfs2d_dist_scan_gather.argtypes = [vp, vp, vp, vp, vp, vp, i64, i64, C.c_int, vp]
     L.sfs2d_dist_destroy.argtypes = [vp]
+    L.sfs2d_dist_scan_gather_streams.argtypes = [vp, vp, vp, vp, vp, C.c_int, i64, C.c_int]
     L.sfs2d_dist_set_gather.argtypes = [vp, C.c_int]
     L.sfs2d_plan_timing_read.argtypes = [vp, C.POINTER(C.c_int)] + [C.POINTER(C.c_double)] * 3
     L.sfs2d_scan.argtypes = [vp, vp, C.POINTER(Params), vp, vp, vp, vp, i64, C.POINTER(i64)]

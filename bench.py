@@ -167,7 +167,7 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world)
 
     from sfs2d import _lib as L
-    from sfs2d.engine import Engine, Plan, ScanConfig
+    from sfs2d.engine import Dist, Engine, Plan, ScanConfig
     from sfs2d.synth import synth_genome
 
     p = synth_genome(1, N_SNP, POP, POP, seed=12345 + rank)
@@ -187,22 +187,24 @@ def main():
         rows = int(c.item())
     else:
         rows = nrec
-    ns = 1 if dl else max(1, args.streams)
+    ns = max(1, args.streams)   # (N > 1: falls back to 1 without the native step loop)
     plans = [pl] + [eng.plan(dev, ScanConfig(n1p=POP, n2p=POP, window=WS, fst=True)) for _ in range(ns - 1)]
     sstreams = [scan_s.cuda_stream] + [torch.cuda.Stream(device=local).cuda_stream for _ in range(ns - 1)]
     outs = [torch.zeros((rows, 64), dtype=torch.uint8, device=cdev) for _ in range(max(2, ns))]
     for o in outs:
         o[nrec:, 39] = 0x80   # padding rows: flags = SFS2D_W_EMPTY
-    gathered = [torch.empty((world * rows, 64), dtype=torch.uint8, device=cdev) for _ in range(2)] if dl else None
+    gathered = [torch.empty((world * rows, 64), dtype=torch.uint8, device=cdev) for _ in range(max(2, ns))] if dl else None
     # the step loop runs in the native library (sfs2d_dist_scan_gather: its own RCCL communicator, the
     # scans and all-gathers enqueued from C); the Python loop below is the fallback
     nat = None
     gather_root = False
     if dl:
-        hdr = torch.zeros(129, dtype=torch.uint8)
+        # one RCCL communicator per stream (each stream's scan -> gather chain is its own)
+        hdr = torch.zeros(1 + 128 * ns, dtype=torch.uint8)
         if rank == 0:
             try:
-                hdr[1:] = torch.tensor(list(eng.dist_unique_id()), dtype=torch.uint8)
+                for k in range(ns):
+                    hdr[1 + 128 * k:129 + 128 * k] = torch.tensor(list(eng.dist_unique_id()), dtype=torch.uint8)
                 hdr[0] = 1
             except Exception as e:  # noqa: BLE001
                 print(f"[bench] RCCL id unavailable ({e}): Python step loop", file=sys.stderr)
@@ -210,7 +212,8 @@ def main():
         dist.broadcast(hdr, 0)
         hdr = hdr.cpu()
         if int(hdr[0]) == 1 and not args.py_loop:
-            nat = eng.dist(bytes(hdr[1:].tolist()), rank, world)
+            nats = [eng.dist(bytes(hdr[1 + 128 * k:129 + 128 * k].tolist()), rank, world) for k in range(ns)]
+            nat = nats[0]
             # one ncclGather of the window tables to rank 0 per step (their one consumer),
             # ncclAllGather where the loaded RCCL lacks it or SFS2D_GATHER=all; the same on every rank
             to_root = os.environ.get("SFS2D_GATHER", "root") != "all"
@@ -222,7 +225,13 @@ def main():
                     ok.zero_()
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
             gather_root = bool(int(ok.item()))
-            nat.set_gather(gather_root)
+            for q in nats:
+                q.set_gather(gather_root)
+    if dl and nat is None and ns > 1:
+        ns = 1
+        for q in plans[1:]:
+            q.close()
+        plans, sstreams = plans[:1], sstreams[:1]
     ev_scan = [torch.cuda.Event() for _ in range(2)]
     ev_comm = [torch.cuda.Event() for _ in range(2)]
     for e in ev_comm:
@@ -249,35 +258,45 @@ def main():
     gather_on = None
     if nat is not None:
         # the warmup times both gather placements (overlapped on the comm stream with events, or
-        # serial on the scan stream) and every rank keeps the faster by the max over ranks
+        # serial on the scan stream) and every rank keeps the faster by the max over ranks; with
+        # several streams each stream's scan -> gather chain is serial (no placement to choose)
+        def run_dist(cs, first, n):
+            if ns > 1:
+                Dist.scan_gather_streams(nats, plans, sstreams, optrs[:ns], gptrs[:ns], rows, n)
+            else:
+                nat.scan_gather(pl, optrs, gptrs, rows, first, n, cs)
+
         def timed(cs, first, n):
             torch.cuda.synchronize()
             dist.barrier()
             t = time.perf_counter()
-            nat.scan_gather(pl, optrs, gptrs, rows, first, n, cs)
+            run_dist(cs, first, n)
             torch.cuda.synchronize()
             tt = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=cdev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             return float(tt.item())
         # (a few serial steps first absorb the first-call costs; overlapped must win by 10%: on one
         # GPU it lost, 44-59 vs 32 us per step, and short samples are noisy)
-        pre = 4
-        nat.scan_gather(pl, optrs, gptrs, rows, 0, pre, None)
-        wh = max(20, args.warmup)
+        pre = 4 * ns
+        run_dist(None, 0, pre)
+        wh = max(20, args.warmup) * ns
         step_no = pre
         if gather_root:
             # gather to rank 0 vs all-gather, both serial: the faster one stays (on one rank the
             # ncclGather's grouped send / receive cost 37 vs 30 us per step; at N > 1 it moves 1/N
             # of the all-gather's bytes)
             t_root = timed(None, step_no, wh)
-            nat.set_gather(False)
+            for q in nats:
+                q.set_gather(False)
             t_all = timed(None, step_no + wh, wh)
             step_no += 2 * wh
             gather_root = t_root < t_all
-            nat.set_gather(gather_root)
-        t_se = timed(None, step_no, wh)
-        t_ov = timed(comm_s.cuda_stream, step_no + wh, wh)
-        gather_on = comm_s.cuda_stream if t_ov < 0.9 * t_se else None
+            for q in nats:
+                q.set_gather(gather_root)
+        if ns == 1:
+            t_se = timed(None, step_no, wh)
+            t_ov = timed(comm_s.cuda_stream, step_no + wh, wh)
+            gather_on = comm_s.cuda_stream if t_ov < 0.9 * t_se else None
         first_timed = step_no + 2 * wh
     elif dl:
         for i in range(args.warmup):
@@ -297,12 +316,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if ns > 1:
+    if nat is not None:
+        run_dist(gather_on, first_timed, args.steps)
+    elif ns > 1:
         Plan.run_streams(plans, sstreams, args.steps, optrs[:ns])   # run i: plan i % ns on stream i % ns
     elif not dl:
         pl.run_many(args.steps, out.data_ptr())   # enqueued from C: no host work between steps
-    elif nat is not None:
-        nat.scan_gather(pl, optrs, gptrs, rows, first_timed, args.steps, gather_on)
     else:
         for i in range(args.steps):
             step(i)
@@ -377,7 +396,8 @@ def main():
             line["cpu_baseline"] = cpu_baseline(p)
         print(json.dumps(line), flush=True)
     if nat is not None:
-        nat.close()
+        for q in nats:
+            q.close()
     for q in plans[::-1]:
         q.close()
     dev.close()

@@ -44,3 +44,49 @@ def test_single_rank_scan_gather():
     finally:
         d.close()
         pl.close()
+
+
+def test_single_rank_scan_gather_streams():
+    """sfs2d_dist_scan_gather_streams: two plans, two one-rank communicators, two streams; every
+    gathered table equals the plan's own records (to the root and all-gathered); argument errors."""
+    import torch
+    from sfs2d import _lib as L
+    from sfs2d.engine import Dist, Engine, ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(2, [30000, 9000], 25, 25, seed=22)
+    eng = Engine.get(0)
+    dev = eng.upload(p)
+    cfg = ScanConfig(n1p=25, n2p=25, window=20000, fst=True)
+    plans = [eng.plan(dev, cfg) for _ in range(2)]
+    plans[0].run()
+    plans[0].check()
+    ref = plans[0].read()
+    rows = plans[0].nrec + 2
+    outs = [torch.zeros((rows, 64), dtype=torch.uint8, device="cuda:0") for _ in range(2)]
+    gath = [torch.full((rows, 64), 7, dtype=torch.uint8, device="cuda:0") for _ in range(2)]
+    streams = [torch.cuda.Stream(device=0).cuda_stream for _ in range(2)]
+    ds = [eng.dist(eng.dist_unique_id(), 0, 1) for _ in range(2)]
+    op = [o.data_ptr() for o in outs]
+    gp = [g.data_ptr() for g in gath]
+    try:
+        for root in (True, False):
+            for d in ds:
+                d.set_gather(root)
+            for g in gath:
+                g.fill_(7)
+            Dist.scan_gather_streams(ds, plans, streams, op, gp, rows, 7)
+            torch.cuda.synchronize()
+            for q, o, g in zip(plans, outs, gath):
+                q.check()
+                assert torch.equal(o, g)
+                recs = np.frombuffer(o[: q.nrec].cpu().numpy().tobytes(), dtype=L.WINDOW_DTYPE)
+                assert recs.tobytes() == ref.tobytes()
+        with pytest.raises(L.Sfs2dError):   # one communicator twice
+            Dist.scan_gather_streams([ds[0], ds[0]], plans, streams, op, gp, rows, 1)
+        with pytest.raises(L.Sfs2dError):   # rows must cover the records
+            Dist.scan_gather_streams(ds, plans, streams, op, gp, plans[0].nrec - 1, 1)
+    finally:
+        for d in ds:
+            d.close()
+        for q in plans:
+            q.close()
