@@ -1479,6 +1479,7 @@ struct sfs2d_dist {
   int rank = 0, world = 1;
   bool to_root = false;   // ncclGather to rank 0 (else ncclAllGather)
   hipEvent_t ev_scan[2] = {nullptr, nullptr}, ev_comm[2] = {nullptr, nullptr};
+  std::vector<hipEvent_t> ev_k;   // sfs2d_dist_scan_gather_streams: per-stream scan events, per-parity gather events
 };
 
 extern "C" {
@@ -1553,37 +1554,56 @@ int sfs2d_dist_scan_gather(sfs2d_dist* d, sfs2d_plan* pl, void* out0, void* out1
   return 0;
 }
 
-int sfs2d_dist_scan_gather_streams(sfs2d_dist* const* dists, sfs2d_plan* const* plans, void* const* streams,
-                                   void* const* outs, void* const* gathered, int nplans, int64_t rows, int nsteps) {
-  if (!dists || !plans || !streams || !outs || !gathered || nplans < 1 || nsteps < 0 || !dists[0])
-    return SFS2D_E_ARG;
-  sfs2d_ctx* ctx = dists[0]->ctx;
+int sfs2d_dist_scan_gather_streams(sfs2d_dist* d, sfs2d_plan* const* plans, void* const* streams, int nplans,
+                                   void* outbuf, void* gathered0, void* gathered1, int64_t rows, int nsteps) {
+  if (!d || !plans || !streams || !outbuf || !gathered0 || !gathered1 || nplans < 1 || nplans > 16 || nsteps < 0)
+    return set_err(d ? d->ctx : nullptr, SFS2D_E_ARG, "bad argument");
+  sfs2d_ctx* ctx = d->ctx;
   for (int k = 0; k < nplans; ++k) {
-    if (!dists[k] || !plans[k] || !outs[k] || !gathered[k] || dists[k]->ctx != ctx || plans[k]->ctx != ctx ||
-        rows < plans[k]->nrec)
-      return set_err(ctx, SFS2D_E_ARG, "bad argument (one ctx; rows must cover every plan's records)");
+    if (!plans[k] || plans[k]->ctx != ctx || rows < plans[k]->nrec)
+      return set_err(ctx, SFS2D_E_ARG, "bad argument (plans of this ctx; rows must cover every plan's records)");
     for (int j = 0; j < k; ++j)
-      if (plans[j] == plans[k] || dists[j] == dists[k] || streams[j] == streams[k])
-        return set_err(ctx, SFS2D_E_ARG, "plans, communicators and streams must be distinct");
+      if (plans[j] == plans[k] || streams[j] == streams[k])
+        return set_err(ctx, SFS2D_E_ARG, "plans and streams must be distinct");
   }
   RcclApi& r = rccl();
   HIPCHK(ctx, hipSetDevice(ctx->device));
-  // step i: plan k = i % nplans scans into outs[k] and its table is gathered through communicator k,
-  // both on streams[k]: each stream is a serial scan -> gather chain of its own (no cross-stream
-  // event), and every communicator sees its collectives in the same order on every rank
+  while ((int)d->ev_k.size() < 2 * nplans) {
+    hipEvent_t e = nullptr;
+    HIPCHK(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    d->ev_k.push_back(e);
+  }
+  // Steps in groups of nplans: in group g, plan k scans on streams[k] into table (g & 1) * nplans + k
+  // of outbuf; streams[0] waits for the group's other scans and gathers the group's tables (one
+  // collective, m * rows records per rank) into gathered[g & 1]; a stream k > 0 waits for the gather
+  // of group g - 2 (which read the tables it is about to overwrite).  One communicator, one stream
+  // for its collectives; cross-stream waits: 2 (nplans - 1) per group.
+  auto st = [&](int k) { return streams[k] ? (hipStream_t)streams[k] : ctx->own; };
   hipStream_t saved = ctx->stream;
-  const size_t bytes = (size_t)rows * sizeof(sfs2d_window);
+  const size_t rec = sizeof(sfs2d_window);
+  void* gath[2] = {gathered0, gathered1};
   int rc = 0;
-  for (int i = 0; i < nsteps && !rc; ++i) {
-    const int k = i % nplans;
-    hipStream_t st = streams[k] ? (hipStream_t)streams[k] : ctx->own;
-    ctx->stream = st;
-    if ((rc = sfs2d_plan_run(plans[k], static_cast<sfs2d_window*>(outs[k])))) break;
-    sfs2d_dist* d = dists[k];
-    const ncclResult_t e = d->to_root ? r.gather(outs[k], gathered[k], bytes, ncclUint8, 0, d->comm, st)
-                                      : r.all_gather(outs[k], gathered[k], bytes, ncclUint8, d->comm, st);
-    if (e != ncclSuccess)
+  for (int64_t g = 0, done = 0; done < nsteps && !rc; ++g) {
+    const int m = (int)std::min<int64_t>(nplans, nsteps - done);
+    const int par = (int)(g & 1);
+    char* base = static_cast<char*>(outbuf) + (size_t)par * nplans * rows * rec;
+    for (int k = 0; k < m && !rc; ++k) {
+      ctx->stream = st(k);
+      if (k > 0 && g >= 2) HIPCHK(ctx, hipStreamWaitEvent(st(k), d->ev_k[nplans + par], 0));
+      if ((rc = sfs2d_plan_run(plans[k], reinterpret_cast<sfs2d_window*>(base + (size_t)k * rows * rec)))) break;
+      if (k > 0) HIPCHK(ctx, hipEventRecord(d->ev_k[k], st(k)));
+    }
+    if (rc) break;
+    for (int k = 1; k < m; ++k) HIPCHK(ctx, hipStreamWaitEvent(st(0), d->ev_k[k], 0));
+    const size_t bytes = (size_t)m * rows * rec;
+    const ncclResult_t e = d->to_root ? r.gather(base, gath[par], bytes, ncclUint8, 0, d->comm, st(0))
+                                      : r.all_gather(base, gath[par], bytes, ncclUint8, d->comm, st(0));
+    if (e != ncclSuccess) {
       rc = set_err(ctx, SFS2D_E_HIP, std::string(d->to_root ? "ncclGather: " : "ncclAllGather: ") + r.errstr(e));
+      break;
+    }
+    HIPCHK(ctx, hipEventRecord(d->ev_k[nplans + par], st(0)));
+    done += m;
   }
   ctx->stream = saved;
   return rc;
@@ -1602,6 +1622,7 @@ int sfs2d_dist_destroy(sfs2d_dist* d) {
     if (d->ev_scan[b]) hipEventDestroy(d->ev_scan[b]);
     if (d->ev_comm[b]) hipEventDestroy(d->ev_comm[b]);
   }
+  for (hipEvent_t e : d->ev_k) hipEventDestroy(e);
   if (d->comm) rccl().destroy(d->comm);
   delete d;
   return 0;

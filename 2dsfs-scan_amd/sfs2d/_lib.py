@@ -124,7 +124,7 @@ def lib():
     L.sfs2d_dist_create.argtypes = [vp, vp, i32, i32, C.POINTER(vp)]
     L.sfs2d_dist_scan_gather.argtypes = [vp, vp, vp, vp, vp, vp, i64, i64, C.c_int, vp]
     L.sfs2d_dist_destroy.argtypes = [vp]
-    L.sfs2d_dist_scan_gather_streams.argtypes = [vp, vp, vp, vp, vp, C.c_int, i64, C.c_int]
+    L.sfs2d_dist_scan_gather_streams.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, i64, C.c_int]
     L.sfs2d_dist_set_gather.argtypes = [vp, C.c_int]
     L.sfs2d_plan_timing_read.argtypes = [vp, C.POINTER(C.c_int)] + [C.POINTER(C.c_double)] * 3
     L.sfs2d_scan.argtypes = [vp, vp, C.POINTER(Params), vp, vp, vp, vp, i64, C.POINTER(i64)]

@@ -309,16 +309,16 @@ class Dist:
             self.h, plan.h, C.c_void_p(outs[0]), C.c_void_p(outs[1]), C.c_void_p(gathered[0]),
             C.c_void_p(gathered[1]), rows, first_step, nsteps, C.c_void_p(comm_stream) if comm_stream else None))
 
-    @staticmethod
-    def scan_gather_streams(dists, plans, streams, outs, gathered, rows: int, nsteps: int):
-        """Step s: plans[s % k] scans into outs[s % k], gathered through dists[s % k] into
-        gathered[s % k], both on streams[s % k] (k distinct plans / communicators / streams)."""
+    def scan_gather_streams(self, plans, streams, outbuf: int, gathered, rows: int, nsteps: int):
+        """Steps in groups of k = len(plans): plan j scans on streams[j] into table
+        (group & 1) * k + j of outbuf (2 k rows records), then one gather of the group's tables into
+        gathered[group & 1] (world * k * rows records) on streams[0] (sfs2d_dist_scan_gather_streams)."""
         k = len(plans)
-        arr = lambda xs: (C.c_void_p * k)(*[x or None for x in xs])  # noqa: E731
-        eng = dists[0].eng
-        eng.check(eng.lib.sfs2d_dist_scan_gather_streams(arr([d.h.value for d in dists]), arr([p.h.value for p in plans]),
-                                                         arr(streams), arr(outs), arr(gathered), k, int(rows),
-                                                         int(nsteps)))
+        ph = (C.c_void_p * k)(*[p.h.value for p in plans])
+        sh = (C.c_void_p * k)(*[x or None for x in streams])
+        self.eng.check(self.eng.lib.sfs2d_dist_scan_gather_streams(self.h, ph, sh, k, C.c_void_p(outbuf),
+                                                                   C.c_void_p(gathered[0]), C.c_void_p(gathered[1]),
+                                                                   int(rows), int(nsteps)))
 
     def set_gather(self, to_root: bool):
         """True: ncclGather to rank 0 (the default where RCCL has it); False: ncclAllGather."""

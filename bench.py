@@ -148,7 +148,7 @@ def main():
     ap.add_argument("--dist-loop", action="store_true",
                     help="diagnostic: the N>1 step loop (scan + RCCL all-gather per step) even on one rank")
     ap.add_argument("--py-loop", action="store_true", help="diagnostic: the Python N>1 step loop instead of the native one")
-    ap.add_argument("--streams", type=int, default=1,
+    ap.add_argument("--streams", type=int, default=2,
                     help="N=1: consecutive steps round-robin over this many plans, each on its own HIP stream "
                          "(independent passes overlap; sfs2d_plan_run_streams)")
     args = ap.parse_args()
@@ -167,7 +167,7 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world)
 
     from sfs2d import _lib as L
-    from sfs2d.engine import Dist, Engine, Plan, ScanConfig
+    from sfs2d.engine import Engine, Plan, ScanConfig
     from sfs2d.synth import synth_genome
 
     p = synth_genome(1, N_SNP, POP, POP, seed=12345 + rank)
@@ -193,18 +193,20 @@ def main():
     outs = [torch.zeros((rows, 64), dtype=torch.uint8, device=cdev) for _ in range(max(2, ns))]
     for o in outs:
         o[nrec:, 39] = 0x80   # padding rows: flags = SFS2D_W_EMPTY
-    gathered = [torch.empty((world * rows, 64), dtype=torch.uint8, device=cdev) for _ in range(max(2, ns))] if dl else None
+    gathered = [torch.empty((world * rows * ns, 64), dtype=torch.uint8, device=cdev) for _ in range(2)] if dl else None
+    # N > 1 with several streams: the group's tables are contiguous (one gather per group of ns steps)
+    outbuf = torch.zeros((2 * ns * rows, 64), dtype=torch.uint8, device=cdev) if dl and ns > 1 else None
+    if outbuf is not None:
+        outbuf.view(2 * ns, rows, 64)[:, nrec:, 39] = 0x80
     # the step loop runs in the native library (sfs2d_dist_scan_gather: its own RCCL communicator, the
     # scans and all-gathers enqueued from C); the Python loop below is the fallback
     nat = None
     gather_root = False
     if dl:
-        # one RCCL communicator per stream (each stream's scan -> gather chain is its own)
-        hdr = torch.zeros(1 + 128 * ns, dtype=torch.uint8)
+        hdr = torch.zeros(129, dtype=torch.uint8)
         if rank == 0:
             try:
-                for k in range(ns):
-                    hdr[1 + 128 * k:129 + 128 * k] = torch.tensor(list(eng.dist_unique_id()), dtype=torch.uint8)
+                hdr[1:] = torch.tensor(list(eng.dist_unique_id()), dtype=torch.uint8)
                 hdr[0] = 1
             except Exception as e:  # noqa: BLE001
                 print(f"[bench] RCCL id unavailable ({e}): Python step loop", file=sys.stderr)
@@ -212,8 +214,8 @@ def main():
         dist.broadcast(hdr, 0)
         hdr = hdr.cpu()
         if int(hdr[0]) == 1 and not args.py_loop:
-            nats = [eng.dist(bytes(hdr[1 + 128 * k:129 + 128 * k].tolist()), rank, world) for k in range(ns)]
-            nat = nats[0]
+            nat = eng.dist(bytes(hdr[1:].tolist()), rank, world)
+            nats = [nat]
             # one ncclGather of the window tables to rank 0 per step (their one consumer),
             # ncclAllGather where the loaded RCCL lacks it or SFS2D_GATHER=all; the same on every rank
             to_root = os.environ.get("SFS2D_GATHER", "root") != "all"
@@ -228,7 +230,7 @@ def main():
             for q in nats:
                 q.set_gather(gather_root)
     if dl and nat is None and ns > 1:
-        ns = 1
+        ns, outbuf = 1, None
         for q in plans[1:]:
             q.close()
         plans, sstreams = plans[:1], sstreams[:1]
@@ -256,48 +258,61 @@ def main():
     optrs = [o.data_ptr() for o in outs]
     gptrs = [g.data_ptr() for g in gathered] if dl else None
     gather_on = None
+    dist_times = None
+    STREAMS_MODE = "streams"
+    timed_ns = ns
     if nat is not None:
         # the warmup times both gather placements (overlapped on the comm stream with events, or
         # serial on the scan stream) and every rank keeps the faster by the max over ranks; with
         # several streams each stream's scan -> gather chain is serial (no placement to choose)
-        def run_dist(cs, first, n):
-            if ns > 1:
-                Dist.scan_gather_streams(nats, plans, sstreams, optrs[:ns], gptrs[:ns], rows, n)
-            else:
-                nat.scan_gather(pl, optrs, gptrs, rows, first, n, cs)
+        STREAMS = STREAMS_MODE
 
-        def timed(cs, first, n):
+        def run_dist(mode, first, n):
+            # mode: STREAMS (steps in groups of ns over ns plans / streams, one gather per group), or
+            # the one-plan loop with its gathers serial (None) or on the comm stream
+            if mode == STREAMS:
+                nat.scan_gather_streams(plans, sstreams, outbuf.data_ptr(), gptrs, rows, n)
+            else:
+                nat.scan_gather(pl, optrs, gptrs, rows, first, n, mode)
+
+        def timed(mode, first, n):
             torch.cuda.synchronize()
             dist.barrier()
             t = time.perf_counter()
-            run_dist(cs, first, n)
+            run_dist(mode, first, n)
             torch.cuda.synchronize()
-            tt = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=cdev)
+            tt = torch.tensor([(time.perf_counter() - t) / n], dtype=torch.float64, device=cdev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             return float(tt.item())
         # (a few serial steps first absorb the first-call costs; overlapped must win by 10%: on one
         # GPU it lost, 44-59 vs 32 us per step, and short samples are noisy)
-        pre = 4 * ns
+        pre = 4
         run_dist(None, 0, pre)
-        wh = max(20, args.warmup) * ns
+        if ns > 1:
+            run_dist(STREAMS, 0, pre * ns)
+        wh = max(20, args.warmup)
         step_no = pre
         if gather_root:
             # gather to rank 0 vs all-gather, both serial: the faster one stays (on one rank the
             # ncclGather's grouped send / receive cost 37 vs 30 us per step; at N > 1 it moves 1/N
             # of the all-gather's bytes)
             t_root = timed(None, step_no, wh)
-            for q in nats:
-                q.set_gather(False)
+            nat.set_gather(False)
             t_all = timed(None, step_no + wh, wh)
             step_no += 2 * wh
             gather_root = t_root < t_all
-            for q in nats:
-                q.set_gather(gather_root)
-        if ns == 1:
-            t_se = timed(None, step_no, wh)
-            t_ov = timed(comm_s.cuda_stream, step_no + wh, wh)
-            gather_on = comm_s.cuda_stream if t_ov < 0.9 * t_se else None
-        first_timed = step_no + 2 * wh
+            nat.set_gather(gather_root)
+        # per-step times (max over ranks) of the placements; the streams loop must win by 5%, the
+        # overlapped one by 10%
+        t_se = timed(None, step_no, wh)
+        t_ov = timed(comm_s.cuda_stream, step_no + wh, wh)
+        step_no += 2 * wh
+        cand = [(t_se, None), (t_ov / 0.9, comm_s.cuda_stream)]
+        if ns > 1:
+            cand.append((timed(STREAMS, 0, wh * ns) / 0.95, STREAMS))
+        dist_times = {"serial": t_se, "overlapped": t_ov, "streams": cand[2][0] * 0.95 if ns > 1 else None}
+        gather_on = min(cand, key=lambda c: c[0])[1]
+        first_timed = step_no
     elif dl:
         for i in range(args.warmup):
             step(i)
@@ -318,6 +333,8 @@ def main():
     t0 = time.perf_counter()
     if nat is not None:
         run_dist(gather_on, first_timed, args.steps)
+        if gather_on != STREAMS_MODE:
+            timed_ns = 1   # (the report: one plan ran the timed steps)
     elif ns > 1:
         Plan.run_streams(plans, sstreams, args.steps, optrs[:ns])   # run i: plan i % ns on stream i % ns
     elif not dl:
@@ -339,9 +356,17 @@ def main():
     _, (k1, _, k3_untimed) = pl.timing_read()
     pl.set_timing(0)
     pl.check()
+    if outbuf is not None:   # the grouped dist loop wrote its tables into outbuf
+        tabs = outbuf.view(2 * ns, rows, 64)
+        for k in range(1, 2 * ns):
+            if not torch.equal(tabs[k][:nrec], tabs[0][:nrec]):
+                raise RuntimeError(f"table {k} of the grouped step loop disagrees with table 0")
+        if gather_on == STREAMS_MODE and (rank == 0 or not gather_root) and not torch.equal(gathered[0].view(world, ns * rows, 64)[rank][:nrec],
+                                                              tabs[0][:nrec]):
+            raise RuntimeError("gathered table disagrees with the local one")
     for k in range(1, ns):   # every plan's last pass wrote the same records (independent per-run state)
         plans[k].check()
-        if not torch.equal(outs[k][:nrec], out[:nrec]):
+        if outbuf is None and not torch.equal(outs[k][:nrec], out[:nrec]):
             raise RuntimeError(f"plan {k} on stream {k} disagrees with plan 0")
     recs = np.frombuffer(out[:nrec].cpu().numpy().tobytes(), dtype=L.WINDOW_DTYPE)
     nwin_rank = int(((recs["flags"] & L.W_EMPTY) == 0).sum())
@@ -371,10 +396,13 @@ def main():
                        "parallelism": f"windows sharded by chromosome over {world} GPU(s); RCCL "
                                       + ("gather to rank 0" if gather_root else "all-gather")
                                       + (f" per step ({'native' if nat is not None else 'Python'} step loop"
-                                         + ("" if nat is None else ", gathers " + ("overlapped on a comm stream" if gather_on else "serial on the scan stream"))
+                                         + ("" if nat is None else ", gathers " + ("one per group of steps over the plans' streams" if gather_on == STREAMS_MODE
+                                                                   else "overlapped on a comm stream" if gather_on
+                                                                   else "serial on the scan stream"))
                                          + ")" if dl else "")
-                                      + (f"; {ns} plans on {ns} HIP streams, steps round-robin (passes overlap)"
-                                         if ns > 1 else "")},
+                                      + (f"; {timed_ns} plans on {timed_ns} HIP streams, steps round-robin (passes overlap)"
+                                         if timed_ns > 1 else "")},
+            **({"dist_step_ms_by_placement": dist_times} if dist_times else {}),
             "kernels_ms": {"k_prep": k1, "k_bg_slice": k2, "k_scan_w": k3, "k_scan_w_untimed_pass": k3_untimed,
                            "timed_runs_sampled": nr, "exact_path_windows": pl.stats(),
                            "note": "k_bg_slice / k_scan_w: events in every 8th timed run; k_prep: 16 runs after "

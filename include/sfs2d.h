@@ -222,12 +222,14 @@ int sfs2d_dist_unique_id(uint8_t* id128);
 int sfs2d_dist_create(sfs2d_ctx* ctx, const uint8_t* id128, int rank, int world, sfs2d_dist** out);
 int sfs2d_dist_scan_gather(sfs2d_dist* d, sfs2d_plan* plan, void* out0, void* out1, void* gathered0,
                            void* gathered1, int64_t rows, int64_t first_step, int nsteps, void* comm_stream);
-/* sfs2d_dist_scan_gather_streams: the same loop over `nplans` distinct plans, communicators (one
- * sfs2d_dist per plan, each from its own unique id) and streams: step s runs plans[s % nplans] into
- * outs[s % nplans] and gathers it through dists[s % nplans] into gathered[s % nplans], both on
- * streams[s % nplans] (no cross-stream event; consecutive steps overlap across the streams). */
-int sfs2d_dist_scan_gather_streams(sfs2d_dist* const* dists, sfs2d_plan* const* plans, void* const* streams,
-                                   void* const* outs, void* const* gathered, int nplans, int64_t rows, int nsteps);
+/* sfs2d_dist_scan_gather_streams: the same loop with consecutive steps spread over `nplans`
+ * distinct plans on their own streams: steps go in groups of nplans, plan k of a group scanning on
+ * streams[k] into table (group & 1) * nplans + k of `outbuf` (2 * nplans * rows records); then ONE
+ * gather (or all-gather) of the group's tables (nplans * rows records per rank, rank-major) into
+ * gathered[group & 1] (world * nplans * rows records each) on streams[0].  A last partial group
+ * gathers its m < nplans tables.  One communicator; scans of a group overlap across the streams. */
+int sfs2d_dist_scan_gather_streams(sfs2d_dist* d, sfs2d_plan* const* plans, void* const* streams, int nplans,
+                                   void* outbuf, void* gathered0, void* gathered1, int64_t rows, int nsteps);
 int sfs2d_dist_set_gather(sfs2d_dist* d, int to_root);
 int sfs2d_dist_destroy(sfs2d_dist* d);
 

@@ -47,11 +47,12 @@ def test_single_rank_scan_gather():
 
 
 def test_single_rank_scan_gather_streams():
-    """sfs2d_dist_scan_gather_streams: two plans, two one-rank communicators, two streams; every
-    gathered table equals the plan's own records (to the root and all-gathered); argument errors."""
+    """sfs2d_dist_scan_gather_streams: steps in groups over two plans on two streams, one gather of a
+    group's tables per group (to the root and all-gathered), a last partial group; every table and
+    every gathered copy equals the plan's own records; argument errors."""
     import torch
     from sfs2d import _lib as L
-    from sfs2d.engine import Dist, Engine, ScanConfig
+    from sfs2d.engine import Engine, ScanConfig
     from sfs2d.synth import synth_genome
     p = synth_genome(2, [30000, 9000], 25, 25, seed=22)
     eng = Engine.get(0)
@@ -62,31 +63,35 @@ def test_single_rank_scan_gather_streams():
     plans[0].check()
     ref = plans[0].read()
     rows = plans[0].nrec + 2
-    outs = [torch.zeros((rows, 64), dtype=torch.uint8, device="cuda:0") for _ in range(2)]
-    gath = [torch.full((rows, 64), 7, dtype=torch.uint8, device="cuda:0") for _ in range(2)]
+    outbuf = torch.zeros((4 * rows, 64), dtype=torch.uint8, device="cuda:0")
+    gath = [torch.full((2 * rows, 64), 7, dtype=torch.uint8, device="cuda:0") for _ in range(2)]
     streams = [torch.cuda.Stream(device=0).cuda_stream for _ in range(2)]
-    ds = [eng.dist(eng.dist_unique_id(), 0, 1) for _ in range(2)]
-    op = [o.data_ptr() for o in outs]
+    d = eng.dist(eng.dist_unique_id(), 0, 1)
     gp = [g.data_ptr() for g in gath]
     try:
-        for root in (True, False):
-            for d in ds:
-                d.set_gather(root)
+        for root, nsteps in ((True, 8), (False, 8), (True, 5)):
+            d.set_gather(root)
+            outbuf.zero_()
             for g in gath:
                 g.fill_(7)
-            Dist.scan_gather_streams(ds, plans, streams, op, gp, rows, 7)
+            d.scan_gather_streams(plans, streams, outbuf.data_ptr(), gp, rows, nsteps)
             torch.cuda.synchronize()
-            for q, o, g in zip(plans, outs, gath):
+            for q in plans:
                 q.check()
-                assert torch.equal(o, g)
-                recs = np.frombuffer(o[: q.nrec].cpu().numpy().tobytes(), dtype=L.WINDOW_DTYPE)
-                assert recs.tobytes() == ref.tobytes()
-        with pytest.raises(L.Sfs2dError):   # one communicator twice
-            Dist.scan_gather_streams([ds[0], ds[0]], plans, streams, op, gp, rows, 1)
+            tabs = outbuf.view(4, rows, 64)
+            # 5 steps: groups (0, 1), (2, 3), (4): tables 0-3 written, group 2 (parity 0) gathers table 0 only
+            for t in range(4):
+                recs = np.frombuffer(tabs[t][: rows - 2].cpu().numpy().tobytes(), dtype=L.WINDOW_DTYPE)
+                assert recs.tobytes() == ref.tobytes(), (root, nsteps, t)
+            for par in range(2):
+                assert torch.equal(gath[par][: rows - 2], tabs[2 * par][: rows - 2])
+                if nsteps == 8:
+                    assert torch.equal(gath[par], outbuf[2 * par * rows: (2 * par + 2) * rows])
+        with pytest.raises(L.Sfs2dError):   # one plan twice
+            d.scan_gather_streams([plans[0], plans[0]], streams, outbuf.data_ptr(), gp, rows, 2)
         with pytest.raises(L.Sfs2dError):   # rows must cover the records
-            Dist.scan_gather_streams(ds, plans, streams, op, gp, plans[0].nrec - 1, 1)
+            d.scan_gather_streams(plans, streams, outbuf.data_ptr(), gp, rows - 3, 2)
     finally:
-        for d in ds:
-            d.close()
+        d.close()
         for q in plans:
             q.close()
