@@ -1582,6 +1582,8 @@ int sfs2d_dist_scan_gather_streams(sfs2d_dist* d, sfs2d_plan* const* plans, void
   hipStream_t saved = ctx->stream;
   const size_t rec = sizeof(sfs2d_window);
   void* gath[2] = {gathered0, gathered1};
+  // (a lambda: the HIPCHK early returns leave through the ctx-stream restore below)
+  const int rc = [&]() -> int {
   int rc = 0;
   for (int64_t g = 0, done = 0; done < nsteps && !rc; ++g) {
     const int m = (int)std::min<int64_t>(nplans, nsteps - done);
@@ -1605,6 +1607,8 @@ int sfs2d_dist_scan_gather_streams(sfs2d_dist* d, sfs2d_plan* const* plans, void
     HIPCHK(ctx, hipEventRecord(d->ev_k[nplans + par], st(0)));
     done += m;
   }
+  return rc;
+  }();
   ctx->stream = saved;
   return rc;
 }

@@ -132,8 +132,7 @@ def hbm_stream_roofline(eng, steps=5):
            "pipeline_bytes_note": "SURVEY 8(d): 12 B/SNP + 64 B/window per run over the wall time of back-to-back runs",
            "windows": nwin, "windows_per_s": nwin / tk,
            "workload": "config 3 stream on 1 GPU: 32 chrom x 1.5625e6 SNPs, 20 kb, per-chromosome bg"}
-    for q in plans[::-1]:
-        q.close()
+    pl.close()
     dev.close()
     return out
 
@@ -310,7 +309,8 @@ def main():
         cand = [(t_se, None), (t_ov / 0.9, comm_s.cuda_stream)]
         if ns > 1:
             cand.append((timed(STREAMS, 0, wh * ns) / 0.95, STREAMS))
-        dist_times = {"serial": t_se, "overlapped": t_ov, "streams": cand[2][0] * 0.95 if ns > 1 else None}
+        dist_times = {"serial": t_se * 1e6, "overlapped": t_ov * 1e6,
+                      "streams": cand[2][0] * 0.95e6 if ns > 1 else None}
         gather_on = min(cand, key=lambda c: c[0])[1]
         first_timed = step_no
     elif dl:
@@ -402,7 +402,7 @@ def main():
                                          + ")" if dl else "")
                                       + (f"; {timed_ns} plans on {timed_ns} HIP streams, steps round-robin (passes overlap)"
                                          if timed_ns > 1 else "")},
-            **({"dist_step_ms_by_placement": dist_times} if dist_times else {}),
+            **({"dist_step_us_by_placement": dist_times} if dist_times else {}),
             "kernels_ms": {"k_prep": k1, "k_bg_slice": k2, "k_scan_w": k3, "k_scan_w_untimed_pass": k3_untimed,
                            "timed_runs_sampled": nr, "exact_path_windows": pl.stats(),
                            "note": "k_bg_slice / k_scan_w: events in every 8th timed run; k_prep: 16 runs after "

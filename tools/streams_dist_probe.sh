@@ -11,9 +11,9 @@ timeout -k 10 300 python -u -m pytest tests/test_dist_native.py tests/test_gpu_p
 tail -1 $OUT/pytest.log
 for s in 1 2; do
   timeout -k 10 240 python bench.py --dist-loop --streams $s --no-cpu-baseline --no-hbm-stream > $OUT/dist_s$s.log 2>&1 || { tail -20 $OUT/dist_s$s.log; exit 1; }
-  tail -1 $OUT/dist_s$s.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('dist-loop streams $s', round(d['value']/1e6,1), 'M windows/s', round(d['ms_per_step']*1e3,2), 'us/step', d['config']['parallelism'])"
+  tail -1 $OUT/dist_s$s.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('dist-loop streams $s', round(d['value']/1e6,1), 'M windows/s', round(d['ms_per_step']*1e3,2), 'us/step', d['config']['parallelism'], d.get('dist_step_ms_by_placement'))"
 done
 for r in 1 2; do
-  timeout -k 10 240 python bench.py --gpus 1 --steps 20 --warmup 5 --streams 2 --no-cpu-baseline --no-hbm-stream > $OUT/driver_s2_$r.log 2>&1 || { tail -20 $OUT/driver_s2_$r.log; exit 1; }
+  timeout -k 10 240 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-hbm-stream > $OUT/driver_s2_$r.log 2>&1 || { tail -20 $OUT/driver_s2_$r.log; exit 1; }
   tail -1 $OUT/driver_s2_$r.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('driver cmd streams 2', round(d['value']/1e6,1), 'M windows/s', round(d['ms_per_step']*1e3,2), 'us/step')"
 done
