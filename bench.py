@@ -326,7 +326,10 @@ def main():
     # (tools/timing_overhead.py); the scan kernel's start event needs the end event of the kernel
     # before it (alone it also counts that kernel's drain: 10.8-11.4 vs 9.6 us).  k_prep is timed in
     # an untimed pass after the timed loop.
-    pl.set_timing(args.steps, every=8, kernels=6)
+    # (short runs -- the driver's 20 steps -- sample every 2nd run of plan 0, so that the roofline's
+    # average is over >= 5 launches; long runs every 8th)
+    every = 8 if args.steps >= 160 else 2
+    pl.set_timing(args.steps, every=every, kernels=6)
     if dl:
         dist.barrier()
     torch.cuda.synchronize()
@@ -405,14 +408,15 @@ def main():
             **({"dist_step_us_by_placement": dist_times} if dist_times else {}),
             "kernels_ms": {"k_prep": k1, "k_bg_slice": k2, "k_scan_w": k3, "k_scan_w_untimed_pass": k3_untimed,
                            "timed_runs_sampled": nr, "exact_path_windows": pl.stats(),
-                           "note": "k_bg_slice / k_scan_w: events in every 8th timed run; k_prep: 16 runs after "
-                                   "the timed loop"},
+                           "note": f"k_bg_slice / k_scan_w: events in every {every}th timed run of plan 0; k_prep: 16 "
+                                   "runs after the timed loop (one stream, untimed)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_scan_w", "ms": k3, "algorithmic_bytes": b3,
                          "note": "k_scan_w: algorithmic bytes 4 B/SNP + 96 B/slot per launch over its average "
-                                 "duration (kernel start/end events in the dispatch packets of every 8th timed run); "
-                                 "the 8 MB config-2 stream is MALL-resident (see roofline_hbm for the HBM-sized "
+                                 f"duration (kernel start/end events in the dispatch packets of every {every}th timed run "
+                                 + ("of plan 0, contended by the other streams' passes); " if timed_ns > 1 else "); ")
+                                 + "the 8 MB config-2 stream is MALL-resident (see roofline_hbm for the HBM-sized "
                                  "stream); traffic: " + (tsrc or "no PMC pass committed")},
             "roofline_pipeline": {"bound": "hbm", "achieved": bp / step_s / 1e9, "peak": HBM_PEAK_GBS,
                                   "unit": "GB/s", "frac": bp / step_s / 1e9 / HBM_PEAK_GBS,
