@@ -147,10 +147,17 @@ def main():
     ap.add_argument("--dist-loop", action="store_true",
                     help="diagnostic: the N>1 step loop (scan + RCCL all-gather per step) even on one rank")
     ap.add_argument("--py-loop", action="store_true", help="diagnostic: the Python N>1 step loop instead of the native one")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=3,
                     help="N=1: consecutive steps round-robin over this many plans, each on its own HIP stream "
                          "(independent passes overlap; sfs2d_plan_run_streams)")
     args = ap.parse_args()
+    # hardware queues per process: HIP maps streams onto GPU_MAX_HW_QUEUES queues (4 on the box); S
+    # pass streams + the library's and torch's own need more than 4 or two passes share a queue and
+    # serialise (3 streams: 1.35e8 windows/s with 4 queues, 1.92-1.94e8 with 6-8; profiles/r02h_*).
+    # Set before the HIP runtime starts (torch imported below).
+    need = max(1, args.streams) + 4
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < need:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(8, need)))
 
     import torch
     import torch.distributed as dist
