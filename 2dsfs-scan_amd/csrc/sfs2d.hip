@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "sfs2d.h"
@@ -84,6 +85,13 @@ void div_magic(uint32_t d, uint32_t* m, int* s1, int* s2) {
 }
 
 }  // namespace
+
+// the stream a host thread enqueues on: the ctx's, unless this thread runs one of
+// sfs2d_plan_run_streams' enqueue threads (each on its own stream)
+namespace {
+thread_local hipStream_t tl_stream = nullptr;
+}
+#define CTX_STREAM(c) (tl_stream ? tl_stream : (c)->stream)
 
 struct sfs2d_ctx {
   int device = 0;
@@ -234,7 +242,7 @@ int repl_par(const sfs2d_plan* pl) { return pl->fused ? plan_par(pl) : 0; }
 template <bool P16, bool FUSED, bool FST>
 void launch_scan_w(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
   hipExtLaunchKernelGGL((k_scan_w<P16, FUSED, FST>), dim3((unsigned)pl->chunks.size()), dim3(SBLOCK), pl->scan_lds,
-                     pl->ctx->stream, pl->kev[4], pl->kev[5], 0, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
+                     CTX_STREAM(pl->ctx), pl->kev[4], pl->kev[5], 0, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
                      per_chrom, pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, bp, pl->d_repl, pl->d_bcount,
                      plan_par(pl), pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels,
                      pl->extra_rec >= 0 ? (int)pl->last_chrom : -1, pl->d_fsum, pl->d_fst, pl->d_ctr,
@@ -244,14 +252,14 @@ void launch_scan_w(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
 template <bool P16, bool FST>
 void launch_scan_g(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
   hipExtLaunchKernelGGL((k_scan_g<P16, FST>), dim3((unsigned)pl->chunks.size()), dim3(BLOCK), pl->scan_lds,
-                     pl->ctx->stream, pl->kev[4], pl->kev[5], 0, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_head, per_chrom,
+                     CTX_STREAM(pl->ctx), pl->kev[4], pl->kev[5], 0, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_head, per_chrom,
                      pl->ctx->d_lnx, out, bp, pl->d_fsum, pl->d_fst);
 }
 
 template <bool P16, bool FST>
 void launch_scan_gw(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
   hipExtLaunchKernelGGL((k_scan_gw<P16, FST>), dim3((unsigned)pl->chunks.size()), dim3(WAVE), pl->scan_lds,
-                     pl->ctx->stream, pl->kev[4], pl->kev[5], 0, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
+                     CTX_STREAM(pl->ctx), pl->kev[4], pl->kev[5], 0, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
                      per_chrom, pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, bp, pl->d_repl, pl->d_bcount,
                      0, pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels, -1, pl->d_fsum, pl->d_fst,
                      pl->d_ctr, (int)(pl->runs & 1), pl->d_leafsum, pl->d_bg1d, 0, pl->d_gscr, pl->nscr);
@@ -284,7 +292,7 @@ hipError_t launch_prep3(sfs2d_plan* pl) {
   const sfs2d_data* d = pl->data;
   const int par = plan_par(pl);
   hipExtLaunchKernelGGL((k_prep<B, S, L, N, F, FS>), dim3((unsigned)pl->tiles.size()), dim3(BLOCK1),
-                     (B && L) ? pl->bg_lds : 0, pl->ctx->stream, pl->kev[0], pl->kev[1], 0, pl->K, d->counts, d->pos, d->ann, pl->d_tiles,
+                     (B && L) ? pl->bg_lds : 0, CTX_STREAM(pl->ctx), pl->kev[0], pl->kev[1], 0, pl->K, d->counts, d->pos, d->ann, pl->d_tiles,
                      pl->d_repl + (size_t)repl_par(pl) * REPL * pl->K.nchrom * pl->K.nh, pl->d_slots, pl->d_bins,
                      pl->d_bcount + (size_t)par * pl->K.nchrom, pl->d_err, L ? pl->hr : 1,
                      reinterpret_cast<const double2*>(pl->ctx->d_df + 2 * LNT), pl->d_fsum);
@@ -317,7 +325,7 @@ hipError_t launch_prep(sfs2d_plan* pl, bool bins) {
 // per-run per-chromosome backgrounds
 hipError_t launch_bg_slices(sfs2d_plan* pl) {
   hipExtLaunchKernelGGL(k_bg_slice, dim3((unsigned)pl->slices.size() + 1 + (unsigned)pl->nfst, (unsigned)pl->nbg), dim3(KBLOCK), 0,
-                     pl->ctx->stream, pl->kev[2], pl->kev[3], 0, pl->K, pl->d_repl, pl->d_bcount + (size_t)plan_par(pl) * pl->K.nchrom, pl->d_tab,
+                     CTX_STREAM(pl->ctx), pl->kev[2], pl->kev[3], 0, pl->K, pl->d_repl, pl->d_bcount + (size_t)plan_par(pl) * pl->K.nchrom, pl->d_tab,
                      pl->d_lp, pl->d_head, pl->d_leafsum, pl->d_bg1d, pl->d_done, pl->d_slices, (int)pl->slices.size(),
                      pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels, pl->sliced ? 0 : 1, pl->nfst,
                      pl->data->counts, pl->d_bins, pl->d_slots, reinterpret_cast<const double2*>(pl->ctx->d_df + 2 * LNT),
@@ -328,7 +336,7 @@ hipError_t launch_bg_slices(sfs2d_plan* pl) {
 // one supplied background (values uploaded to d_bgval)
 hipError_t launch_finalize(sfs2d_plan* pl, int integer_values) {
   const size_t lds = pl->K.nt <= FIN_LDS_BINS ? sizeof(double) * pl->K.nt : 0;
-  hipLaunchKernelGGL(k_bg_finalize, dim3(1), dim3(FBLOCK), lds, pl->ctx->stream, pl->K, integer_values, pl->d_bgval,
+  hipLaunchKernelGGL(k_bg_finalize, dim3(1), dim3(FBLOCK), lds, CTX_STREAM(pl->ctx), pl->K, integer_values, pl->d_bgval,
                      pl->d_bgval, pl->d_tab, pl->d_lp, pl->d_head, pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes);
   return hipGetLastError();
 }
@@ -336,7 +344,7 @@ hipError_t launch_finalize(sfs2d_plan* pl, int integer_values) {
 template <bool P16>
 hipError_t launch_extra(sfs2d_plan* pl, sfs2d_window* out) {
   const sfs2d_data* d = pl->data;
-  hipLaunchKernelGGL((k_scan_extra<P16>), dim3(1), dim3(WAVE), pl->extra_lds, pl->ctx->stream, pl->K, pl->d_bins,
+  hipLaunchKernelGGL((k_scan_extra<P16>), dim3(1), dim3(WAVE), pl->extra_lds, CTX_STREAM(pl->ctx), pl->K, pl->d_bins,
                      d->pos, pl->last_chrom, d->d_chrom_off, pl->d_tab, pl->d_head,
                      pl->prm.bg_mode == SFS2D_BG_PER_CHROM ? 1 : 0, pl->ctx->d_lnx, out, (long long)pl->extra_rec);
   return hipGetLastError();
@@ -357,15 +365,15 @@ hipError_t launch_attached(sfs2d_plan* a) {
   if (!ns) { a->runs++; return hipSuccess; }
   const dim3 g((ns + 255) / 256);
   if (a->prm.window_mode == SFS2D_WINDOW_BP)
-    hipLaunchKernelGGL(k_slots_bp, g, dim3(256), 0, a->ctx->stream, d->pos, d->d_chrom_off, a->d_slot_base,
+    hipLaunchKernelGGL(k_slots_bp, g, dim3(256), 0, CTX_STREAM(a->ctx), d->pos, d->d_chrom_off, a->d_slot_base,
                        d->nchrom, (uint32_t)a->prm.window, ns, a->d_slots);
   if (a->fst_m)
-    hipLaunchKernelGGL(k_fst_agg, g, dim3(256), 0, a->ctx->stream, a->base->d_fsum, a->base->d_slot_base,
+    hipLaunchKernelGGL(k_fst_agg, g, dim3(256), 0, CTX_STREAM(a->ctx), a->base->d_fsum, a->base->d_slot_base,
                        a->d_slot_base, d->nchrom, a->fst_m, ns,
                        std::max(0, a->base->K.fst_e - a->K.fst_e), a->d_fsum);
   if (a->fst_win)   // before the scan clears the slots
     hipLaunchKernelGGL(k_fst_win, dim3((unsigned)std::min<uint32_t>(2048u, (ns + 3u) / 4u)), dim3(256), 0,
-                       a->ctx->stream, d->counts, a->d_bins, a->d_slots,
+                       CTX_STREAM(a->ctx), d->counts, a->d_bins, a->d_slots,
                        reinterpret_cast<const double2*>(a->ctx->d_df + 2 * LNT), a->d_fst, ns);
   const hipError_t e = launch_scan_any(a, a->d_out);
   a->last_out = a->d_out;
@@ -414,7 +422,7 @@ int sfs2d_ctx_create(int device, sfs2d_ctx** out) {
 int sfs2d_ctx_destroy(sfs2d_ctx* ctx) {
   if (!ctx) return SFS2D_E_ARG;
   hipSetDevice(ctx->device);
-  hipStreamSynchronize(ctx->stream);
+  hipStreamSynchronize(CTX_STREAM(ctx));
   hipFree(ctx->d_lnx);
   hipFree(ctx->d_df);
   hipStreamDestroy(ctx->own);
@@ -551,22 +559,22 @@ int sfs2d_data_synth_sims(sfs2d_ctx* ctx, const sfs2d_synth_params* sp, const ui
     hipFree(d->counts); hipFree(d->pos); hipFree(d->ann); hipFree(d_woff); hipFree(d->d_chrom_off); delete d;
     return SFS2D_E_NOMEM;
   }
-  hipError_t e = hipMemsetAsync(d->ann, 0, sizeof(uint16_t) * np, ctx->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(d->counts, 0, sizeof(uint32_t) * np, ctx->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(d->pos, 0, sizeof(uint32_t) * np, ctx->stream);
-  if (e == hipSuccess) e = hipMemcpyAsync(d_woff, woff.data(), sizeof(unsigned long long) * (nw + 1), hipMemcpyHostToDevice, ctx->stream);
-  if (e == hipSuccess) e = hipMemcpyAsync(d_mt, miss_cdf1, sizeof(uint32_t) * nm1, hipMemcpyHostToDevice, ctx->stream);
-  if (e == hipSuccess) e = hipMemcpyAsync(d_mt + nm1, miss_cdf2, sizeof(uint32_t) * nm2, hipMemcpyHostToDevice, ctx->stream);
+  hipError_t e = hipMemsetAsync(d->ann, 0, sizeof(uint16_t) * np, CTX_STREAM(ctx));
+  if (e == hipSuccess) e = hipMemsetAsync(d->counts, 0, sizeof(uint32_t) * np, CTX_STREAM(ctx));
+  if (e == hipSuccess) e = hipMemsetAsync(d->pos, 0, sizeof(uint32_t) * np, CTX_STREAM(ctx));
+  if (e == hipSuccess) e = hipMemcpyAsync(d_woff, woff.data(), sizeof(unsigned long long) * (nw + 1), hipMemcpyHostToDevice, CTX_STREAM(ctx));
+  if (e == hipSuccess) e = hipMemcpyAsync(d_mt, miss_cdf1, sizeof(uint32_t) * nm1, hipMemcpyHostToDevice, CTX_STREAM(ctx));
+  if (e == hipSuccess) e = hipMemcpyAsync(d_mt + nm1, miss_cdf2, sizeof(uint32_t) * nm2, hipMemcpyHostToDevice, CTX_STREAM(ctx));
   if (e == hipSuccess && nw) {
     SynthP S;
     S.seed = sp->seed; S.gen = sp->generation; S.nwin = sp->n_windows; S.ws = sp->window_bp;
     S.n1 = 2u * (uint32_t)sp->n1p; S.n2 = 2u * (uint32_t)sp->n2p; S.nm1 = (uint32_t)nm1; S.nm2 = (uint32_t)nm2;
     const unsigned grid = (unsigned)std::min<uint64_t>(16384, (nw + 3) / 4);
-    hipLaunchKernelGGL(k_synth_sims, dim3(grid), dim3(256), 0, ctx->stream, S, d_woff, (unsigned long long)nw,
+    hipLaunchKernelGGL(k_synth_sims, dim3(grid), dim3(256), 0, CTX_STREAM(ctx), S, d_woff, (unsigned long long)nw,
                        d_mt, d_mt + nm1, d->counts, d->pos);
     e = hipGetLastError();
   }
-  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(CTX_STREAM(ctx));
   hipFree(d_woff);
   hipFree(d_mt);
   if (e != hipSuccess) {
@@ -583,7 +591,7 @@ int sfs2d_data_read(const sfs2d_data* d, uint32_t* counts, uint32_t* pos, int64_
   if (!d || n != d->n) return SFS2D_E_ARG;
   sfs2d_ctx* ctx = d->ctx;
   HIPCHK(ctx, hipSetDevice(ctx->device));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(CTX_STREAM(ctx)));
   if (counts && n) HIPCHK(ctx, hipMemcpy(counts, d->counts, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost));
   if (pos && n) HIPCHK(ctx, hipMemcpy(pos, d->pos, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost));
   return 0;
@@ -939,7 +947,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   }
   if (pl->slices.empty()) pl->slices.push_back(make_int4(0, K.nb2, 0, 0));
 
-  hipStream_t st = ctx->stream;
+  hipStream_t st = CTX_STREAM(ctx);
   rc = 0;
   rc = rc ? rc : dalloc(ctx, &pl->d_tiles, pl->tiles.size());
   rc = rc ? rc : dalloc(ctx, &pl->d_chunks, pl->chunks.size());
@@ -1012,9 +1020,9 @@ int sfs2d_plan_set_background(sfs2d_plan* pl, const double* bg2d, const double* 
   for (double x : v)
     if (!(x == std::floor(x)) || std::fabs(x) > 9.0e15) { integer_values = false; break; }
   HIPCHK(ctx, hipSetDevice(ctx->device));
-  HIPCHK(ctx, hipMemcpyAsync(pl->d_bgval, v.data(), sizeof(double) * K.nt, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(pl->d_bgval, v.data(), sizeof(double) * K.nt, hipMemcpyHostToDevice, CTX_STREAM(ctx)));
   HIPCHK(ctx, launch_finalize(pl, integer_values ? 1 : 0));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(CTX_STREAM(ctx)));
   pl->bg_ready = true;
   return 0;
 }
@@ -1034,8 +1042,8 @@ int sfs2d_plan_run_phase(sfs2d_plan* pl, int phase, sfs2d_window* out_dev) {
   for (int k = 0; k < 6; ++k) pl->kev[k] = (te && ((pl->tmask >> (k / 2)) & 1)) ? te[k] : nullptr;
   auto mark = [&](int k) -> int {
     if (te && ((pl->tmask >> (k / 2)) & 1)) {
-      HIPCHK(ctx, hipEventRecord(te[k], ctx->stream));
-      HIPCHK(ctx, hipEventRecord(te[k + 1], ctx->stream));
+      HIPCHK(ctx, hipEventRecord(te[k], CTX_STREAM(ctx)));
+      HIPCHK(ctx, hipEventRecord(te[k + 1], CTX_STREAM(ctx)));
     }
     return 0;
   };
@@ -1082,7 +1090,7 @@ int sfs2d_plan_set_timing_kernels(sfs2d_plan* pl, int max_runs, int every, int k
   pl->tmask = kernel_mask;
   pl->tseen = 0;
   sfs2d_ctx* ctx = pl->ctx;
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(CTX_STREAM(ctx)));
   for (auto& e : pl->tev) if (e) hipEventDestroy(e);
   pl->tev.assign((size_t)max_runs * 6, nullptr);
   for (auto& e : pl->tev) HIPCHK(ctx, hipEventCreate(&e));
@@ -1136,9 +1144,31 @@ int sfs2d_plan_run_streams(sfs2d_plan* const* plans, void* const* streams, sfs2d
       if (plans[j] == plans[k]) return set_err(ctx, SFS2D_E_ARG, "a plan may appear once (its per-run state is not shareable)");
   }
   // run i: plan i % nplans on stream i % nplans.  The plans' per-run state (bins, replicas, slots,
-  // counters) is their own, so consecutive runs on different streams overlap; the ctx stream is
-  // switched per run and restored
-  hipStream_t saved = ctx->stream;
+  // counters) is their own, so consecutive runs on different streams overlap.  With distinct streams
+  // each plan's runs are enqueued by a host thread of its own (tl_stream: that thread's stream), so
+  // the host's ~4 us per launch is paid in parallel (SFS2D_ENQ_THREADS=0: one thread, the ctx stream
+  // switched per run)
+  bool distinct = nplans > 1;
+  for (int k = 0; k < nplans && distinct; ++k)
+    for (int j = 0; j < k; ++j)
+      if (streams[j] == streams[k]) distinct = false;
+  const char* ev = std::getenv("SFS2D_ENQ_THREADS");
+  if (distinct && !(ev && ev[0] == '0')) {
+    std::vector<int> rcs((size_t)nplans, 0);
+    std::vector<std::thread> th;
+    for (int k = 0; k < nplans; ++k)
+      th.emplace_back([&, k]() {
+        tl_stream = streams[k] ? (hipStream_t)streams[k] : ctx->own;
+        for (int i = k; i < nruns && !rcs[(size_t)k]; i += nplans)
+          rcs[(size_t)k] = sfs2d_plan_run_phase(plans[k], 0, outs ? outs[k] : nullptr);
+        tl_stream = nullptr;
+      });
+    for (auto& t : th) t.join();
+    for (int r : rcs)
+      if (r) return r;
+    return 0;
+  }
+  hipStream_t saved = CTX_STREAM(ctx);
   int rc = 0;
   for (int i = 0; i < nruns && !rc; ++i) {
     const int k = i % nplans;
@@ -1172,8 +1202,8 @@ int sfs2d_plan_fst_read(sfs2d_plan* pl, double* out_host, int64_t cap) {
   if (cap < pl->nslots) return set_err(ctx, SFS2D_E_CAP, "output capacity too small");
   if (pl->nslots && !out_host) return SFS2D_E_ARG;
   if (pl->nslots)
-    HIPCHK(ctx, hipMemcpyAsync(out_host, pl->d_fst, sizeof(double) * pl->nslots, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(out_host, pl->d_fst, sizeof(double) * pl->nslots, hipMemcpyDeviceToHost, CTX_STREAM(ctx)));
+  HIPCHK(ctx, hipStreamSynchronize(CTX_STREAM(ctx)));
   return 0;
 }
 
@@ -1181,11 +1211,11 @@ int sfs2d_plan_check(sfs2d_plan* pl) {
   if (!pl) return SFS2D_E_ARG;
   sfs2d_ctx* ctx = pl->ctx;
   uint32_t e = 0;
-  HIPCHK(ctx, hipMemcpyAsync(&e, pl->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(&e, pl->d_err, 4, hipMemcpyDeviceToHost, CTX_STREAM(ctx)));
+  HIPCHK(ctx, hipStreamSynchronize(CTX_STREAM(ctx)));
   if (e) {
-    HIPCHK(ctx, hipMemsetAsync(pl->d_err, 0, 4, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(pl->d_err, 0, 4, CTX_STREAM(ctx)));
+    HIPCHK(ctx, hipStreamSynchronize(CTX_STREAM(ctx)));
     if (e & ERR_KEY) return set_err(ctx, SFS2D_E_KEY, "allele count above 2*pop_size (reference: KeyError in calculate_1d_sfs)");
     return set_err(ctx, SFS2D_E_GRID, "folded 2D bin outside the (2n1+1)x(2n2+1) grid");
   }
@@ -1212,8 +1242,8 @@ int sfs2d__debug_stamps(unsigned long long* out64) {
 int sfs2d_plan_stats(sfs2d_plan* pl, uint32_t* exact_windows) {
   if (!pl || !exact_windows) return SFS2D_E_ARG;
   sfs2d_ctx* ctx = pl->ctx;
-  HIPCHK(ctx, hipMemcpyAsync(exact_windows, pl->d_err + 1, 4, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(exact_windows, pl->d_err + 1, 4, hipMemcpyDeviceToHost, CTX_STREAM(ctx)));
+  HIPCHK(ctx, hipStreamSynchronize(CTX_STREAM(ctx)));
   return 0;
 }
 
@@ -1225,15 +1255,15 @@ int sfs2d_plan_read(sfs2d_plan* pl, sfs2d_window* out_host, int64_t cap, int64_t
   if (pl->nrec && !out_host) return SFS2D_E_ARG;
   const sfs2d_window* src = pl->last_out ? pl->last_out : pl->d_out;
   if (pl->nrec)
-    HIPCHK(ctx, hipMemcpyAsync(out_host, src, sizeof(sfs2d_window) * pl->nrec, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(out_host, src, sizeof(sfs2d_window) * pl->nrec, hipMemcpyDeviceToHost, CTX_STREAM(ctx)));
+  HIPCHK(ctx, hipStreamSynchronize(CTX_STREAM(ctx)));
   return 0;
 }
 
 int sfs2d_plan_time(sfs2d_plan* pl, int iters, double* ms_run, double* ms_k1, double* ms_k2, double* ms_k3) {
   if (!pl || iters < 1) return SFS2D_E_ARG;
   sfs2d_ctx* ctx = pl->ctx;
-  hipStream_t st = ctx->stream;
+  hipStream_t st = CTX_STREAM(ctx);
   double t1 = 0, t2 = 0, t3 = 0, tall = 0;
   for (int it = 0; it < iters; ++it) {
     HIPCHK(ctx, hipEventRecord(pl->ev[0], st));
@@ -1264,7 +1294,7 @@ int sfs2d_plan_time(sfs2d_plan* pl, int iters, double* ms_run, double* ms_k1, do
 int sfs2d_plan_destroy(sfs2d_plan* pl) {
   if (!pl) return SFS2D_E_ARG;
   hipSetDevice(pl->ctx->device);
-  hipStreamSynchronize(pl->ctx->stream);
+  hipStreamSynchronize(CTX_STREAM(pl->ctx));
   for (sfs2d_plan* a : pl->attached) {   // attached plans go with their base
     a->base = pl;
     plan_free(a);
@@ -1385,18 +1415,18 @@ int sfs2d_bg_hist(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* pr
   rc = rc ? rc : dalloc(ctx, &pl.d_err, 1);
   hipError_t e = hipSuccess;
   if (!rc) {
-    if (!pl.tiles.empty()) e = hipMemcpyAsync(pl.d_tiles, pl.tiles.data(), sizeof(Tile) * pl.tiles.size(), hipMemcpyHostToDevice, ctx->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(pl.d_repl, 0, sizeof(uint32_t) * REPL * K.nh, ctx->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(pl.d_err, 0, 4, ctx->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(pl.d_bcount, 0, 4, ctx->stream);
+    if (!pl.tiles.empty()) e = hipMemcpyAsync(pl.d_tiles, pl.tiles.data(), sizeof(Tile) * pl.tiles.size(), hipMemcpyHostToDevice, CTX_STREAM(ctx));
+    if (e == hipSuccess) e = hipMemsetAsync(pl.d_repl, 0, sizeof(uint32_t) * REPL * K.nh, CTX_STREAM(ctx));
+    if (e == hipSuccess) e = hipMemsetAsync(pl.d_err, 0, 4, CTX_STREAM(ctx));
+    if (e == hipSuccess) e = hipMemsetAsync(pl.d_bcount, 0, 4, CTX_STREAM(ctx));
     if (e == hipSuccess && pl.lds_hist && pl.bg_lds > 64 * 1024)
       hipFuncSetAttribute((const void*)k_prep<true, false, true, false, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.bg_lds),
       hipFuncSetAttribute((const void*)k_prep<true, false, true, false, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.bg_lds);
     if (e == hipSuccess) e = launch_prep(&pl, false);
-    if (e == hipSuccess) e = hipMemcpyAsync(hist.data(), pl.d_repl, sizeof(uint32_t) * REPL * K.nh, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(hist.data(), pl.d_repl, sizeof(uint32_t) * REPL * K.nh, hipMemcpyDeviceToHost, CTX_STREAM(ctx));
     uint32_t err = 0;
-    if (e == hipSuccess) e = hipMemcpyAsync(&err, pl.d_err, 4, hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(&err, pl.d_err, 4, hipMemcpyDeviceToHost, CTX_STREAM(ctx));
+    if (e == hipSuccess) e = hipStreamSynchronize(CTX_STREAM(ctx));
     if (e == hipSuccess && err) rc = (err & ERR_KEY) ? set_err(ctx, SFS2D_E_KEY, "allele count above 2*pop_size")
                                                      : set_err(ctx, SFS2D_E_GRID, "folded 2D bin outside the grid");
   }
@@ -1531,17 +1561,17 @@ int sfs2d_dist_scan_gather(sfs2d_dist* d, sfs2d_plan* pl, void* out0, void* out1
   // overlapped: gathers on comm_stream, ordered by events; serial (comm_stream NULL or the library's
   // stream): each gather follows its scan on one stream, no events (measured on one GPU: the two
   // cross-stream dependencies per step cost ~12 us, the serial one-rank gather ~2 us)
-  hipStream_t cs = comm_stream ? (hipStream_t)comm_stream : ctx->stream;
-  const bool overlap = cs != ctx->stream;
+  hipStream_t cs = comm_stream ? (hipStream_t)comm_stream : CTX_STREAM(ctx);
+  const bool overlap = cs != CTX_STREAM(ctx);
   void* outs[2] = {out0, out1};
   void* gath[2] = {gathered0, gathered1};
   for (int i = 0; i < nsteps; ++i) {
     const int b = (int)((first_step + i) & 1);
-    if (overlap && first_step + i >= 2) HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, d->ev_comm[b], 0));   // table b is free
+    if (overlap && first_step + i >= 2) HIPCHK(ctx, hipStreamWaitEvent(CTX_STREAM(ctx), d->ev_comm[b], 0));   // table b is free
     const int rc = sfs2d_plan_run(pl, static_cast<sfs2d_window*>(outs[b]));
     if (rc) return rc;
     if (overlap) {
-      HIPCHK(ctx, hipEventRecord(d->ev_scan[b], ctx->stream));
+      HIPCHK(ctx, hipEventRecord(d->ev_scan[b], CTX_STREAM(ctx)));
       HIPCHK(ctx, hipStreamWaitEvent(cs, d->ev_scan[b], 0));
     }
     const size_t bytes = (size_t)rows * sizeof(sfs2d_window);
@@ -1579,7 +1609,7 @@ int sfs2d_dist_scan_gather_streams(sfs2d_dist* d, sfs2d_plan* const* plans, void
   // of group g - 2 (which read the tables it is about to overwrite).  One communicator, one stream
   // for its collectives; cross-stream waits: 2 (nplans - 1) per group.
   auto st = [&](int k) { return streams[k] ? (hipStream_t)streams[k] : ctx->own; };
-  hipStream_t saved = ctx->stream;
+  hipStream_t saved = CTX_STREAM(ctx);
   const size_t rec = sizeof(sfs2d_window);
   void* gath[2] = {gathered0, gathered1};
   // (a lambda: the HIPCHK early returns leave through the ctx-stream restore below)
