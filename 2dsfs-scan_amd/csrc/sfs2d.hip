@@ -1144,16 +1144,17 @@ int sfs2d_plan_run_streams(sfs2d_plan* const* plans, void* const* streams, sfs2d
       if (plans[j] == plans[k]) return set_err(ctx, SFS2D_E_ARG, "a plan may appear once (its per-run state is not shareable)");
   }
   // run i: plan i % nplans on stream i % nplans.  The plans' per-run state (bins, replicas, slots,
-  // counters) is their own, so consecutive runs on different streams overlap.  With distinct streams
-  // each plan's runs are enqueued by a host thread of its own (tl_stream: that thread's stream), so
-  // the host's ~4 us per launch is paid in parallel (SFS2D_ENQ_THREADS=0: one thread, the ctx stream
-  // switched per run)
+  // counters) is their own, so consecutive runs on different streams overlap.  SFS2D_ENQ_THREADS=1
+  // (distinct streams): each plan's runs are enqueued by a host thread of its own (tl_stream: that
+  // thread's stream).  Off by default: config 2 with 3 streams is not host-bound (enqueue 10.7 us per
+  // pass on one thread, 9.1 threaded, vs 14.5 us per pass on the GPU): +1.5% at 400 passes, and the
+  // thread starts cost more than that in 20-pass runs (profiles/r02i_enqueue_probe.txt)
   bool distinct = nplans > 1;
   for (int k = 0; k < nplans && distinct; ++k)
     for (int j = 0; j < k; ++j)
       if (streams[j] == streams[k]) distinct = false;
   const char* ev = std::getenv("SFS2D_ENQ_THREADS");
-  if (distinct && !(ev && ev[0] == '0')) {
+  if (distinct && ev && ev[0] == '1') {
     std::vector<int> rcs((size_t)nplans, 0);
     std::vector<std::thread> th;
     for (int k = 0; k < nplans; ++k)

@@ -154,7 +154,9 @@ int sfs2d_plan_run_many(sfs2d_plan* plan, int nruns, sfs2d_window* out_dev);
 /* enqueue `nruns` runs round-robin over `nplans` distinct plans of one ctx: run i is plans[i % nplans]
  * on streams[i % nplans] (NULL = the ctx's own stream) into outs[i % nplans] (outs NULL or an entry
  * NULL = plan-owned).  Independent scans (replicates, data sets, repeated passes) overlap across the
- * streams; each plan's own runs stay ordered on its stream.  The ctx stream is restored after. */
+ * streams; each plan's own runs stay ordered on its stream.  SFS2D_ENQ_THREADS=1 (distinct
+ * streams): every plan's runs are enqueued by a host thread of its own, joined before return.  The
+ * ctx stream is unchanged after. */
 int sfs2d_plan_run_streams(sfs2d_plan* const* plans, void* const* streams, sfs2d_window* const* outs, int nplans,
                            int nruns);
 /* copy the last run's records to host (synchronises the stream) */
