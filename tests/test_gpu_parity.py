@@ -196,10 +196,12 @@ def test_plan_replay_is_deterministic():
     pl.close()
 
 
-@pytest.mark.parametrize("fst", [False, True])
-def test_run_streams_overlapped_plans(fst):
-    """sfs2d_plan_run_streams: passes round-robin over plans on their own HIP streams (overlapping)
-    write the same records and Fst as one plan run alone; argument errors are reported."""
+@pytest.mark.parametrize("fst,threads", [(False, "0"), (True, "0"), (True, "1")])
+def test_run_streams_overlapped_plans(monkeypatch, fst, threads):
+    """sfs2d_plan_run_streams: passes round-robin over plans on their own HIP streams (overlapping;
+    enqueued by one host thread or, SFS2D_ENQ_THREADS=1, one per stream) write the same records and
+    Fst as one plan run alone; argument errors are reported."""
+    monkeypatch.setenv("SFS2D_ENQ_THREADS", threads)
     import torch
     from sfs2d import _lib as L
     from sfs2d.engine import Engine, Plan, ScanConfig
