@@ -272,9 +272,10 @@ def main():
     STREAMS_MODE = "streams"
     timed_ns = ns
     if nat is not None:
-        # the warmup times both gather placements (overlapped on the comm stream with events, or
-        # serial on the scan stream) and every rank keeps the faster by the max over ranks; with
-        # several streams each stream's scan -> gather chain is serial (no placement to choose)
+        # the warmup times the step loop's placements -- one plan with its gathers serial on the scan
+        # stream or overlapped on the comm stream (events), and with --streams > 1 the grouped loop
+        # (ns plans on ns streams, one gather per group) -- and every rank keeps the fastest by the
+        # max over ranks
         STREAMS = STREAMS_MODE
 
         def run_dist(mode, first, n):
