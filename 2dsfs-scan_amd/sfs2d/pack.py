@@ -132,6 +132,60 @@ class PackedSNPs:
                           list(self.ann_names), self.pop1, self.pop2)
 
 
+def last_key_index(data, p: PackedSNPs) -> int:
+    """Index in ``p`` (scan order) of the data dict's last-inserted key; for packed input the dict
+    is the one ``to_snp_dict`` would build (insertion in scan order), i.e. the last SNP."""
+    if isinstance(data, PackedSNPs) or p.n == 0:
+        return p.n - 1
+    key = next(reversed(data))
+    chrom, pos = key.split("-")
+    c = p.chrom_names.index(chrom)
+    lo, hi = int(p.chrom_off[c]), int(p.chrom_off[c + 1])
+    return lo + int(np.searchsorted(p.pos[lo:hi], int(pos)))
+
+
+def shadow_chrom_starts(p: PackedSNPs, last: int, ws: int, start_position=None, end_position=None) -> PackedSNPs:
+    """The SNP stream ``T2D_scan`` (twoDSFS_class.py:686-776) actually scores.
+
+    At every chromosome change the driver computes a per-chromosome background with
+    ``for snp_key, snp_data in data_dict.items()`` (:740), which rebinds the outer loop's
+    ``snp_key``: the chromosome's first SNP then enters its window as the data dict's LAST key
+    (its calls and annotation, :748 / :763), while the window itself still follows the first SNP's
+    own position (``pos``).  When that last SNP lies in the same window, both are one dict key and
+    the window holds it once.  The position filter (:179-182) reads the key's position, so it is
+    applied here: filtered SNPs keep their place with (0, 0) counts, which the 2D SFS skips
+    (:212-213) and count_snps still counts (:291-302); the scan then runs without it."""
+    n = p.n
+    counts = p.counts.copy()
+    ann = p.ann_id.copy()
+    keypos = p.pos.astype(np.int64)
+    keep = np.ones(n, dtype=bool)
+    if n:
+        lc = int(np.searchsorted(p.chrom_off, last, side="right")) - 1
+        wid = lambda q: max(int(q) - 1, 0) // int(ws)   # window of a position: start 1 + k ws (:747, :762)
+        for c in range(p.nchrom):
+            x = int(p.chrom_off[c])
+            if x == int(p.chrom_off[c + 1]) or x == last:
+                continue
+            counts[x] = p.counts[last]
+            ann[x] = p.ann_id[last]
+            keypos[x] = int(p.pos[last])
+            if c == lc and wid(p.pos[x]) == wid(p.pos[last]):
+                keep[x] = False
+    drop = np.zeros(n, dtype=bool)
+    if start_position is not None:
+        drop |= keypos < int(start_position)
+    if end_position is not None:
+        drop |= keypos > int(end_position)
+    counts[drop] = 0
+    if keep.all():
+        return PackedSNPs(counts, p.pos, p.chrom_off, list(p.chrom_names), ann, list(p.ann_names), p.pop1, p.pop2)
+    cum = np.concatenate([[0], np.cumsum(keep)])
+    off = cum[p.chrom_off]
+    return PackedSNPs(counts[keep], p.pos[keep], off, list(p.chrom_names), ann[keep], list(p.ann_names),
+                      p.pop1, p.pop2)
+
+
 def pack_snp_dict(data_dict: dict, pop1: str = "uv", pop2: str = "bv") -> PackedSNPs:
     """Pack the reference SNP dict into scan order.
 

@@ -127,6 +127,18 @@ def fixed_bg_scan(recs, packed, ws, nslots):
     return res
 
 
+def single_stat_scan(recs, packed, ws, nslots, which, name):
+    """T1D_scan (539-623) / T2D_scan (686-776): {label: {"snp_count", name}} per non-empty fixed-bp
+    window, the statistic None for an empty window or background (no guard, no derived terms).
+    which: 2 = T2D, 1 = the first population's T1D."""
+    names = packed.chrom_names
+    res = {}
+    for r in _windows(recs, nslots):
+        s = 1 + int(r["wid"]) * ws
+        res[f"{names[int(r['chrom'])]} {s}-{s + ws - 1}"] = {"snp_count": int(r["snp_count"]), name: _v(r, which)}
+    return res
+
+
 def bysnp_scan(recs, packed, S, with_diff, final_warning):
     """scan_chooseChr_bySNPs (1303-1420) / scan_perChr_bySNPs (1422-1541)."""
     names = packed.chrom_names

@@ -203,41 +203,68 @@ def process_windows_batch(replicates, bg_2d_sfs, bg_p1_sfs, bg_p2_sfs, window_si
     return out
 
 
-def likelihood_scan(main_dir, output, popinfo_filename, pop1='p1', pop2='p2', pop1_size=5, pop2_size=5,
-                    window_size=500000, bg_end=500000):
-    """sims_scan.py:593-644: per generation, background = the concatenated VCF's SNPs with
-    pos in [0, bg_end] (2D folded, 1D unfolded); every replicate VCF scanned in fixed windows.
-    The reference hard-codes the popmap path and sizes; here they are arguments.  The replicates of a
-    generation are parsed by the native VCF reader and scanned in one launch
-    (``process_windows_batch``); rows come out in the reference's order."""
+def _generation_scans(main_dir, popinfo_filename, pop1, pop2, pop1_size, pop2_size, window_size, bg_end):
+    """The loops shared by both ``likelihood_scan`` variants (sims_scan.py:607-622 / 657-671):
+    yields (generation, iteration number, window coords, process_window result) in the reference's
+    order -- generations in get_gens' set order, targets in glob order, windows in scan order.  Per
+    generation, background = the concatenated VCF's SNPs with pos in [0, bg_end] (2D folded, 1D
+    unfolded); the replicates of a generation are parsed by the native VCF reader and scanned in one
+    launch (``process_windows_batch``)."""
     from sfs2d.vcf import read_vcf
-    generations = get_gens(main_dir)
+    for generation in get_gens(main_dir):
+        target_vcfs = glob.glob(f"{main_dir}/iter*/*{generation}*.vcf.gz")
+        concatenated_vcfs = glob.glob(f"{main_dir}/concatenated_vcfs/gen.{generation}.concatenated.vcf.gz")
+        for vcf in concatenated_vcfs:
+            bgp = read_vcf(vcf, popinfo_filename).to_packed(pop1, pop2)
+            bg_2d_sfs = calculate_2d_sfs(bgp, pop1, pop2, pop1_size, pop2_size, start_position=0,
+                                         end_position=bg_end, variant_type=None)
+            bg_p1_sfs = calculate_1d_sfs(bgp, pop1, pop1_size, start_position=0, end_position=bg_end,
+                                         variant_type=None)
+            bg_p2_sfs = calculate_1d_sfs(bgp, pop2, pop2_size, start_position=0, end_position=bg_end,
+                                         variant_type=None)
+            targets = [read_vcf(v, popinfo_filename).to_packed(pop1, pop2) for v in target_vcfs]
+            batch = process_windows_batch(targets, bg_2d_sfs, bg_p1_sfs, bg_p2_sfs, window_size, pop1, pop2,
+                                          pop1_size, pop2_size)
+            for vcf_input, results in zip(target_vcfs, batch):
+                iteration_number = int(vcf_input.split('.')[2])
+                for window_coords, result in results.items():
+                    yield generation, iteration_number, window_coords, result
+
+
+def likelihood_scan(main_dir, output=None, popinfo_filename=None, pop1='p1', pop2='p2', pop1_size=5, pop2_size=5,
+                    window_size=500000, bg_end=500000):
+    """Both reference variants.  ``likelihood_scan(main_dir)`` (sims_scan.py:646-690, the definition
+    the module keeps): returns {(generation, iteration, window_coords): {"generation", "iteration",
+    "region", "window_coords", "likelihood": process_window's record}}.  With ``output``
+    (sims_scan.py:593-644): writes the per-window CSV instead and returns None.  The reference
+    hard-codes the popmap path and the sizes; here they are arguments (``popinfo_filename`` defaults
+    to $SFS2D_SIMS_POPMAP; a missing file raises FileNotFoundError, as the reference's open of its
+    absolute path does elsewhere)."""
+    if popinfo_filename is None:
+        popinfo_filename = os.environ.get("SFS2D_SIMS_POPMAP", "popmap_sims_copy.txt")
+    if not os.path.exists(popinfo_filename):
+        raise FileNotFoundError(f"[Errno 2] No such file or directory: '{popinfo_filename}'")
+    scans = _generation_scans(main_dir, popinfo_filename, pop1, pop2, pop1_size, pop2_size, window_size, bg_end)
+    if output is None:
+        likelihood_results = {}
+        for generation, iteration_number, key, value in scans:
+            window_start, window_end = map(int, key.split(' ')[1].split('-'))
+            region = 'background' if window_end <= 1000000 else 'foreground'
+            likelihood_results[(generation, iteration_number, key)] = {
+                'generation': generation, 'iteration': iteration_number, 'region': region,
+                'window_coords': key, 'likelihood': value}
+        return likelihood_results
     col_names = ['generation', 'iteration', 'region', 'window_coords', 'snp_count', 'T2D', 'T1D_p1', 'T1D_p2',
                  'new_term_p1', 'new_term_p2', 'T2D_diff']
     with open(output, 'w', newline='') as csvfile:
         writer = csv.DictWriter(csvfile, fieldnames=col_names)
         writer.writeheader()
-        for generation in generations:
-            target_vcfs = glob.glob(f"{main_dir}/iter*/*{generation}*.vcf.gz")
-            concatenated_vcfs = glob.glob(f"{main_dir}/concatenated_vcfs/gen.{generation}.concatenated.vcf.gz")
-            for vcf in concatenated_vcfs:
-                bgp = read_vcf(vcf, popinfo_filename).to_packed(pop1, pop2)
-                bg_2d_sfs = calculate_2d_sfs(bgp, pop1, pop2, pop1_size, pop2_size, start_position=0,
-                                             end_position=bg_end, variant_type=None)
-                bg_p1_sfs = calculate_1d_sfs(bgp, pop1, pop1_size, start_position=0, end_position=bg_end,
-                                             variant_type=None)
-                bg_p2_sfs = calculate_1d_sfs(bgp, pop2, pop2_size, start_position=0, end_position=bg_end,
-                                             variant_type=None)
-                targets = [read_vcf(v, popinfo_filename).to_packed(pop1, pop2) for v in target_vcfs]
-                batch = process_windows_batch(targets, bg_2d_sfs, bg_p1_sfs, bg_p2_sfs, window_size, pop1, pop2,
-                                              pop1_size, pop2_size)
-                for vcf_input, results in zip(target_vcfs, batch):
-                    iteration_number = int(vcf_input.split('.')[2])
-                    for window_coords, result in results.items():
-                        window_start, window_end = window_coords.split(' ')[1].split('-')
-                        region = 'background' if int(window_end) <= 1000000 else 'foreground'
-                        writer.writerow({'generation': generation, 'iteration': iteration_number, 'region': region,
-                                         'window_coords': window_coords, 'snp_count': result["snp_count"],
-                                         'T2D': result["T2D"], 'T1D_p1': result["T1D_p1"], 'T1D_p2': result["T1D_p2"],
-                                         'new_term_p1': result["new_term_p1"], 'new_term_p2': result["new_term_p2"],
-                                         'T2D_diff': result["T2D_diff"]})
+        for generation, iteration_number, window_coords, result in scans:
+            window_start, window_end = window_coords.split(' ')[1].split('-')
+            region = 'background' if int(window_end) <= 1000000 else 'foreground'
+            writer.writerow({'generation': generation, 'iteration': iteration_number, 'region': region,
+                             'window_coords': window_coords, 'snp_count': result["snp_count"],
+                             'T2D': result["T2D"], 'T1D_p1': result["T1D_p1"], 'T1D_p2': result["T1D_p2"],
+                             'new_term_p1': result["new_term_p1"], 'new_term_p2': result["new_term_p2"],
+                             'T2D_diff': result["T2D_diff"]})
+    return None

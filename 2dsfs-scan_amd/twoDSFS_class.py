@@ -21,7 +21,7 @@ from sfs2d import _lib as L
 from sfs2d import post
 from sfs2d.engine import Engine, ScanConfig
 from sfs2d.vcf import make_data_dict_vcf as _make_data_dict_vcf
-from sfs2d.pack import PackedSNPs, pack_snp_dict
+from sfs2d.pack import PackedSNPs, last_key_index, pack_snp_dict, shadow_chrom_starts
 
 __all__ = ["LikelihoodInference_jointSFS", "save_csv_stats", "col_names", "chr_ids", "load_chr_ids"]
 
@@ -186,6 +186,56 @@ class LikelihoodInference_jointSFS:
         recs = self._scan(p, self._cfg(p, window_mode=L.WINDOW_SNPS, window=snp_window_size,
                                        bg_mode=L.BG_PER_CHROM))
         return post.bysnp_scan(recs, p, snp_window_size, with_diff=True, final_warning=False)
+
+    # ------------------------------------------------------------------ single-statistic scans
+    def _filters(self, p: PackedSNPs):
+        ann = -1
+        if self.variant_type is not None:
+            ann = p.ann_names.index(self.variant_type) if self.variant_type in p.ann_names else _NO_ANN
+        return ann
+
+    def T1D_scan(self, data_dict, background_sfs, window_size, pop, pop_size):
+        """T1D of population ``pop`` (``pop_size`` individuals) per fixed-bp window against a supplied
+        folded 1D background (twoDSFS_class.py:539-623): raw alt counts of ``pop`` (no joint fold),
+        folded against 2*pop_size (:576-578), the constructor's position / variant_type filters.
+        Returns {label: {"snp_count", "T1D"}}; T1D None for an empty window or background."""
+        self.data_dict = data_dict
+        self.background_sfs = background_sfs
+        self.window_size = window_size
+        self.pop = pop
+        self.pop_size = pop_size
+        p = self._pack(data_dict, pop1=pop, pop2=pop).single_pop(pop)
+        if p.n == 0:
+            return {}
+        n = 2 * int(pop_size)
+        # pop in both count slots, no fold: the 2D key (alt, alt) is in the grid exactly when the 1D
+        # key is; the 2D statistic (against a dummy background) is not read
+        cfg = ScanConfig(n1p=pop_size, n2p=pop_size, fold=False, ann_want=self._filters(p),
+                         start_position=None if self.start_position is None else int(self.start_position),
+                         end_position=None if self.end_position is None else int(self.end_position),
+                         window_mode=L.WINDOW_BP, window=window_size, bg_mode=L.BG_SUPPLIED)
+        bg = (np.ones((n + 1) * (n + 1)), self._bg1d_array(background_sfs, pop_size), np.ones(pop_size + 1))
+        recs = self._scan(p, cfg, bg)
+        return post.single_stat_scan(recs, p, window_size, post.num_slots(recs), 1, "T1D")
+
+    def T2D_scan(self, data_dict, background_2d_sfs, window_size):
+        """T2D per fixed-bp window against the SUPPLIED background (twoDSFS_class.py:686-776).  The
+        per-chromosome background the reference computes at each chromosome change (:738-744) is not
+        used for scoring (:753, :768 read ``self.background_2d_sfs``), but its loop rebinds the SNP key:
+        the stream is rebuilt accordingly (``sfs2d.pack.shadow_chrom_starts``).
+        Returns {label: {"snp_count", "T2D"}}; T2D None for an empty window or background."""
+        self.data_dict = data_dict
+        self.background_2d_sfs = background_2d_sfs
+        self.window_size = window_size
+        p = self._pack(data_dict)
+        if p.n == 0:
+            return {}
+        q = shadow_chrom_starts(p, last_key_index(data_dict, p), window_size, self.start_position, self.end_position)
+        cfg = ScanConfig(n1p=self.pop1_size, n2p=self.pop2_size, fold=bool(self.fold), ann_want=self._filters(q),
+                         window_mode=L.WINDOW_BP, window=window_size, bg_mode=L.BG_SUPPLIED)
+        bg = (self._bg2d_array(background_2d_sfs), np.ones(self.pop1_size + 1), np.ones(self.pop2_size + 1))
+        recs = self._scan(q, cfg, bg)
+        return post.single_stat_scan(recs, q, window_size, post.num_slots(recs), 2, "T2D")
 
     # ------------------------------------------------------------------ multi-resolution (extension)
     def multi_scan(self, data_dict, window_sizes=(), snp_window_sizes=(), fst=False):

@@ -17,7 +17,8 @@ per-window algorithm of ``scripts/src/twoDSFS_class.py`` (class
 * 1D SFS / fold ................. twoDSFS_class.py:398-463  (sims_scan.py:262-322)
 * normalisation ................. twoDSFS_class.py:234-247, 465-476
 * multinomial CLR T1D / T2D ..... twoDSFS_class.py:478-537, 625-684 (sims_scan.py:325-440)
-* drivers (windows, bg, quirks) . combined_scan 787-991, scan_chooseChr 993-1159,
+* drivers (windows, bg, quirks) . T1D_scan 539-623, T2D_scan 686-776,
+                                  combined_scan 787-991, scan_chooseChr 993-1159,
                                   scan_precomputed_BG 1161-1299,
                                   scan_chooseChr_bySNPs 1303-1420,
                                   scan_perChr_bySNPs 1422-1541,
@@ -343,6 +344,64 @@ def scan_chooseChr_bySNPs(p, S, bg_chrom, cfg):
 def scan_perChr_bySNPs(p, S, cfg):
     bgs = chrom_backgrounds(p, cfg)
     return _bysnp_scan(p, S, cfg, lambda c: bgs[c], with_diff=True)
+
+
+def T1D_scan(p, ws, bg1d, pop, pop_size, cfg):
+    """twoDSFS_class.py:539-623: fixed-bp windows, calculate_1d_sfs of ``pop`` (raw alt counts, the
+    constructor's filters), fold_1d_sfs, calculate_likelihood_1D against the supplied ``bg1d``."""
+    which = 1 if pop == p.pop1 else (2 if pop == p.pop2 else 0)
+    c1 = Cfg(pop_size, pop_size, cfg.variant_type, cfg.fold, cfg.start_position, cfg.end_position)
+    res = {}
+    for (c, start, b, e) in bp_windows(p, ws):
+        idx = np.arange(b, e)
+        if which:
+            u = sfs1d(p, idx, which, c1)
+        else:   # calls.get(pop, (0, 0)): no SNP enters the spectrum
+            u = np.zeros(2 * pop_size + 1, np.int64)
+        res[f"{p.chrom_names[c]} {start}-{start + ws - 1}"] = {
+            "snp_count": count_snps(p, b, e, cfg), "T1D": clr1d(fold1d(u), bg1d)}
+    return res
+
+
+def T2D_scan(p, ws, bg2, cfg, last=None):
+    """twoDSFS_class.py:686-776, restated as the reference's own loop over the sorted SNPs with a
+    window dict keyed by SNP.  At each chromosome change the per-chromosome background loop (:740)
+    rebinds ``snp_key`` to the data dict's last key (``last``: its index in p; default the last SNP,
+    the order to_snp_dict inserts), so that key -- its calls, annotation and key position -- enters
+    the window in place of the chromosome's first SNP (:748 / :763).  Scored against the supplied
+    ``bg2`` (:753, :768)."""
+    last = p.n - 1 if last is None else int(last)
+    chrom = p.chrom_of()
+    res = {}
+    cur, start, win = None, 0, {}
+
+    def emit():
+        idx = np.array(list(win), dtype=np.int64)   # keys = SNP indices; sfs2d filters by p.pos[key]
+        res[f"{p.chrom_names[cur]} {start}-{start + ws - 1}"] = {
+            "snp_count": count_snps_idx(p, idx, cfg), "T2D": clr2d(sfs2d(p, idx, cfg), bg2)}
+
+    for i in range(p.n):
+        c, q, key = int(chrom[i]), int(p.pos[i]), i
+        if c != cur:
+            if win:
+                emit()
+            cur, start, win = c, 1, {}
+            key = last
+        if q < start + ws:
+            win[key] = True
+        else:
+            if win:
+                emit()
+            start += ws * ((q - start) // ws)
+            win = {key: True}
+    if win:
+        emit()
+    return res
+
+
+def count_snps_idx(p, idx, cfg):
+    vm = p.variant_mask(cfg.variant_type)
+    return len(idx) if vm is None else int(vm[idx].sum())
 
 
 def sims_backgrounds(p, n1p, n2p, start=0, end=500000, variant_type=None):

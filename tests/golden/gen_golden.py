@@ -93,11 +93,21 @@ def dense2d(sfs, n1, n2):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-chr1", action="store_true")
+    ap.add_argument("--only", default="", help="comma list of sections to (re)generate (A-F, C2, pub); "
+                                               "the other cases stay as the manifest has them")
     args = ap.parse_args()
+    only = [x for x in args.only.split(",") if x]
+
+    def want(sec):
+        return not only or sec in only
     cls_mod = load_reference_module(f"{REF}/scripts/src/twoDSFS_class.py", "ref_twoDSFS_class")
     sims = load_reference_module(f"{REF}/scripts/sims_scan.py", "ref_sims_scan")
     L = cls_mod.LikelihoodInference_jointSFS
+    mpath = os.path.join(HERE, "manifest.json")
     manifest = {}
+    if only and os.path.exists(mpath):   # partial regeneration: keep the other cases
+        with open(mpath) as fh:
+            manifest = json.load(fh)
 
     def case(name, packed, cfg, calls, note=""):
         save_packed(os.path.join(HERE, f"{name}.npz"), packed)
@@ -106,13 +116,36 @@ def main():
               + ", ".join(f"{c['fn']}{'' if c['out']['ok'] else '!' + c['out']['error']}"
                           f" {c['out']['seconds']:.2f}s" for c in calls), flush=True)
 
+    def new_obj(cfg):
+        return L(None, None, start_position=cfg.get("start_position"), end_position=cfg.get("end_position"),
+                 pop1=cfg["pop1"], pop2=cfg["pop2"], pop1_size=cfg["n1p"], pop2_size=cfg["n2p"],
+                 variant_type=cfg.get("variant_type"), fold=cfg.get("fold", True))
+
     def class_calls(d, cfg, specs):
-        obj = L(None, None, start_position=cfg.get("start_position"), end_position=cfg.get("end_position"),
-                pop1=cfg["pop1"], pop2=cfg["pop2"], pop1_size=cfg["n1p"], pop2_size=cfg["n2p"],
-                variant_type=cfg.get("variant_type"), fold=cfg.get("fold", True))
+        obj = new_obj(cfg)
         calls = []
         for fn, a in specs:
-            if fn == "scan_precomputed_BG":
+            if fn in ("T2D_scan", "T1D_scan"):
+                # args: [bg ("norm" | "raw"), window, (pop, pop_size,) last_key]: the background is the
+                # whole data set's 2D / folded 1D SFS (a fresh object, the same filters), normalised or
+                # not; last_key (None = the scan-order dict) is moved to the end of the data dict --
+                # T2D_scan reads the dict's last key (twoDSFS_class.py:740)
+                b = new_obj(cfg)
+                dd = dict(d)
+                if a[-1] is not None:
+                    dd[a[-1]] = dd.pop(a[-1])
+                if fn == "T2D_scan":
+                    bg = b.calculate_2d_sfs(d)
+                    if a[0] == "norm":
+                        bg = b.normalize_2d_sfs(bg)
+                    out = run(obj.T2D_scan, dd, bg, a[1])
+                else:
+                    bg = b.fold_1d_sfs(b.calculate_1d_sfs(d, a[2], a[3], b.start_position, b.end_position,
+                                                          b.variant_type))
+                    if a[0] == "norm":
+                        bg = b.normalize_1d_sfs(bg)
+                    out = run(obj.T1D_scan, dd, bg, a[1], a[2], a[3])
+            elif fn == "scan_precomputed_BG":
                 # script cell twoDSFS_class.py:1970-1981 (genome-wide normalised backgrounds)
                 bg2 = obj.normalize_2d_sfs(obj.calculate_2d_sfs(d))
                 bg1 = obj.normalize_1d_sfs(obj.fold_1d_sfs(obj.calculate_1d_sfs(
@@ -126,7 +159,7 @@ def main():
         return calls
 
     # ---------------------------------------------------------------- A. real chr1 (config 1)
-    if not args.skip_chr1:
+    if want('A') and not args.skip_chr1:
         d = load_snp_dict_pkl(f"{REF}/data/chr1.pkl.bz2")
         p = pack_snp_dict(d, "uv", "bv")
         cfg = dict(pop1="uv", pop2="bv", n1p=18, n2p=14)
@@ -155,44 +188,160 @@ def main():
         del d
 
     # ---------------------------------------------------------------- B. synthetic n1=n2=50
-    p = synth_genome(3, [9000, 7000, 300], 25, 25, seed=1, n_ann=3)
-    d = to_snp_dict(p)
-    cfg = dict(pop1="p1", pop2="p2", n1p=25, n2p=25)
-    calls = class_calls(d, cfg, [("combined_scan", [20000]), ("combined_scan", [100000]),
-                                 ("scan_perChr_bySNPs", [300]), ("scan_chooseChr", [20000, "chr0001"]),
-                                 ("scan_precomputed_BG", [50000]), ("scan_chooseChr_bySNPs", [250, "chr0000"])])
-    case("synth_n50", p, cfg, calls, "SURVEY 8d generator, seed 1, pop 25/25 (config 2 shape, small)")
+    if want('B'):
+        p = synth_genome(3, [9000, 7000, 300], 25, 25, seed=1, n_ann=3)
+        d = to_snp_dict(p)
+        cfg = dict(pop1="p1", pop2="p2", n1p=25, n2p=25)
+        calls = class_calls(d, cfg, [("combined_scan", [20000]), ("combined_scan", [100000]),
+                                     ("scan_perChr_bySNPs", [300]), ("scan_chooseChr", [20000, "chr0001"]),
+                                     ("scan_precomputed_BG", [50000]), ("scan_chooseChr_bySNPs", [250, "chr0000"])])
+        case("synth_n50", p, cfg, calls, "SURVEY 8d generator, seed 1, pop 25/25 (config 2 shape, small)")
 
-    cfg_f = dict(cfg, variant_type="intron_variant", start_position=50000, end_position=350000)
-    calls = class_calls(d, cfg_f, [("combined_scan", [20000]), ("scan_perChr_bySNPs", [200]),
-                                   ("scan_precomputed_BG", [40000])])
-    case("synth_n50_filters", p, cfg_f, calls, "variant_type + start/end position filters")
+        cfg_f = dict(cfg, variant_type="intron_variant", start_position=50000, end_position=350000)
+        calls = class_calls(d, cfg_f, [("combined_scan", [20000]), ("scan_perChr_bySNPs", [200]),
+                                       ("scan_precomputed_BG", [40000])])
+        case("synth_n50_filters", p, cfg_f, calls, "variant_type + start/end position filters")
 
-    cfg_f2 = dict(cfg, variant_type="intron_variant", end_position=300000)
-    calls = class_calls(d, cfg_f2, [("combined_scan", [50000]), ("scan_chooseChr_bySNPs", [150, "chr0000"])])
-    case("synth_n50_filters2", p, cfg_f2, calls, "variant_type + end_position (windows past it: N=0 -> stale)")
+        cfg_f2 = dict(cfg, variant_type="intron_variant", end_position=300000)
+        calls = class_calls(d, cfg_f2, [("combined_scan", [50000]), ("scan_chooseChr_bySNPs", [150, "chr0000"])])
+        case("synth_n50_filters2", p, cfg_f2, calls, "variant_type + end_position (windows past it: N=0 -> stale)")
 
-    cfg_u = dict(cfg, fold=False)
-    calls = class_calls(d, cfg_u, [("combined_scan", [20000]), ("scan_perChr_bySNPs", [300])])
-    case("synth_n50_nofold", p, cfg_u, calls, "fold=False")
+        cfg_u = dict(cfg, fold=False)
+        calls = class_calls(d, cfg_u, [("combined_scan", [20000]), ("scan_perChr_bySNPs", [300])])
+        case("synth_n50_nofold", p, cfg_u, calls, "fold=False")
 
     # ---------------------------------------------------------------- C. asymmetric 200x150 (config 5)
-    p = synth_genome(1, 6000, 100, 75, seed=5)
-    d = to_snp_dict(p)
-    cfg = dict(pop1="p1", pop2="p2", n1p=100, n2p=75)
-    calls = class_calls(d, cfg, [("scan_perChr_bySNPs", [500]), ("combined_scan", [20000])])
-    case("synth_200x150", p, cfg, calls, "config 5 shape, small")
+    if want('C'):
+        p = synth_genome(1, 6000, 100, 75, seed=5)
+        d = to_snp_dict(p)
+        cfg = dict(pop1="p1", pop2="p2", n1p=100, n2p=75)
+        calls = class_calls(d, cfg, [("scan_perChr_bySNPs", [500]), ("combined_scan", [20000])])
+        case("synth_200x150", p, cfg, calls, "config 5 shape, small")
 
     # ---------------------------------------------------------------- C2. n1=n2=100 (config 4 grid)
-    p = synth_genome(1, 5000, 50, 50, seed=4)
-    d = to_snp_dict(p)
-    cfg = dict(pop1="p1", pop2="p2", n1p=50, n2p=50)
-    calls = class_calls(d, cfg, [("combined_scan", [20000])])
-    case("synth_n100", p, cfg, calls, "config 4 grid (101x101), small")
+    if want('C2'):
+        p = synth_genome(1, 5000, 50, 50, seed=4)
+        d = to_snp_dict(p)
+        cfg = dict(pop1="p1", pop2="p2", n1p=50, n2p=50)
+        calls = class_calls(d, cfg, [("combined_scan", [20000])])
+        case("synth_n100", p, cfg, calls, "config 4 grid (101x101), small")
 
     # ---------------------------------------------------------------- D. quirks Q5/Q6/Q9
-    def build(chroms, n1p=3, n2p=3):
-        """chroms: list of (name, [(pos, r1, a1, r2, a2), ...])"""
+    if want('D'):
+        def build(chroms, n1p=3, n2p=3):
+            """chroms: list of (name, [(pos, r1, a1, r2, a2), ...])"""
+            names = sorted(c for c, _ in chroms)
+            by = dict(chroms)
+            cs, ps, offs = [], [], [0]
+            for nme in names:
+                rows = sorted(by[nme])
+                ps += [r[0] for r in rows]
+                cs.append(pack_counts([r[1] for r in rows], [r[2] for r in rows], [r[3] for r in rows],
+                                      [r[4] for r in rows]))
+                offs.append(offs[-1] + len(rows))
+            return PackedSNPs(np.concatenate(cs), np.array(ps, np.uint32), np.array(offs), names,
+                              np.zeros(len(ps), np.uint16), ["intergenic_region"], "A", "B")
+
+        rng = np.random.default_rng(7)
+
+        def rand_rows(n, lo, hi, n1p=3, n2p=3):
+            pos = np.sort(rng.choice(np.arange(lo, hi), size=n, replace=False))
+            out = []
+            for q in pos:
+                a1 = int(rng.integers(0, 2 * n1p + 1))
+                a2 = int(rng.integers(0, 2 * n2p + 1))
+                out.append((int(q), 2 * n1p - a1, a1, 2 * n2p - a2, a2))
+            return out
+
+        mono = lambda q: (q, 6, 0, 6, 0)            # (0,0) after fold -> skipped from every SFS
+        half1 = lambda q, a2: (q, 3, 3, 6 - a2, a2)  # pop1 MAF 1/2 -> excluded 1D bin (Q3)
+        cfg = dict(pop1="A", pop2="B", n1p=3, n2p=3)
+        qcases = {
+            # chrA: 4 windows; window 3 is all-monomorphic (T2D None -> stale carry)
+            # chrB: single window -> T2D == 0.0 exactly (bg == window, Q5) -> stale carry (Q6)
+            # chrC: windows with T1D_pop1 None (pop1 only MAF 1/2) and a normal last window
+            "q_stale": [("chrA", rand_rows(30, 1, 300) + [mono(310), mono(350)] + rand_rows(20, 400, 700)),
+                        ("chrB", rand_rows(15, 1, 90)),
+                        ("chrC", rand_rows(25, 1, 200) + [half1(210, 1), half1(220, 2), half1(230, 0)]
+                         + rand_rows(12, 300, 390))],
+            # last window: previous window has T1D_pop2 None -> final window dropped (Q9)
+            "q_last_drop": [("chrA", rand_rows(30, 1, 200) + [(210, 5, 1, 3, 3), (220, 4, 2, 3, 3)]
+                             + rand_rows(10, 300, 399))],
+            # last window: previous T1D_pop1 None -> final T1D_pop2 from previous window's SFS (Q9)
+            "q_last_prev1": [("chrA", rand_rows(30, 1, 200) + [half1(205, 1), half1(215, 2)]),
+                             ("chrB", rand_rows(10, 1, 99))],
+            # last window (own chromosome) has T2D None -> its T1D_pop1 uses the previous window's SFS
+            "q_last_t2dnone": [("chrA", rand_rows(40, 1, 300)), ("chrB", [mono(5), mono(50)])],
+            # first window fails the guard -> UnboundLocalError in the reference
+            "q_first_unbound": [("chrA", [mono(3), mono(20)] + rand_rows(20, 100, 400))],
+            # one window in the whole scan -> UnboundLocalError at the final block
+            "q_single": [("chrA", rand_rows(20, 1, 99))],
+        }
+        for name, chroms in qcases.items():
+            p = build(chroms)
+            d = to_snp_dict(p)
+            specs = [("combined_scan", [100])]
+            if name == "q_stale":
+                specs += [("scan_chooseChr", [100, "chrA"]), ("scan_perChr_bySNPs", [7]),
+                          ("scan_chooseChr_bySNPs", [6, "chrC"]), ("scan_precomputed_BG", [100])]
+            calls = class_calls(d, cfg, specs)
+            case(name, p, cfg, calls, "hand-built quirk case")
+
+    # ---------------------------------------------------------------- E. sims_scan (config 4 semantics)
+    if want('E'):
+        for tag, npop, nbg, nrep in [("sims_n10", 5, 6000, 3000), ("sims_n100", 50, 6000, 3000)]:
+            bgp = synth_genome(1, nbg, npop, npop, seed=11, pop1="p1", pop2="p2", chrom_prefix="")
+            bgp.chrom_names = ["1"]
+            rep = synth_genome(1, nrep, npop, npop, seed=12, pop1="p1", pop2="p2", chrom_prefix="")
+            rep.chrom_names = ["1"]
+            # replicate positions spread over ~4 Mb so there are several 500 kb windows
+            rep.pos = np.cumsum(np.full(rep.n, 4_000_000 // nrep, np.int64)).astype(np.uint32)
+            bd = to_snp_dict(bgp)
+            rd = to_snp_dict(rep)
+            bg2 = sims.calculate_2d_sfs(bd, 'p1', 'p2', npop, npop, start_position=0, end_position=500000,
+                                        variant_type=None)
+            bg1 = sims.calculate_1d_sfs(bd, 'p1', npop, start_position=0, end_position=500000, variant_type=None)
+            bg1b = sims.calculate_1d_sfs(bd, 'p2', npop, start_position=0, end_position=500000, variant_type=None)
+            out = run(sims.process_window, rd, bg2, bg1, bg1b, 500000, 'p1', 'p2', npop, npop,
+                      start_position=None, end_position=None, variant_type=None)
+            save_packed(os.path.join(HERE, f"{tag}_bgdata.npz"), bgp)
+            np.savez_compressed(os.path.join(HERE, f"{tag}_bg.npz"),
+                                bg2d=dense2d(bg2, 2 * npop, 2 * npop).astype(np.int64),
+                                bg1a=np.array([bg1[k] for k in range(2 * npop + 1)], np.int64),
+                                bg1b=np.array([bg1b[k] for k in range(2 * npop + 1)], np.int64))
+            case(tag, rep, dict(pop1="p1", pop2="p2", n1p=npop, n2p=npop),
+                 [{"fn": "sims_process_window", "args": [500000], "out": out}],
+                 "sims_scan.process_window with the sims bg (pos <= 500 kb, unfolded 1D)")
+
+    # ---------------------------------------------------------------- F. T1D_scan / T2D_scan
+    if want('F'):
+        # the synth_n50 data (3 chromosomes; the last one's 300 SNPs span one 20 kb window, so T2D_scan's
+        # substituted first SNP and the data dict's last key collapse there)
+        p = synth_genome(3, [9000, 7000, 300], 25, 25, seed=1, n_ann=3)
+        d = to_snp_dict(p)
+        mid = list(d)[12000]   # a key inside chr0001: another last key for T2D_scan's rebinding
+        first1 = list(d)[9000]  # the first SNP of chr0001 as the last key (no substitution there)
+        cfg = dict(pop1="p1", pop2="p2", n1p=25, n2p=25)
+        calls = class_calls(d, cfg, [("T2D_scan", ["norm", 20000, None]), ("T2D_scan", ["raw", 100000, mid]),
+                                     ("T2D_scan", ["norm", 20000, first1]),
+                                     ("T1D_scan", ["norm", 20000, "p1", 25, None]),
+                                     ("T1D_scan", ["raw", 50000, "p2", 25, None]),
+                                     ("T1D_scan", ["norm", 20000, "p1", 30, None]),
+                                     ("T1D_scan", ["raw", 20000, "zz", 25, None])])
+        case("t12_n50", p, cfg, calls, "T1D_scan / T2D_scan on the synth_n50 data")
+        cfg_f = dict(cfg, variant_type="intron_variant", start_position=50000, end_position=350000)
+        calls = class_calls(d, cfg_f, [("T2D_scan", ["norm", 20000, None]), ("T2D_scan", ["raw", 20000, mid]),
+                                       ("T1D_scan", ["norm", 20000, "p2", 25, None])])
+        case("t12_n50_filters", p, cfg_f, calls, "T1D_scan / T2D_scan with variant_type + position filters "
+                                                 "(the substituted key's position filtered)")
+        # quirk data (n = 3): empty windows / MAF-1/2-only windows -> None statistics
+        rng = np.random.default_rng(7)
+        chroms = [("chrA", [(q, 6 - a1, a1, 6 - a2, a2) for q, a1, a2 in
+                            zip(sorted(rng.choice(np.arange(1, 600), 40, replace=False).tolist()),
+                                rng.integers(0, 7, 40).tolist(), rng.integers(0, 7, 40).tolist())]
+                   + [(610, 6, 0, 6, 0), (650, 6, 0, 6, 0), (720, 3, 3, 5, 1), (730, 3, 3, 4, 2)]),
+                  ("chrB", [(5, 6, 0, 6, 0), (50, 6, 0, 6, 0)]),
+                  ("chrC", [(q, 5, 1, 6, 0) for q in (3, 40, 70)])]
         names = sorted(c for c, _ in chroms)
         by = dict(chroms)
         cs, ps, offs = [], [], [0]
@@ -202,81 +351,17 @@ def main():
             cs.append(pack_counts([r[1] for r in rows], [r[2] for r in rows], [r[3] for r in rows],
                                   [r[4] for r in rows]))
             offs.append(offs[-1] + len(rows))
-        return PackedSNPs(np.concatenate(cs), np.array(ps, np.uint32), np.array(offs), names,
-                          np.zeros(len(ps), np.uint16), ["intergenic_region"], "A", "B")
-
-    rng = np.random.default_rng(7)
-
-    def rand_rows(n, lo, hi, n1p=3, n2p=3):
-        pos = np.sort(rng.choice(np.arange(lo, hi), size=n, replace=False))
-        out = []
-        for q in pos:
-            a1 = int(rng.integers(0, 2 * n1p + 1))
-            a2 = int(rng.integers(0, 2 * n2p + 1))
-            out.append((int(q), 2 * n1p - a1, a1, 2 * n2p - a2, a2))
-        return out
-
-    mono = lambda q: (q, 6, 0, 6, 0)            # (0,0) after fold -> skipped from every SFS
-    half1 = lambda q, a2: (q, 3, 3, 6 - a2, a2)  # pop1 MAF 1/2 -> excluded 1D bin (Q3)
-    cfg = dict(pop1="A", pop2="B", n1p=3, n2p=3)
-    qcases = {
-        # chrA: 4 windows; window 3 is all-monomorphic (T2D None -> stale carry)
-        # chrB: single window -> T2D == 0.0 exactly (bg == window, Q5) -> stale carry (Q6)
-        # chrC: windows with T1D_pop1 None (pop1 only MAF 1/2) and a normal last window
-        "q_stale": [("chrA", rand_rows(30, 1, 300) + [mono(310), mono(350)] + rand_rows(20, 400, 700)),
-                    ("chrB", rand_rows(15, 1, 90)),
-                    ("chrC", rand_rows(25, 1, 200) + [half1(210, 1), half1(220, 2), half1(230, 0)]
-                     + rand_rows(12, 300, 390))],
-        # last window: previous window has T1D_pop2 None -> final window dropped (Q9)
-        "q_last_drop": [("chrA", rand_rows(30, 1, 200) + [(210, 5, 1, 3, 3), (220, 4, 2, 3, 3)]
-                         + rand_rows(10, 300, 399))],
-        # last window: previous T1D_pop1 None -> final T1D_pop2 from previous window's SFS (Q9)
-        "q_last_prev1": [("chrA", rand_rows(30, 1, 200) + [half1(205, 1), half1(215, 2)]),
-                         ("chrB", rand_rows(10, 1, 99))],
-        # last window (own chromosome) has T2D None -> its T1D_pop1 uses the previous window's SFS
-        "q_last_t2dnone": [("chrA", rand_rows(40, 1, 300)), ("chrB", [mono(5), mono(50)])],
-        # first window fails the guard -> UnboundLocalError in the reference
-        "q_first_unbound": [("chrA", [mono(3), mono(20)] + rand_rows(20, 100, 400))],
-        # one window in the whole scan -> UnboundLocalError at the final block
-        "q_single": [("chrA", rand_rows(20, 1, 99))],
-    }
-    for name, chroms in qcases.items():
-        p = build(chroms)
+        p = PackedSNPs(np.concatenate(cs), np.array(ps, np.uint32), np.array(offs), names,
+                       np.zeros(len(ps), np.uint16), ["intergenic_region"], "A", "B")
         d = to_snp_dict(p)
-        specs = [("combined_scan", [100])]
-        if name == "q_stale":
-            specs += [("scan_chooseChr", [100, "chrA"]), ("scan_perChr_bySNPs", [7]),
-                      ("scan_chooseChr_bySNPs", [6, "chrC"]), ("scan_precomputed_BG", [100])]
-        calls = class_calls(d, cfg, specs)
-        case(name, p, cfg, calls, "hand-built quirk case")
-
-    # ---------------------------------------------------------------- E. sims_scan (config 4 semantics)
-    for tag, npop, nbg, nrep in [("sims_n10", 5, 6000, 3000), ("sims_n100", 50, 6000, 3000)]:
-        bgp = synth_genome(1, nbg, npop, npop, seed=11, pop1="p1", pop2="p2", chrom_prefix="")
-        bgp.chrom_names = ["1"]
-        rep = synth_genome(1, nrep, npop, npop, seed=12, pop1="p1", pop2="p2", chrom_prefix="")
-        rep.chrom_names = ["1"]
-        # replicate positions spread over ~4 Mb so there are several 500 kb windows
-        rep.pos = np.cumsum(np.full(rep.n, 4_000_000 // nrep, np.int64)).astype(np.uint32)
-        bd = to_snp_dict(bgp)
-        rd = to_snp_dict(rep)
-        bg2 = sims.calculate_2d_sfs(bd, 'p1', 'p2', npop, npop, start_position=0, end_position=500000,
-                                    variant_type=None)
-        bg1 = sims.calculate_1d_sfs(bd, 'p1', npop, start_position=0, end_position=500000, variant_type=None)
-        bg1b = sims.calculate_1d_sfs(bd, 'p2', npop, start_position=0, end_position=500000, variant_type=None)
-        out = run(sims.process_window, rd, bg2, bg1, bg1b, 500000, 'p1', 'p2', npop, npop,
-                  start_position=None, end_position=None, variant_type=None)
-        save_packed(os.path.join(HERE, f"{tag}_bgdata.npz"), bgp)
-        np.savez_compressed(os.path.join(HERE, f"{tag}_bg.npz"),
-                            bg2d=dense2d(bg2, 2 * npop, 2 * npop).astype(np.int64),
-                            bg1a=np.array([bg1[k] for k in range(2 * npop + 1)], np.int64),
-                            bg1b=np.array([bg1b[k] for k in range(2 * npop + 1)], np.int64))
-        case(tag, rep, dict(pop1="p1", pop2="p2", n1p=npop, n2p=npop),
-             [{"fn": "sims_process_window", "args": [500000], "out": out}],
-             "sims_scan.process_window with the sims bg (pos <= 500 kb, unfolded 1D)")
+        cfg = dict(pop1="A", pop2="B", n1p=3, n2p=3)
+        calls = class_calls(d, cfg, [("T2D_scan", ["raw", 100, None]), ("T2D_scan", ["norm", 100, "chrB-5"]),
+                                     ("T1D_scan", ["raw", 100, "A", 3, None]),
+                                     ("T1D_scan", ["norm", 100, "B", 3, None])])
+        case("t12_quirk", p, cfg, calls, "T1D_scan / T2D_scan: None statistics, rebinding to a (0,0) key")
 
     # ---------------------------------------------------------------- published chr1 rows (pins)
-    if not args.skip_chr1:
+    if want('pub') and not args.skip_chr1:
         import csv
         pub = {}
         for fname in ["ECBstats_20kb.csv", "ECBstats_500kb.csv", "ECBstats_500snps.csv"]:
@@ -289,7 +374,7 @@ def main():
         with open(os.path.join(HERE, "published_chr1.json"), "w") as fh:
             json.dump(pub, fh)
 
-    with open(os.path.join(HERE, "manifest.json"), "w") as fh:
+    with open(mpath, "w") as fh:
         json.dump(manifest, fh, indent=1)
     print("wrote", os.path.join(HERE, "manifest.json"))
 

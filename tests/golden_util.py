@@ -116,3 +116,34 @@ def run_capture(fn, *a, **kw):
         return True, out, buf.getvalue()
     except Exception as e:  # noqa: BLE001
         return False, e, buf.getvalue()
+
+
+def t12_inputs(p, cfgd, fn, args):
+    """Inputs of a golden T2D_scan / T1D_scan call (tests/golden/gen_golden.py section F): the data
+    (the packed set, or its dict with args[-1] moved to the end: T2D_scan reads the dict's last key)
+    and the background dict the reference was given (whole-data 2D / folded 1D SFS with the object's
+    filters, normalised for "norm"), rebuilt with the oracle.  Returns (data, bg, extra args)."""
+    from oracle import sfs_oracle as O
+    from sfs2d.pack import to_snp_dict
+    data = p
+    if args[-1] is not None:
+        data = to_snp_dict(p)
+        data[args[-1]] = data.pop(args[-1])
+    idx = np.arange(p.n)
+    if fn == "T2D_scan":
+        cfg = O.Cfg(cfgd["n1p"], cfgd["n2p"], cfgd.get("variant_type"), cfgd.get("fold", True),
+                    cfgd.get("start_position"), cfgd.get("end_position"))
+        g = O.sfs2d(p, idx, cfg).ravel()
+        vals = O.normalize(g) if args[0] == "norm" else g
+        n2 = 2 * cfgd["n2p"] + 1
+        bg = {(k // n2, k % n2): (float(v) if args[0] == "norm" else int(v)) for k, v in enumerate(vals)}
+        return data, bg, [args[1]]
+    pop, npop = args[2], args[3]
+    cfg = O.Cfg(npop, npop, cfgd.get("variant_type"), cfgd.get("fold", True), cfgd.get("start_position"),
+                cfgd.get("end_position"))
+    which = 1 if pop == p.pop1 else (2 if pop == p.pop2 else 0)
+    u = O.sfs1d(p, idx, which, cfg) if which else np.zeros(2 * npop + 1, np.int64)
+    f = O.fold1d(u)
+    vals = O.normalize(f) if args[0] == "norm" else f
+    bg = {k: (float(v) if args[0] == "norm" else int(v)) for k, v in enumerate(vals)}
+    return data, bg, [args[1], pop, npop]

@@ -30,6 +30,11 @@ def _gpu_call(obj, p, fn, args):
         bg1b = obj.normalize_1d_sfs(obj.fold_1d_sfs(obj.calculate_1d_sfs(
             d, obj.pop2, obj.pop2_size, obj.start_position, obj.end_position, obj.variant_type)))
         return obj.scan_precomputed_BG(p, args[0], bg2, bg1, bg1b)
+    if fn in ("T2D_scan", "T1D_scan"):
+        cfgd = dict(n1p=obj.pop1_size, n2p=obj.pop2_size, variant_type=obj.variant_type, fold=obj.fold,
+                    start_position=obj.start_position, end_position=obj.end_position)
+        data, bg, extra = gu.t12_inputs(p, cfgd, fn, args)
+        return getattr(obj, fn)(data, bg, *extra)
     return getattr(obj, fn)(p, *args)
 
 

@@ -25,6 +25,19 @@ def oracle_call(p, cfgd, fn, args):
     if fn == "scan_precomputed_BG":
         g2, g1a, g1b = O.genome_backgrounds_normalized(p, cfg)
         return O.scan_precomputed_BG(p, args[0], g2, g1a, g1b, cfg)
+    if fn in ("T2D_scan", "T1D_scan"):
+        _, bg, extra = gu.t12_inputs(p, cfgd, fn, args)
+        if fn == "T2D_scan":
+            last = None
+            if args[-1] is not None:   # the dict's last key, as an index into the scan order
+                c, q = args[-1].split("-")
+                ci = p.chrom_names.index(c)
+                lo, hi = int(p.chrom_off[ci]), int(p.chrom_off[ci + 1])
+                last = lo + int(np.searchsorted(p.pos[lo:hi], int(q)))
+            n2 = 2 * cfgd["n2p"] + 1
+            g = np.array([bg[(k // n2, k % n2)] for k in range(len(bg))]).reshape(-1, n2)
+            return O.T2D_scan(p, extra[0], g, cfg, last)
+        return O.T1D_scan(p, extra[0], np.array([bg[k] for k in range(len(bg))]), extra[1], extra[2], cfg)
     raise KeyError(fn)
 
 

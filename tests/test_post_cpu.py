@@ -40,6 +40,26 @@ def _post_call(p, cfgd, fn, args):
               O.normalize(O.fold1d(O.sfs1d(p, idx, 2, ocfg))))
         recs = F.snp_records(p, args[0], ocfg, lambda _c: bg)
         return post.bysnp_scan(recs, p, args[0], False, True)
+    if fn in ("T2D_scan", "T1D_scan"):
+        # the drop-in's host side (stream rebuild, packing) with oracle-made records
+        from sfs2d.pack import last_key_index, pack_snp_dict, shadow_chrom_starts
+        data, bg, extra = gu.t12_inputs(p, cfgd, fn, args)
+        ws = extra[0]
+        if fn == "T2D_scan":
+            q = shadow_chrom_starts(p, last_key_index(data, p), ws, cfgd.get("start_position"),
+                                    cfgd.get("end_position"))
+            qcfg = O.Cfg(cfgd["n1p"], cfgd["n2p"], cfgd.get("variant_type"), cfgd.get("fold", True))
+            n2 = 2 * cfgd["n2p"] + 1
+            g = np.array([bg[(k // n2, k % n2)] for k in range(len(bg))]).reshape(-1, n2)
+            ones = np.ones(cfgd["n1p"] + 1), np.ones(cfgd["n2p"] + 1)
+            recs = F.bp_records(q, ws, qcfg, lambda _c: (g,) + ones)
+            return post.single_stat_scan(recs, q, ws, post.num_slots(recs), 2, "T2D")
+        pop, npop = extra[1], extra[2]
+        q = (pack_snp_dict(data, pop, pop) if isinstance(data, dict) else p).single_pop(pop)
+        qcfg = O.Cfg(npop, npop, cfgd.get("variant_type"), False, cfgd.get("start_position"), cfgd.get("end_position"))
+        g1 = np.array([bg[k] for k in range(len(bg))])
+        recs = F.bp_records(q, ws, qcfg, lambda _c: (np.ones((2 * npop + 1, 2 * npop + 1)), g1, np.ones(npop + 1)))
+        return post.single_stat_scan(recs, q, ws, post.num_slots(recs), 1, "T1D")
     raise KeyError(fn)
 
 

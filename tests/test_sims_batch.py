@@ -108,3 +108,39 @@ def test_likelihood_scan_end_to_end(tmp_path):
             for f in ("T2D", "T1D_p1", "T1D_p2"):
                 assert gu.close(float(r[f]), o[f])
             assert gu.close(float(r["T2D_diff"]), o["T2D_diff"], scale=abs(o["T2D"]))
+
+
+def test_likelihood_scan_dict_variant(tmp_path):
+    """sims_scan.py:646-690 (the definition the reference module keeps): the dict keyed by
+    (generation, iteration, window) whose 'likelihood' is process_window's record, equal to the CSV
+    variant's rows and to the oracle."""
+    import sims_scan as S
+    from oracle import sfs_oracle as O
+    from sfs2d.synth import synth_genome
+    n = 5
+    s1, s2 = [f"a{i}" for i in range(n)], [f"b{i}" for i in range(n)]
+    popmap = tmp_path / "popmap.txt"
+    popmap.write_text("".join(f"{s}\tp1\n" for s in s1) + "".join(f"{s}\tp2\n" for s in s2))
+    (tmp_path / "concatenated_vcfs").mkdir()
+    bgd = synth_genome(1, 30000, n, n, seed=6, chrom_prefix="1")
+    _write_vcf(tmp_path / "concatenated_vcfs" / "gen.500.concatenated.vcf.gz", bgd, s1, s2)
+    reps = {}
+    for it in (1, 4):
+        d = tmp_path / f"iter{it}"
+        d.mkdir()
+        reps[it] = synth_genome(1, 20000, n, n, seed=40 + it, chrom_prefix="1")
+        _write_vcf(d / f"rep.500.{it}.vcf.gz", reps[it], s1, s2)
+    got = S.likelihood_scan(str(tmp_path), popinfo_filename=str(popmap))
+    o2, o1, o1b = O.sims_backgrounds(bgd, n, n)
+    want_keys = []
+    for it in sorted(reps):
+        ref = O.sims_process_window(reps[it], o2, o1, o1b, 500000, n, n)
+        for k, o in ref.items():
+            want_keys.append(("500", it, k))
+            v = got[("500", it, k)]
+            assert v["generation"] == "500" and v["iteration"] == it and v["window_coords"] == k
+            assert v["region"] == ("background" if int(k.split(" ")[1].split("-")[1]) <= 1000000 else "foreground")
+            assert not gu.compare_results({k: v["likelihood"]}, {k: o})
+    assert sorted(got) == sorted(want_keys)
+    with pytest.raises(FileNotFoundError):
+        S.likelihood_scan(str(tmp_path), popinfo_filename=str(tmp_path / "absent.txt"))
