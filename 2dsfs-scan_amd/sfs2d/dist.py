@@ -1,11 +1,14 @@
 """Multi-GPU scan: chromosome shards, one process per GPU, one gather of the window tables.
 
 Given per-chromosome backgrounds (combined_scan, scan_perChr_bySNPs; twoDSFS_class.py:809-825,
-1422-1541) every chromosome is independent, so a rank scans a contiguous range of whole
-chromosomes with no collective on the data path.  The only exchange is one all-gather
-of the fixed-stride 64-B window records (RCCL over xGMI with the "nccl" backend on MI355X, gloo
-on CPU), after which the tables are concatenated in chromosome order and the sequential rules of
-the drivers (sfs2d.post: stale carry Q6, final block Q9) run once on the whole table.
+1422-1541) or one supplied background (scan_chooseChr, scan_precomputed_BG, the bySNPs driver
+with a chosen chromosome, T1D_scan / T2D_scan, the sims replicates) every chromosome is
+independent, so a rank scans a contiguous range of whole chromosomes with no collective on the
+data path.  The only exchange is one all-gather of the fixed-stride 64-B window records
+(RCCL over xGMI with the "nccl" backend on MI355X, gloo on CPU), after which the tables are
+concatenated in chromosome order -- the table one plan over all chromosomes would emit -- and the
+sequential rules of the drivers (sfs2d.post: stale carry Q6, final block Q9) run on it, on every
+rank (``scan_records``; the drop-in class with ``distributed=True``).
 
 The final-block helper record (Q9) needs the window before the last one of the whole scan, which
 may sit in the previous chromosome: the last rank therefore also scans the chromosome before its
@@ -108,6 +111,60 @@ def gather_tables(local: np.ndarray, world: int, device=None) -> List[np.ndarray
         dist.all_gather_into_tensor(allb, buf)
     allb = allb.cpu().numpy().reshape(world, m, 64)
     return [allb[r, : ns[r]].copy().view(L.WINDOW_DTYPE).reshape(-1) for r in range(world)]
+
+
+def _comm_device(device):
+    import torch.distributed as dist
+    return f"cuda:{device}" if dist.get_backend() == "nccl" else None
+
+
+def scan_records(p, cfg, bg, scan_local, device: int = 0, comm_device="auto") -> np.ndarray:
+    """One scan of ``p`` (ScanConfig ``cfg``, supplied background ``bg`` or None) sharded over the
+    default process group: this rank scans its chromosome range with ``scan_local(sub, cfg, bg)``
+    (the HIP scan of one GPU), the tables are all-gathered and merged.  Every rank returns the global
+    record table (what one plan over all of ``p`` emits: slots in chromosome order, the Q9 helper
+    record last when ``cfg.prev_extra``)."""
+    import dataclasses
+
+    import torch.distributed as dist
+    rank, world = dist.get_rank(), dist.get_world_size()
+    shards = shard_chromosomes(p.chrom_off, world)
+    pe = bool(cfg.prev_extra)
+    lo, hi = scan_range(shards, rank, pe)
+    last = max((r for r, (a, b) in enumerate(shards) if b > a), default=-1)
+    local = np.zeros(0, dtype=L.WINDOW_DTYPE)
+    err = None
+    if shards[rank][1] > shards[rank][0]:
+        sub = p.subset_chroms(range(lo, hi))
+        try:
+            local = scan_local(sub, dataclasses.replace(cfg, prev_extra=pe and rank == last), bg)
+        except Exception as e:  # noqa: BLE001  (raised on every rank below, not left to hang the gather)
+            err = e
+    _raise_collective(err, world)
+    if comm_device == "auto":
+        comm_device = _comm_device(device)
+    tables = gather_tables(local, world, comm_device)
+    return merge_tables(tables, shards, pe, p.chrom_off)
+
+
+def _raise_collective(err, world):
+    """A rank's scan error (e.g. KeyError for counts above the sample size, found by the rank that
+    holds the SNP) raised on every rank, the lowest failing rank's: no rank is left waiting in the
+    gather."""
+    import builtins
+
+    import torch.distributed as dist
+    got = [None] * world
+    dist.all_gather_object(got, None if err is None else (type(err).__name__, str(err.args[0]) if err.args else ""))
+    first = next((g for g in got if g is not None), None)
+    if first is None:
+        return
+    if err is not None and (type(err).__name__, str(err.args[0]) if err.args else "") == first:
+        raise err
+    t = getattr(builtins, first[0], None)
+    if isinstance(t, type) and issubclass(t, Exception):
+        raise t(first[1])
+    raise L.Sfs2dError(L.E_HIP, f"{first[0]} on another rank: {first[1]}")
 
 
 def combined_scan_sharded(packed, window_size: int, n1p: int, n2p: int, rank: int, world: int,

@@ -171,28 +171,38 @@ def _concat(packs):
                       cat(ann, np.uint16), ann_names), base
 
 
+def _scan_local(p, cfg, bg):
+    eng = Engine.get(DEVICE)
+    dev = eng.upload(p)
+    try:
+        return eng.scan(dev, cfg, bg)
+    finally:
+        dev.close()
+
+
 def process_windows_batch(replicates, bg_2d_sfs, bg_p1_sfs, bg_p2_sfs, window_size, pop1, pop2, pop1_size,
-                          pop2_size, start_position=None, end_position=None, variant_type=None):
+                          pop2_size, start_position=None, end_position=None, variant_type=None, distributed=False):
     """``process_window`` (sims_scan.py:451-590) over many replicate data sets in ONE scan launch:
     all replicates resident in HBM as one data set, one supplied background, one plan.  Returns the
     list of per-replicate result dicts, each equal to ``process_window(replicate, ...)``; the first
     replicate (in order) whose window has no SNP / an empty background raises ZeroDivisionError, as
-    the reference's loop over replicates would (sims_scan.py:619-622)."""
+    the reference's loop over replicates would (sims_scan.py:619-622).  ``distributed``: the
+    replicates' chromosomes are sharded over the torch.distributed group (one process per GPU, all
+    ranks calling with the same arguments; every rank returns the whole list)."""
     packs = [_pack(d, pop1, pop2) for d in replicates]
     if not packs:
         return []
     data, base = _concat(packs)
-    eng = Engine.get(DEVICE)
     cfg = ScanConfig(n1p=pop1_size, n2p=pop2_size, fold=True, window_mode=L.WINDOW_BP, window=window_size,
                      bg_mode=L.BG_SUPPLIED, ann_want=_ann(data, variant_type),
                      start_position=None if start_position is None else int(start_position),
                      end_position=None if end_position is None else int(end_position))
     bg = _bg_arrays(bg_2d_sfs, bg_p1_sfs, bg_p2_sfs, pop1_size, pop2_size)
-    dev = eng.upload(data)
-    try:
-        recs = eng.scan(dev, cfg, bg)
-    finally:
-        dev.close()
+    if distributed:
+        from sfs2d import dist as D
+        recs = D.scan_records(data, cfg, bg, _scan_local, DEVICE)
+    else:
+        recs = _scan_local(data, cfg, bg)
     chrom = recs["chrom"].astype(np.int64)
     out = []
     for i, q in enumerate(packs):

@@ -75,7 +75,12 @@ def _fold_counts(u: np.ndarray) -> np.ndarray:
 
 class LikelihoodInference_jointSFS:
     def __init__(self, vcf_filename, popinfo_filename, start_position=None, end_position=None,
-                 pop1='uv', pop2='bv', pop1_size=18, pop2_size=14, variant_type=None, fold=True, device=0):
+                 pop1='uv', pop2='bv', pop1_size=18, pop2_size=14, variant_type=None, fold=True, device=0,
+                 distributed=False):
+        """The reference's constructor (twoDSFS_class.py:21-33), plus ``device`` (the GPU of this
+        process) and ``distributed``: with a torch.distributed process group (one process per GPU),
+        every window scan is sharded by chromosome over the group and every rank returns the whole
+        result (sfs2d.dist.scan_records); all ranks must make the same calls."""
         self.vcf_filename = vcf_filename
         self.popinfo_filename = popinfo_filename
         self.pop1 = pop1
@@ -87,6 +92,7 @@ class LikelihoodInference_jointSFS:
         self.variant_type = variant_type
         self.fold = fold
         self.device = device
+        self.distributed = distributed
 
     # ------------------------------------------------------------------ ingest
     def make_data_dict_vcf(self, vcf_filename=None, popinfo_filename=None):
@@ -113,6 +119,12 @@ class LikelihoodInference_jointSFS:
                           start_position=start, end_position=end, **kw)
 
     def _scan(self, p: PackedSNPs, cfg: ScanConfig, bg=None):
+        if self.distributed:
+            from sfs2d import dist as D
+            return D.scan_records(p, cfg, bg, self._scan_local, self.device)
+        return self._scan_local(p, cfg, bg)
+
+    def _scan_local(self, p: PackedSNPs, cfg: ScanConfig, bg=None):
         eng = self._engine()
         dev = eng.upload(p)
         try:
@@ -122,11 +134,12 @@ class LikelihoodInference_jointSFS:
         return recs
 
     def _bg_arrays(self, p: PackedSNPs, chrom: int):
-        """Unnormalised background of one chromosome (2D grid + folded 1D), computed on the GPU."""
+        """Unnormalised background of one chromosome (2D grid + folded 1D), computed on the GPU (every
+        rank computes it itself when distributed: integer counts, no collective)."""
         eng = self._engine()
-        dev = eng.upload(p)
+        dev = eng.upload(p.subset_chroms([chrom]))
         try:
-            h2, u1, u2 = eng.bg_hist(dev, self._cfg(p), chrom)
+            h2, u1, u2 = eng.bg_hist(dev, self._cfg(p), 0)
         finally:
             dev.close()
         return h2, _fold_counts(u1), _fold_counts(u2)

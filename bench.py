@@ -5,10 +5,15 @@ Workload (BASELINE configs[1]): one synthetic chromosome of 1e6 SNPs per GPU (SU
 generator, seed 12345 + rank), n1 = n2 = 50 haploid (pop_size 25/25), 20 kb fixed-bp windows,
 each chromosome its own background (combined_scan semantics).  A step = one full scan pass over
 the HBM-resident packed SNPs: background histograms + window segmentation (K1), background
-tables (K2), window scan (K3) -> device-resident 64-B window records; with N > 1 ranks, plus one
-RCCL all-gather of every rank's window table (weak scaling: per-GPU work fixed).  Consecutive
-passes are independent: they go round-robin over --streams plans (default 3), each on its own HIP
-stream, so one pass's latency-bound kernels overlap the next one's (sfs2d_plan_run_streams).
+tables (K2), window scan (K3) -> device-resident 64-B window records.  Consecutive passes are
+independent: they go round-robin over --streams plans (default 3), each on its own HIP stream, so
+one pass's latency-bound kernels overlap the next one's (sfs2d_plan_run_streams).  The timed loop
+is the same at every N (weak scaling: each rank its own chromosome, no data-path collective); with
+N > 1 ranks the timed region ends with one RCCL all-gather of every rank's final window table.
+
+`--gpus N` with no launcher: this script starts the N rank processes itself (before touching the
+GPU) and exits with their status; under torchrun, WORLD_SIZE must equal N, and a box with fewer
+than N GPUs fails instead of reporting fewer.
 
 Prints ONE JSON line on rank 0.  `roofline` is for the dominant kernel (K3) from HIP events in its
 dispatch packets, on the stream it runs on (with overlapped passes: in a single-stream pass right
@@ -141,6 +146,37 @@ def hbm_stream_roofline(eng, steps=5):
     return out
 
 
+def launch_ranks(n):
+    """``--gpus N`` with no launcher around this process: start N rank processes of this script
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rendezvous on 127.0.0.1) before this process
+    imports torch or touches the GPU, wait for them, and return the first failing status (the other
+    ranks are then killed by PID)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for q in list(live):
+            c = q.poll()
+            if c is None:
+                continue
+            live.remove(q)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 1
+                for o in live:
+                    o.kill()
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -148,283 +184,160 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-hbm-stream", action="store_true")
-    ap.add_argument("--dist-loop", action="store_true",
-                    help="diagnostic: the N>1 step loop (scan + RCCL all-gather per step) even on one rank")
-    ap.add_argument("--py-loop", action="store_true", help="diagnostic: the Python N>1 step loop instead of the native one")
     ap.add_argument("--streams", type=int, default=3,
-                    help="N=1: consecutive steps round-robin over this many plans, each on its own HIP stream "
+                    help="consecutive steps round-robin over this many plans, each on its own HIP stream "
                          "(independent passes overlap; sfs2d_plan_run_streams)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
     # hardware queues per process: HIP maps streams onto GPU_MAX_HW_QUEUES queues (4 on the box); S
     # pass streams + the library's and torch's own need more than 4 or two passes share a queue and
     # serialise (3 streams: 1.35e8 windows/s with 4 queues, 1.92-1.94e8 with 6-8; profiles/r02h_*).
-    # Set before the HIP runtime starts (torch imported below).
+    # Set before the HIP runtime starts (torch imported below; rank processes inherit it).
     need = max(1, args.streams) + 4
     if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < need:
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(8, need)))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} launched with WORLD_SIZE={world}")
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    if ndev < world or local >= ndev:
+        raise RuntimeError(f"bench.py --gpus {world}: rank {rank} needs device {local}, {ndev} visible")
     torch.cuda.set_device(local)
-    dl = world > 1 or args.dist_loop   # the distributed step loop
-    if dl:
+    if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
         dist.init_process_group("nccl", rank=rank, world_size=world)
+        world = dist.get_world_size()   # n_gpus from the communicator
 
     from sfs2d import _lib as L
     from sfs2d.engine import Engine, Plan, ScanConfig
     from sfs2d.synth import synth_genome
 
+    # weak scaling: every rank scans its own chromosome (seed 12345 + rank) -- whole chromosomes are
+    # the shard unit of per-chromosome-background scans
     p = synth_genome(1, N_SNP, POP, POP, seed=12345 + rank)
     eng = Engine.get(local)
-    scan_s = torch.cuda.Stream(device=local)    # the HIP library's stream
-    comm_s = torch.cuda.Stream(device=local)    # RCCL gathers of the window tables
+    scan_s = torch.cuda.Stream(device=local)    # the HIP library's stream (and the final gather's)
     torch.cuda.set_stream(scan_s)
     eng.set_stream(scan_s.cuda_stream)
     dev = eng.upload(p)
-    pl = eng.plan(dev, ScanConfig(n1p=POP, n2p=POP, window=WS, fst=True))
+    cfg = ScanConfig(n1p=POP, n2p=POP, window=WS, fst=True)
+    ns = max(1, args.streams)
+    plans = [eng.plan(dev, cfg) for _ in range(ns)]
+    pl = plans[0]
     nrec = pl.nrec
     cdev = f"cuda:{local}"
-    if dl:
-        # shards differ in window count: tables are padded to the largest (unused rows flagged empty)
+    rows = nrec
+    if world > 1:   # shards differ in window count: tables are padded to the largest (rows flagged empty)
         c = torch.tensor([nrec], dtype=torch.int64, device=cdev)
         dist.all_reduce(c, op=dist.ReduceOp.MAX)
         rows = int(c.item())
-    else:
-        rows = nrec
-    ns = max(1, args.streams)   # (N > 1: falls back to 1 without the native step loop)
-    plans = [pl] + [eng.plan(dev, ScanConfig(n1p=POP, n2p=POP, window=WS, fst=True)) for _ in range(ns - 1)]
     sstreams = [scan_s.cuda_stream] + [torch.cuda.Stream(device=local).cuda_stream for _ in range(ns - 1)]
-    outs = [torch.zeros((rows, 64), dtype=torch.uint8, device=cdev) for _ in range(max(2, ns))]
+    ev_done = [torch.cuda.Event() for _ in range(ns)]
+    outs = [torch.zeros((rows, 64), dtype=torch.uint8, device=cdev) for _ in range(ns)]
     for o in outs:
         o[nrec:, 39] = 0x80   # padding rows: flags = SFS2D_W_EMPTY
-    gathered = [torch.empty((world * rows * ns, 64), dtype=torch.uint8, device=cdev) for _ in range(2)] if dl else None
-    # N > 1 with several streams: the group's tables are contiguous (one gather per group of ns steps)
-    outbuf = torch.zeros((2 * ns * rows, 64), dtype=torch.uint8, device=cdev) if dl and ns > 1 else None
-    if outbuf is not None:
-        outbuf.view(2 * ns, rows, 64)[:, nrec:, 39] = 0x80
-    # the step loop runs in the native library (sfs2d_dist_scan_gather: its own RCCL communicator, the
-    # scans and all-gathers enqueued from C); the Python loop below is the fallback
-    nat = None
-    gather_root = False
-    if dl:
-        hdr = torch.zeros(129, dtype=torch.uint8)
-        if rank == 0:
-            try:
-                hdr[1:] = torch.tensor(list(eng.dist_unique_id()), dtype=torch.uint8)
-                hdr[0] = 1
-            except Exception as e:  # noqa: BLE001
-                print(f"[bench] RCCL id unavailable ({e}): Python step loop", file=sys.stderr)
-        hdr = hdr.to(cdev)
-        dist.broadcast(hdr, 0)
-        hdr = hdr.cpu()
-        if int(hdr[0]) == 1 and not args.py_loop:
-            nat = eng.dist(bytes(hdr[1:].tolist()), rank, world)
-            nats = [nat]
-            # one ncclGather of the window tables to rank 0 per step (their one consumer),
-            # ncclAllGather where the loaded RCCL lacks it or SFS2D_GATHER=all; the same on every rank
-            to_root = os.environ.get("SFS2D_GATHER", "root") != "all"
-            ok = torch.tensor([1 if to_root else 0], dtype=torch.int32, device=f"cuda:{local}")
-            if to_root:
-                try:
-                    nat.set_gather(True)
-                except Exception:  # noqa: BLE001
-                    ok.zero_()
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-            gather_root = bool(int(ok.item()))
-            for q in nats:
-                q.set_gather(gather_root)
-    if dl and nat is None and ns > 1:
-        ns, outbuf = 1, None
-        for q in plans[1:]:
-            q.close()
-        plans, sstreams = plans[:1], sstreams[:1]
-    ev_scan = [torch.cuda.Event() for _ in range(2)]
-    ev_comm = [torch.cuda.Event() for _ in range(2)]
-    for e in ev_comm:
-        e.record(comm_s)
-    torch.cuda.synchronize()
-
-    def step(i):
-        # step i: scan into table i&1 on the scan stream; gather it on the comm stream while step
-        # i+1 scans into the other table (the scan of step i+2 waits for gather i to finish)
-        b = i & 1
-        scan_s.wait_event(ev_comm[b])
-        pl.run(outs[b].data_ptr())
-        ev_scan[b].record(scan_s)
-        comm_s.wait_event(ev_scan[b])
-        with torch.cuda.stream(comm_s):
-            dist.all_gather_into_tensor(gathered[b], outs[b])
-        ev_comm[b].record(comm_s)
-
-    out = outs[0]
-    pl.run(out.data_ptr())
-    pl.check()
     optrs = [o.data_ptr() for o in outs]
-    gptrs = [g.data_ptr() for g in gathered] if dl else None
-    gather_on = None
-    dist_times = None
-    STREAMS_MODE = "streams"
-    timed_ns = ns
-    if nat is not None:
-        # the warmup times the step loop's placements -- one plan with its gathers serial on the scan
-        # stream or overlapped on the comm stream (events), and with --streams > 1 the grouped loop
-        # (ns plans on ns streams, one gather per group) -- and every rank keeps the fastest by the
-        # max over ranks
-        STREAMS = STREAMS_MODE
+    gathered = torch.empty((world * rows, 64), dtype=torch.uint8, device=cdev) if world > 1 else None
+    last = (args.steps - 1) % ns   # the table the last timed step writes
 
-        def run_dist(mode, first, n):
-            # mode: STREAMS (steps in groups of ns over ns plans / streams, one gather per group), or
-            # the one-plan loop with its gathers serial (None) or on the comm stream
-            if mode == STREAMS:
-                nat.scan_gather_streams(plans, sstreams, outbuf.data_ptr(), gptrs, rows, n)
-            else:
-                nat.scan_gather(pl, optrs, gptrs, rows, first, n, mode)
+    def gather_final(k):
+        # the single collective: every rank's final window table to every rank (RCCL over xGMI),
+        # ordered after the scans of all the plans' streams
+        for j, e in enumerate(ev_done):
+            e.record(torch.cuda.ExternalStream(sstreams[j]))
+            scan_s.wait_event(e)
+        dist.all_gather_into_tensor(gathered, outs[k])
 
-        def timed(mode, first, n):
-            torch.cuda.synchronize()
-            dist.barrier()
-            t = time.perf_counter()
-            run_dist(mode, first, n)
-            torch.cuda.synchronize()
-            tt = torch.tensor([(time.perf_counter() - t) / n], dtype=torch.float64, device=cdev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            return float(tt.item())
-        # (a few serial steps first absorb the first-call costs; overlapped must win by 10%: on one
-        # GPU it lost, 44-59 vs 32 us per step, and short samples are noisy)
-        pre = 4
-        run_dist(None, 0, pre)
-        if ns > 1:
-            run_dist(STREAMS, 0, pre * ns)
-        wh = max(20, args.warmup)
-        step_no = pre
-        if gather_root:
-            # gather to rank 0 vs all-gather, both serial: the faster one stays (on one rank the
-            # ncclGather's grouped send / receive cost 37 vs 30 us per step; at N > 1 it moves 1/N
-            # of the all-gather's bytes)
-            t_root = timed(None, step_no, wh)
-            nat.set_gather(False)
-            t_all = timed(None, step_no + wh, wh)
-            step_no += 2 * wh
-            gather_root = t_root < t_all
-            nat.set_gather(gather_root)
-        # per-step times (max over ranks) of the placements; the streams loop must win by 5%, the
-        # overlapped one by 10%
-        t_se = timed(None, step_no, wh)
-        t_ov = timed(comm_s.cuda_stream, step_no + wh, wh)
-        step_no += 2 * wh
-        cand = [(t_se, None), (t_ov / 0.9, comm_s.cuda_stream)]
-        if ns > 1:
-            cand.append((timed(STREAMS, 0, wh * ns) / 0.95, STREAMS))
-        dist_times = {"serial": t_se * 1e6, "overlapped": t_ov * 1e6,
-                      "streams": cand[2][0] * 0.95e6 if ns > 1 else None}
-        gather_on = min(cand, key=lambda c: c[0])[1]
-        first_timed = step_no
-    elif dl:
-        for i in range(args.warmup):
-            step(i)
-    elif ns > 1:
-        Plan.run_streams(plans, sstreams, args.warmup * ns, optrs[:ns])
-    else:
-        pl.run_many(args.warmup, out.data_ptr())
-    # HIP events around the scan kernel (the roofline's) and k_bg_slice of every 8th timed run, on the
-    # stream the kernels run on, carried in their dispatch packets.  An event pair costs queue time:
-    # events around all three kernels of every 8th run cost ~2 us per step, these two ~1 us
-    # (tools/timing_overhead.py); the scan kernel's start event needs the end event of the kernel
-    # before it (alone it also counts that kernel's drain: 10.8-11.4 vs 9.6 us).  k_prep is timed in
-    # an untimed pass after the timed loop.
-    # (short runs -- the driver's 20 steps -- sample every 2nd run of plan 0, so that the roofline's
-    # average is over >= 5 launches; long runs every 8th)
+    pl.run(optrs[0])
+    pl.check()
+    # warmup: the same loop, and (N > 1) the collective once (RCCL communicators are made lazily)
+    Plan.run_streams(plans, sstreams, args.warmup * ns, optrs)
+    if world > 1:
+        gather_final(last)
+    torch.cuda.synchronize()
+    # HIP events around the scan kernel (the roofline's) and k_bg_slice of sampled timed runs of plan 0,
+    # carried in their dispatch packets on the stream the kernels run on (events around all three
+    # kernels of every 8th run cost ~2 us per step, around these two ~1 us: tools/timing_overhead.py);
+    # k_prep is timed in an untimed pass after the timed loop.  Short runs (the driver's 20 steps)
+    # sample every 2nd run of plan 0 so that the average is over >= 5 launches.
     every = 8 if args.steps >= 160 else 2
     pl.set_timing(args.steps, every=every, kernels=6)
-    if dl:
+    if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if nat is not None:
-        run_dist(gather_on, first_timed, args.steps)
-        if gather_on != STREAMS_MODE:
-            timed_ns = 1   # (the report: one plan ran the timed steps)
-    elif ns > 1:
-        Plan.run_streams(plans, sstreams, args.steps, optrs[:ns])   # run i: plan i % ns on stream i % ns
-    elif not dl:
-        pl.run_many(args.steps, out.data_ptr())   # enqueued from C: no host work between steps
-    else:
-        for i in range(args.steps):
-            step(i)
+    # the timed loop, the same at every N: step i = one scan pass of plan i % ns on stream i % ns;
+    # with N > 1 ranks, then one gather of the final window tables
+    Plan.run_streams(plans, sstreams, args.steps, optrs)
+    if world > 1:
+        gather_final(last)
     t_enq = time.perf_counter() - t0   # host time to enqueue the timed steps (diagnostic)
     torch.cuda.synchronize()
-    if dl:
+    if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    if dl:
+    if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     nr, (_, k2, k3) = pl.timing_read()
-    pl.set_timing(16, every=1)   # k_prep (and the other two again), outside the timed region
-    pl.run_many(16, out.data_ptr())
+    pl.set_timing(16, every=1)   # k_prep (and the other two again), one stream, outside the timed region
+    pl.run_many(16, optrs[0])
     _, (k1, _, k3_untimed) = pl.timing_read()
     pl.set_timing(0)
-    pl.check()
-    if outbuf is not None:   # the grouped dist loop wrote its tables into outbuf
-        tabs = outbuf.view(2 * ns, rows, 64)
-        for k in range(1, 2 * ns):
-            if not torch.equal(tabs[k][:nrec], tabs[0][:nrec]):
-                raise RuntimeError(f"table {k} of the grouped step loop disagrees with table 0")
-        if gather_on == STREAMS_MODE and (rank == 0 or not gather_root) and not torch.equal(gathered[0].view(world, ns * rows, 64)[rank][:nrec],
-                                                              tabs[0][:nrec]):
-            raise RuntimeError("gathered table disagrees with the local one")
-    for k in range(1, ns):   # every plan's last pass wrote the same records (independent per-run state)
-        plans[k].check()
-        if outbuf is None and not torch.equal(outs[k][:nrec], out[:nrec]):
+    for k, q in enumerate(plans):   # every plan's last pass wrote the same records (independent state)
+        q.check()
+        if not torch.equal(outs[k][:nrec], outs[0][:nrec]):
             raise RuntimeError(f"plan {k} on stream {k} disagrees with plan 0")
-    recs = np.frombuffer(out[:nrec].cpu().numpy().tobytes(), dtype=L.WINDOW_DTYPE)
+    recs = np.frombuffer(outs[0][:nrec].cpu().numpy().tobytes(), dtype=L.WINDOW_DTYPE)
     nwin_rank = int(((recs["flags"] & L.W_EMPTY) == 0).sum())
     total_windows = nwin_rank
     if world > 1:
-        tw = torch.tensor([nwin_rank], dtype=torch.int64, device=cdev)
-        dist.all_reduce(tw)
-        total_windows = int(tw.item())
+        g = gathered.view(world, rows, 64)
+        if not torch.equal(g[rank][:nrec], outs[0][:nrec]):
+            raise RuntimeError("the gathered table disagrees with this rank's own")
+        allr = np.frombuffer(g.cpu().numpy().tobytes(), dtype=L.WINDOW_DTYPE)
+        total_windows = int(((allr["flags"] & L.W_EMPTY) == 0).sum())
     value = total_windows * args.steps / dt
 
     if rank == 0:
         b3 = algorithmic_bytes(p.n, nrec, nwin_rank, "k3")
-        # the roofline's duration: with overlapped passes (timed_ns > 1) a kernel's event interval in
-        # the timed region also holds the time its workgroups wait for CUs that the other passes'
-        # kernels occupy (k_scan_w 14-16 us there vs 9.5-9.8 us in rocprofv3's kernel trace of the
-        # same command), so the kernel's own duration comes from the single-stream pass of 16 runs
-        # after the timed loop (the same kernel, data and dispatch-packet events)
-        k3_roof = k3_untimed if timed_ns > 1 else k3
+        # the roofline's duration: with overlapped passes (ns > 1) a kernel's event interval in the
+        # timed region also holds the time its workgroups wait for CUs that the other passes' kernels
+        # occupy (k_scan_w 14-16 us there vs 9.5-9.8 us in rocprofv3's kernel trace of the same
+        # command), so the kernel's own duration comes from the single-stream pass of 16 runs after
+        # the timed loop (the same kernel, data and dispatch-packet events)
+        k3_roof = k3_untimed if ns > 1 else k3
         achieved = b3 / (k3_roof * 1e-3) / 1e9
-        bp = algorithmic_bytes(p.n, nrec, nwin_rank, "pipeline")
+        bp = algorithmic_bytes(p.n, nrec, nwin_rank, "pipeline") * world
         step_s = dt / args.steps
         traffic, tsrc = pmc_traffic("k_scan_w", pl.grids()[1])
         line = {
             "metric": "genomic windows/s (T2D+T1D+Fst) at 20 kb, n1=n2=50; HBM GB/s fraction",
             "value": value, "unit": "windows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": dt / args.steps * 1e3, "host_enqueue_ms_per_step": t_enq / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": dt / args.steps * 1e3, "host_enqueue_ms_per_step": t_enq / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic (SURVEY 8d generator, seed 12345+rank)",
             "config": {"workload": "configs[1]: synthetic 1 chromosome x 1e6 SNPs per GPU, 20 kb windows, "
                                    "n1=n2=50 haploid (pop_size 25/25), per-chromosome background",
-                       "snps_per_gpu": p.n, "windows_per_gpu": nwin_rank, "window_bp": WS,
+                       "snps_per_gpu": p.n, "windows_per_gpu": nwin_rank, "windows_all_gpus": total_windows,
+                       "window_bp": WS,
                        "stats": "T2D, T1D_p1, T1D_p2 (reference semantics) + Hudson Fst (DESIGN.md; not in the "
                                 "reference, parity vs its own oracle restatement)",
-                       "parallelism": f"windows sharded by chromosome over {world} GPU(s); RCCL "
-                                      + ("gather to rank 0" if gather_root else "all-gather")
-                                      + (f" per step ({'native' if nat is not None else 'Python'} step loop"
-                                         + ("" if nat is None else ", gathers " + ("one per group of steps over the plans' streams" if gather_on == STREAMS_MODE
-                                                                   else "overlapped on a comm stream" if gather_on
-                                                                   else "serial on the scan stream"))
-                                         + ")" if dl else "")
-                                      + (f"; {timed_ns} plans on {timed_ns} HIP streams, steps round-robin (passes overlap)"
-                                         if timed_ns > 1 else "")},
-            **({"dist_step_us_by_placement": dist_times} if dist_times else {}),
+                       "parallelism": f"one chromosome per GPU ({world} GPU(s)), no data-path collective; "
+                                      f"{ns} plans on {ns} HIP streams, steps round-robin (passes overlap)"
+                                      + ("; one RCCL all-gather of the final window tables in the timed region"
+                                         if world > 1 else "")},
             "kernels_ms": {"k_prep": k1, "k_bg_slice": k2, "k_scan_w": k3, "k_scan_w_untimed_pass": k3_untimed,
                            "timed_runs_sampled": nr, "exact_path_windows": pl.stats(),
                            "note": f"k_bg_slice / k_scan_w: events in every {every}th timed run of plan 0; k_prep: 16 "
@@ -436,27 +349,25 @@ def main():
                                  + (f"duration in the single-stream pass of 16 runs after the timed loop (kernel "
                                     "start/end events in the dispatch packets; in the timed region, every "
                                     f"{every}th run of plan 0, the interval also holds the wait for CUs held by "
-                                    "the other streams' passes: ms_timed_region); " if timed_ns > 1 else
+                                    "the other streams' passes: ms_timed_region); " if ns > 1 else
                                     f"duration (kernel start/end events in the dispatch packets of every {every}th "
                                     "timed run); ")
                                  + "the 8 MB config-2 stream is MALL-resident (see roofline_hbm for the HBM-sized "
                                  "stream); traffic: " + (tsrc or "no PMC pass committed")},
-            "roofline_pipeline": {"bound": "hbm", "achieved": bp / step_s / 1e9, "peak": HBM_PEAK_GBS,
-                                  "unit": "GB/s", "frac": bp / step_s / 1e9 / HBM_PEAK_GBS,
-                                  "note": "whole step (SURVEY 8(d): 12 B/SNP + 64 B/window) over ms_per_step"},
+            "roofline_pipeline": {"bound": "hbm", "achieved": bp / step_s / 1e9, "peak": HBM_PEAK_GBS * world,
+                                  "unit": "GB/s", "frac": bp / step_s / 1e9 / (HBM_PEAK_GBS * world),
+                                  "note": "whole step over all GPUs (SURVEY 8(d): 12 B/SNP + 64 B/window) over "
+                                          "ms_per_step"},
         }
         if not args.no_hbm_stream and world == 1:
             line["roofline_hbm"] = hbm_stream_roofline(eng)
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(p)
         print(json.dumps(line), flush=True)
-    if nat is not None:
-        for q in nats:
-            q.close()
     for q in plans[::-1]:
         q.close()
     dev.close()
-    if dl:
+    if world > 1:
         dist.destroy_process_group()
 
 

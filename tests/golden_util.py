@@ -147,3 +147,20 @@ def t12_inputs(p, cfgd, fn, args):
     vals = O.normalize(f) if args[0] == "norm" else f
     bg = {k: (float(v) if args[0] == "norm" else int(v)) for k, v in enumerate(vals)}
     return data, bg, [args[1], pop, npop]
+
+
+def enc_value(v):
+    """JSON-safe encoding of a result value (floats by repr, as tests/golden/gen_golden.py)."""
+    if v is None or isinstance(v, (bool, str)):
+        return v
+    if isinstance(v, (int, np.integer)):
+        return int(v)
+    if isinstance(v, (float, np.floating)):
+        return repr(float(v))
+    if isinstance(v, dict):
+        return {k: enc_value(x) for k, x in v.items()}
+    raise TypeError(type(v))
+
+
+def enc_results(res):
+    return [[k, {f: enc_value(x) for f, x in d.items()}] for k, d in res.items()]

@@ -110,3 +110,66 @@ def test_gloo_allgather_two_ranks():
     bgs = O.chrom_backgrounds(p, ocfg)
     full = FR.bp_records(p, 20000, ocfg, lambda c: bgs[c], prev_extra=True)
     assert _same(merged, full)
+
+
+def run_dist_workers(mode, world, out, extra=(), timeout=600, env_extra=None):
+    """Start `world` rank processes of tests/dist_worker.py (gloo on 127.0.0.1); returns rank 0's
+    JSON (every golden driver call, scanned sharded)."""
+    import json
+    import subprocess
+    import sys
+    port = _free_port()
+    here = os.path.dirname(os.path.abspath(__file__))
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   OMP_NUM_THREADS="1", **(env_extra or {}))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(here, "dist_worker.py"), mode, out, *extra],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    logs = []
+    try:
+        for q in procs:
+            o, _ = q.communicate(timeout=timeout)
+            logs.append(o.decode(errors="replace"))
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                q.kill()
+    assert all(q.returncode == 0 for q in procs), "\n".join(x[-3000:] for x in logs)
+    with open(out) as fh:
+        return json.load(fh)
+
+
+def check_dist_results(got, golden):
+    """Every call's sharded result equals the reference's (golden) result or error."""
+    import golden_util as gu
+    n = 0
+    for name in golden.cases():
+        for i, c in enumerate(golden.calls(name)):
+            key = f"{name}-{i}"
+            if key not in got:
+                continue
+            n += 1
+            g, ref = got[key], c["out"]
+            if c["fn"] == "sims_process_window":
+                assert g["ok"], (key, g)
+                errs = gu.compare_results(gu.decode_results(g["results"]), gu.decode_results(ref["results"]))
+                assert not errs, (key, errs[:5])
+                continue
+            if not ref["ok"]:
+                assert not g["ok"] and g["error"] == ref["error"], (key, g)
+                continue
+            assert g["ok"], (key, g)
+            errs = gu.compare_results(gu.decode_results(g["results"]), gu.decode_results(ref["results"]))
+            assert not errs, (key, errs[:5])
+    return n
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_drivers_vs_reference(golden, tmp_path, world):
+    """Every golden driver call (combined_scan, scan_chooseChr, scan_precomputed_BG, both bySNPs
+    drivers, T1D_scan / T2D_scan, the sims batch) through the drop-in modules with distributed=True
+    over `world` gloo ranks: shard, per-rank scan (the oracle's records in place of the GPU's),
+    collective error handling, gather, merge, post-pass -- equal to the reference's outputs."""
+    got = run_dist_workers("fake", world, str(tmp_path / "out.json"))
+    assert check_dist_results(got, golden) >= 40
