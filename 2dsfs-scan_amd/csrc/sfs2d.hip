@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -101,6 +102,7 @@ struct sfs2d_ctx {
   double* d_lnx = nullptr;
   double* d_df = nullptr;   // D(r), F(x) (LNT each), then (1/k, 1/(k(k-1))) pairs (RCPN)
   std::string err;
+  std::mutex err_mu;
 };
 
 struct sfs2d_data {
@@ -129,6 +131,8 @@ struct sfs2d_plan {
   bool fused = false;       // per-chromosome tables built inside k_scan_w (parity-alternating replicas)
   bool sliced = false;      // per-chromosome tables by k_bg_slice without its tail; k_scan_w combines
                             // the leaf sums (parity-alternating inner sums)
+  bool cnt = false;         // counts plan (no position / variant_type filter): k_prep writes no per-SNP bins,
+                            // the scan kernels classify the counts themselves (12 B/SNP per pass instead of 20)
   bool fst = false;         // SFS2D_F_FST: Fst per slot into d_fst
   double* d_fst = nullptr;
   unsigned long long* d_fsum = nullptr;   // k_prep's per-slot Fst sums (int64 fixed point), cleared by the scan
@@ -192,7 +196,10 @@ struct sfs2d_plan {
 namespace {
 
 int set_err(sfs2d_ctx* ctx, int code, const std::string& m) {
-  if (ctx) ctx->err = m;
+  if (ctx) {   // (the SFS2D_ENQ_THREADS enqueue threads may fail concurrently on one ctx)
+    std::lock_guard<std::mutex> g(ctx->err_mu);
+    ctx->err = m;
+  }
   return code;
 }
 
@@ -239,52 +246,60 @@ int plan_par(const sfs2d_plan* pl) {
 // replica parity: only fused plans alternate replicas (k_bg_slice clears what it reads)
 int repl_par(const sfs2d_plan* pl) { return pl->fused ? plan_par(pl) : 0; }
 
-template <bool P16, bool FUSED, bool FST>
+// what the scan kernels stream per SNP: the bins k_prep wrote, or (counts plans) the counts themselves
+const uint32_t* scan_src(const sfs2d_plan* pl) { return pl->cnt ? pl->data->counts : pl->d_bins; }
+
+template <bool P16, bool FUSED, bool FST, bool CNT>
 void launch_scan_w(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
-  hipExtLaunchKernelGGL((k_scan_w<P16, FUSED, FST>), dim3((unsigned)pl->chunks.size()), dim3(SBLOCK), pl->scan_lds,
-                     CTX_STREAM(pl->ctx), pl->kev[4], pl->kev[5], 0, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
+  hipExtLaunchKernelGGL((k_scan_w<P16, FUSED, FST, CNT>), dim3((unsigned)pl->chunks.size()), dim3(SBLOCK), pl->scan_lds,
+                     CTX_STREAM(pl->ctx), pl->kev[4], pl->kev[5], 0, pl->K, scan_src(pl), pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
                      per_chrom, pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, bp, pl->d_repl, pl->d_bcount,
                      plan_par(pl), pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels,
                      pl->extra_rec >= 0 ? (int)pl->last_chrom : -1, pl->d_fsum, pl->d_fst, pl->d_ctr,
                      (int)(pl->runs & 1), pl->d_leafsum, pl->d_bg1d, pl->sliced ? 1 : 0, nullptr, 0);
 }
 
-template <bool P16, bool FST>
+template <bool P16, bool FST, bool CNT>
 void launch_scan_g(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
-  hipExtLaunchKernelGGL((k_scan_g<P16, FST>), dim3((unsigned)pl->chunks.size()), dim3(BLOCK), pl->scan_lds,
-                     CTX_STREAM(pl->ctx), pl->kev[4], pl->kev[5], 0, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_head, per_chrom,
+  hipExtLaunchKernelGGL((k_scan_g<P16, FST, CNT>), dim3((unsigned)pl->chunks.size()), dim3(BLOCK), pl->scan_lds,
+                     CTX_STREAM(pl->ctx), pl->kev[4], pl->kev[5], 0, pl->K, scan_src(pl), pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_head, per_chrom,
                      pl->ctx->d_lnx, out, bp, pl->d_fsum, pl->d_fst);
 }
 
-template <bool P16, bool FST>
+template <bool P16, bool FST, bool CNT>
 void launch_scan_gw(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
-  hipExtLaunchKernelGGL((k_scan_gw<P16, FST>), dim3((unsigned)pl->chunks.size()), dim3(WAVE), pl->scan_lds,
-                     CTX_STREAM(pl->ctx), pl->kev[4], pl->kev[5], 0, pl->K, pl->d_bins, pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
+  hipExtLaunchKernelGGL((k_scan_gw<P16, FST, CNT>), dim3((unsigned)pl->chunks.size()), dim3(WAVE), pl->scan_lds,
+                     CTX_STREAM(pl->ctx), pl->kev[4], pl->kev[5], 0, pl->K, scan_src(pl), pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
                      per_chrom, pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, bp, pl->d_repl, pl->d_bcount,
                      0, pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels, -1, pl->d_fsum, pl->d_fst,
                      pl->d_ctr, (int)(pl->runs & 1), pl->d_leafsum, pl->d_bg1d, 0, pl->d_gscr, pl->nscr);
 }
 
-template <bool P16>
-hipError_t launch_scan(sfs2d_plan* pl, sfs2d_window* out) {
+template <bool P16, bool CNT>
+hipError_t launch_scan_c(sfs2d_plan* pl, sfs2d_window* out) {
   const int per_chrom = pl->prm.bg_mode == SFS2D_BG_PER_CHROM ? 1 : 0;
   const int bp = pl->prm.window_mode == SFS2D_WINDOW_BP ? 1 : 0;
   if (pl->gw) {
-    if (pl->fst) launch_scan_gw<P16, true>(pl, out, per_chrom, bp);
-    else launch_scan_gw<P16, false>(pl, out, per_chrom, bp);
+    if (pl->fst) launch_scan_gw<P16, true, CNT>(pl, out, per_chrom, bp);
+    else launch_scan_gw<P16, false, CNT>(pl, out, per_chrom, bp);
   } else if (pl->G == WAVE) {
     if (pl->fused) {
-      if (pl->fst && !pl->fst_win) launch_scan_w<P16, true, true>(pl, out, per_chrom, bp);
-      else launch_scan_w<P16, true, false>(pl, out, per_chrom, bp);
+      if (pl->fst && !pl->fst_win) launch_scan_w<P16, true, true, CNT>(pl, out, per_chrom, bp);
+      else launch_scan_w<P16, true, false, CNT>(pl, out, per_chrom, bp);
     } else {
-      if (pl->fst && !pl->fst_win) launch_scan_w<P16, false, true>(pl, out, per_chrom, bp);
-      else launch_scan_w<P16, false, false>(pl, out, per_chrom, bp);
+      if (pl->fst && !pl->fst_win) launch_scan_w<P16, false, true, CNT>(pl, out, per_chrom, bp);
+      else launch_scan_w<P16, false, false, CNT>(pl, out, per_chrom, bp);
     }
   } else {
-    if (pl->fst) launch_scan_g<P16, true>(pl, out, per_chrom, bp);
-    else launch_scan_g<P16, false>(pl, out, per_chrom, bp);
+    if (pl->fst) launch_scan_g<P16, true, CNT>(pl, out, per_chrom, bp);
+    else launch_scan_g<P16, false, CNT>(pl, out, per_chrom, bp);
   }
   return hipGetLastError();
+}
+
+template <bool P16>
+hipError_t launch_scan(sfs2d_plan* pl, sfs2d_window* out) {
+  return pl->cnt ? launch_scan_c<P16, true>(pl, out) : launch_scan_c<P16, false>(pl, out);
 }
 
 template <bool B, bool S, bool L, bool N, bool F, bool FS>
@@ -301,7 +316,8 @@ hipError_t launch_prep3(sfs2d_plan* pl) {
 
 template <bool B, bool S, bool L, bool N, bool F>
 hipError_t launch_prep2(sfs2d_plan* pl) {
-  if (N && pl->fst && !pl->fst_win) return launch_prep3<B, S, L, N, F, N>(pl);   // Fst only with the bins pass
+  // Fst sums with a plan's pass (the bins pass, or a counts plan's bins-less one); not in sfs2d_bg_hist
+  if (pl->fst && !pl->fst_win && (N || pl->cnt)) return launch_prep3<B, S, L, N, F, true>(pl);
   return launch_prep3<B, S, L, N, F, false>(pl);
 }
 
@@ -311,10 +327,29 @@ hipError_t launch_prep1(sfs2d_plan* pl) {
   return f ? launch_prep2<B, S, L, N, true>(pl) : launch_prep2<B, S, L, N, false>(pl);
 }
 
+// k_prep for a plan run: a counts plan's pass stores no bins (and is skipped when it has nothing to do:
+// supplied background, SNP-count windows, no Fst sums)
+hipError_t launch_prep_cnt(sfs2d_plan* pl) {
+  const bool L = pl->lds_hist;
+  const bool fs = pl->fst && !pl->fst_win;
+  if (pl->do_bg && pl->do_seg)
+    return L ? launch_prep1<true, true, true, false>(pl) : launch_prep1<true, true, false, false>(pl);
+  if (pl->do_bg) return L ? launch_prep1<true, false, true, false>(pl) : launch_prep1<true, false, false, false>(pl);
+  if (pl->do_seg) return launch_prep1<false, true, false, false>(pl);
+  if (fs) return launch_prep1<false, false, false, false>(pl);
+  return hipSuccess;
+}
+
+// whether a plan run launches k_prep at all
+bool prep_runs(const sfs2d_plan* pl) {
+  return !pl->tiles.empty() && (!pl->cnt || pl->do_bg || pl->do_seg || (pl->fst && !pl->fst_win));
+}
+
 hipError_t launch_prep(sfs2d_plan* pl, bool bins) {
   if (pl->tiles.empty()) return hipSuccess;
   const bool L = pl->lds_hist;
   if (!bins) return L ? launch_prep1<true, false, true, false>(pl) : launch_prep1<true, false, false, false>(pl);
+  if (pl->cnt) return launch_prep_cnt(pl);
   if (pl->do_bg && pl->do_seg)
     return L ? launch_prep1<true, true, true, true>(pl) : launch_prep1<true, true, false, true>(pl);
   if (pl->do_bg) return L ? launch_prep1<true, false, true, true>(pl) : launch_prep1<true, false, false, true>(pl);
@@ -328,7 +363,7 @@ hipError_t launch_bg_slices(sfs2d_plan* pl) {
                      CTX_STREAM(pl->ctx), pl->kev[2], pl->kev[3], 0, pl->K, pl->d_repl, pl->d_bcount + (size_t)plan_par(pl) * pl->K.nchrom, pl->d_tab,
                      pl->d_lp, pl->d_head, pl->d_leafsum, pl->d_bg1d, pl->d_done, pl->d_slices, (int)pl->slices.size(),
                      pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels, pl->sliced ? 0 : 1, pl->nfst,
-                     pl->data->counts, pl->d_bins, pl->d_slots, reinterpret_cast<const double2*>(pl->ctx->d_df + 2 * LNT),
+                     pl->data->counts, scan_src(pl), pl->d_slots, reinterpret_cast<const double2*>(pl->ctx->d_df + 2 * LNT),
                      pl->d_fst, (uint32_t)pl->nslots);
   return hipGetLastError();
 }
@@ -341,10 +376,10 @@ hipError_t launch_finalize(sfs2d_plan* pl, int integer_values) {
   return hipGetLastError();
 }
 
-template <bool P16>
+template <bool P16, bool CNT>
 hipError_t launch_extra(sfs2d_plan* pl, sfs2d_window* out) {
   const sfs2d_data* d = pl->data;
-  hipLaunchKernelGGL((k_scan_extra<P16>), dim3(1), dim3(WAVE), pl->extra_lds, CTX_STREAM(pl->ctx), pl->K, pl->d_bins,
+  hipLaunchKernelGGL((k_scan_extra<P16, CNT>), dim3(1), dim3(WAVE), pl->extra_lds, CTX_STREAM(pl->ctx), pl->K, scan_src(pl),
                      d->pos, pl->last_chrom, d->d_chrom_off, pl->d_tab, pl->d_head,
                      pl->prm.bg_mode == SFS2D_BG_PER_CHROM ? 1 : 0, pl->ctx->d_lnx, out, (long long)pl->extra_rec);
   return hipGetLastError();
@@ -353,7 +388,9 @@ hipError_t launch_extra(sfs2d_plan* pl, sfs2d_window* out) {
 hipError_t launch_scan_any(sfs2d_plan* pl, sfs2d_window* out) {
   hipError_t e = hipSuccess;
   if (!pl->chunks.empty()) e = pl->p16 ? launch_scan<true>(pl, out) : launch_scan<false>(pl, out);
-  if (e == hipSuccess && pl->extra_rec >= 0) e = pl->p16 ? launch_extra<true>(pl, out) : launch_extra<false>(pl, out);
+  if (e == hipSuccess && pl->extra_rec >= 0)
+    e = pl->p16 ? (pl->cnt ? launch_extra<true, true>(pl, out) : launch_extra<true, false>(pl, out))
+                : (pl->cnt ? launch_extra<false, true>(pl, out) : launch_extra<false, false>(pl, out));
   return e;
 }
 
@@ -371,10 +408,15 @@ hipError_t launch_attached(sfs2d_plan* a) {
     hipLaunchKernelGGL(k_fst_agg, g, dim3(256), 0, CTX_STREAM(a->ctx), a->base->d_fsum, a->base->d_slot_base,
                        a->d_slot_base, d->nchrom, a->fst_m, ns,
                        std::max(0, a->base->K.fst_e - a->K.fst_e), a->d_fsum);
-  if (a->fst_win)   // before the scan clears the slots
-    hipLaunchKernelGGL(k_fst_win, dim3((unsigned)std::min<uint32_t>(2048u, (ns + 3u) / 4u)), dim3(256), 0,
-                       CTX_STREAM(a->ctx), d->counts, a->d_bins, a->d_slots,
-                       reinterpret_cast<const double2*>(a->ctx->d_df + 2 * LNT), a->d_fst, ns);
+  if (a->fst_win) {   // before the scan clears the slots
+    const dim3 gf((unsigned)std::min<uint32_t>(2048u, (ns + 3u) / 4u));
+    if (a->cnt)
+      hipLaunchKernelGGL(k_fst_win<true>, gf, dim3(256), 0, CTX_STREAM(a->ctx), a->K, d->counts, scan_src(a), a->d_slots,
+                         reinterpret_cast<const double2*>(a->ctx->d_df + 2 * LNT), a->d_fst, ns);
+    else
+      hipLaunchKernelGGL(k_fst_win<false>, gf, dim3(256), 0, CTX_STREAM(a->ctx), a->K, d->counts, scan_src(a), a->d_slots,
+                         reinterpret_cast<const double2*>(a->ctx->d_df + 2 * LNT), a->d_fst, ns);
+  }
   const hipError_t e = launch_scan_any(a, a->d_out);
   a->last_out = a->d_out;
   a->runs++;
@@ -673,6 +715,14 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   }
   pl->nslots = (int64_t)slot_base[nc];
   pl->slot_base_h = slot_base;
+  // counts plan: no filter (the scan kernels classify counts without positions / annotations);
+  // SFS2D_CNT=0 forces the bins pipeline (comparison)
+  pl->cnt = prm->ann_want < 0 && !prm->has_start && !prm->has_end;
+  if (const char* ev = std::getenv("SFS2D_CNT")) pl->cnt = pl->cnt && ev[0] != '0';
+  pl->K.nm1 = data->n > 0 ? (uint32_t)(data->n - 1) : 0u;
+  pl->K.kmul = (uint32_t)(pl->K.n2 + 1) | (1u << 16);
+  pl->K.n12 = (uint32_t)pl->K.n1 | ((uint32_t)pl->K.n2 << 16);
+  pl->K.lim12 = (uint32_t)(pl->K.n1p - 1) | ((uint32_t)(pl->K.n2p - 1) << 16);
   if (pl->nslots > 0x7fffffffll) { delete pl; return set_err(ctx, SFS2D_E_ARG, "too many window slots (window too small)"); }
   pl->extra_rec = ((prm->flags & SFS2D_F_PREV_EXTRA) && bp && any) ? pl->nslots : -1;
   pl->nrec = pl->nslots + (pl->extra_rec >= 0 ? 1 : 0);
@@ -727,7 +777,14 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
       const int per = h2w + R1 * (K.n1p + 1) + R1 * (K.n2p + 1) + TRASH;
       const size_t hist_words = std::max<size_t>((size_t)(SBLOCK / WAVE) * per, (size_t)FUSED_VCNT + K.nt + 16);
       pl->scan_lds = sizeof(double) * (size_t)(((K.nt + 1) & ~1) + 2 * LNT) + hist_words * 4;
-    } else {
+      // with the static LDS of the variant that uses most (the batched finish's per-wave arrays, Fst);
+      // grids whose workgroup does not fit the 160 KB (e.g. 81 x 81) take the large-grid kernels
+      hipFuncAttributes fa{};
+      const size_t stat = hipFuncGetAttributes(&fa, (const void*)k_scan_w<true, true, true, true>) == hipSuccess
+                              ? fa.sharedSizeBytes : 4096;
+      if (pl->scan_lds + stat > 160 * 1024) pl->G = 256;
+    }
+    if (pl->G != WAVE) {
       pl->scan_lds = (size_t)(core + TRASH + 2) * 4 + 32 * 8 + 32 * 8;
       // k_scan_gw (a wavefront per window, tables from L2) when its one-wave workgroups, whose LDS
       // holds only the wave's histograms, still leave >= 2 wavefronts per CU (101 x 101: 7);
@@ -739,11 +796,13 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
       if (gw_lds <= 160 * 1024) {
         const hipFuncAttribute A = hipFuncAttributeMaxDynamicSharedMemorySize;
         if (gw_lds > 64 * 1024)
-          for (const void* f : {(const void*)k_scan_gw<true, false>, (const void*)k_scan_gw<false, false>,
-                                (const void*)k_scan_gw<true, true>, (const void*)k_scan_gw<false, true>})
+          for (const void* f : {(const void*)k_scan_gw<true, false, false>, (const void*)k_scan_gw<false, false, false>,
+                                (const void*)k_scan_gw<true, true, false>, (const void*)k_scan_gw<false, true, false>,
+                                (const void*)k_scan_gw<true, false, true>, (const void*)k_scan_gw<false, false, true>,
+                                (const void*)k_scan_gw<true, true, true>, (const void*)k_scan_gw<false, true, true>})
             hipFuncSetAttribute(f, A, (int)gw_lds);
-        const hipError_t oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<true, true>, WAVE, gw_lds)
-                                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<false, true>, WAVE, gw_lds);
+        const hipError_t oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<true, true, true>, WAVE, gw_lds)
+                                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<false, true, true>, WAVE, gw_lds);
         if (oe != hipSuccess) occ = 0;
         pl->gw = occ >= 2;   // measured on 201 x 151 with u16 bins (2 per CU): 22 vs 32 us for k_scan_g
         if (const char* ev = std::getenv("SFS2D_GW")) pl->gw = occ >= 1 && ev[0] == '1';
@@ -778,22 +837,24 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   if (pl->scan_lds > 64 * 1024) {
     const int lds = (int)pl->scan_lds;
     const hipFuncAttribute A = hipFuncAttributeMaxDynamicSharedMemorySize;
-    hipFuncSetAttribute((const void*)k_scan_w<true, true, false>, A, lds);
-    hipFuncSetAttribute((const void*)k_scan_w<false, true, false>, A, lds);
-    hipFuncSetAttribute((const void*)k_scan_w<true, false, false>, A, lds);
-    hipFuncSetAttribute((const void*)k_scan_w<false, false, false>, A, lds);
-    hipFuncSetAttribute((const void*)k_scan_w<true, true, true>, A, lds);
-    hipFuncSetAttribute((const void*)k_scan_w<false, true, true>, A, lds);
-    hipFuncSetAttribute((const void*)k_scan_w<true, false, true>, A, lds);
-    hipFuncSetAttribute((const void*)k_scan_w<false, false, true>, A, lds);
-    hipFuncSetAttribute((const void*)k_scan_g<true, false>, A, lds);
-    hipFuncSetAttribute((const void*)k_scan_g<false, false>, A, lds);
-    hipFuncSetAttribute((const void*)k_scan_g<true, true>, A, lds);
-    hipFuncSetAttribute((const void*)k_scan_g<false, true>, A, lds);
+    for (const void* f : {(const void*)k_scan_w<true, true, false, false>, (const void*)k_scan_w<false, true, false, false>,
+                          (const void*)k_scan_w<true, false, false, false>, (const void*)k_scan_w<false, false, false, false>,
+                          (const void*)k_scan_w<true, true, true, false>, (const void*)k_scan_w<false, true, true, false>,
+                          (const void*)k_scan_w<true, false, true, false>, (const void*)k_scan_w<false, false, true, false>,
+                          (const void*)k_scan_w<true, true, false, true>, (const void*)k_scan_w<false, true, false, true>,
+                          (const void*)k_scan_w<true, false, false, true>, (const void*)k_scan_w<false, false, false, true>,
+                          (const void*)k_scan_w<true, true, true, true>, (const void*)k_scan_w<false, true, true, true>,
+                          (const void*)k_scan_w<true, false, true, true>, (const void*)k_scan_w<false, false, true, true>,
+                          (const void*)k_scan_g<true, false, false>, (const void*)k_scan_g<false, false, false>,
+                          (const void*)k_scan_g<true, true, false>, (const void*)k_scan_g<false, true, false>,
+                          (const void*)k_scan_g<true, false, true>, (const void*)k_scan_g<false, false, true>,
+                          (const void*)k_scan_g<true, true, true>, (const void*)k_scan_g<false, true, true>})
+      hipFuncSetAttribute(f, A, lds);
   }
   if (pl->extra_lds > 64 * 1024) {
-    hipFuncSetAttribute((const void*)k_scan_extra<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->extra_lds);
-    hipFuncSetAttribute((const void*)k_scan_extra<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->extra_lds);
+    for (const void* f : {(const void*)k_scan_extra<true, false>, (const void*)k_scan_extra<false, false>,
+                          (const void*)k_scan_extra<true, true>, (const void*)k_scan_extra<false, true>})
+      hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl->extra_lds);
   }
 
   // scan work items.  k_scan_w: about one workgroup per resident slot (one dispatch wave, no
@@ -806,14 +867,14 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
     // (the grid is one dispatch wave of resident workgroups: occupancy of the variant that runs)
     hipError_t oe;
     if (pl->gw)
-      oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<true, true>, WAVE, pl->scan_lds)
-                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<false, true>, WAVE, pl->scan_lds);
+      oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<true, true, true>, WAVE, pl->scan_lds)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<false, true, true>, WAVE, pl->scan_lds);
     else if (pl->fused)
-      oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<true, true, true>, SBLOCK, pl->scan_lds)
-                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<false, true, true>, SBLOCK, pl->scan_lds);
+      oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<true, true, true, true>, SBLOCK, pl->scan_lds)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<false, true, true, true>, SBLOCK, pl->scan_lds);
     else
-      oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<true, false, true>, SBLOCK, pl->scan_lds)
-                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<false, false, true>, SBLOCK, pl->scan_lds);
+      oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<true, false, true, true>, SBLOCK, pl->scan_lds)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<false, false, true, true>, SBLOCK, pl->scan_lds);
     if (oe != hipSuccess || occ < 1) occ = 1;
     int64_t cap = (int64_t)occ * ctx->ncu;
     if (pl->gw) pl->nscr = (int)cap;   // one exact-path histogram per resident wavefront
@@ -922,6 +983,9 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
     set((const void*)k_prep<true, false, true, true, true, true>);
     set((const void*)k_prep<true, false, true, false, false, false>);   // (the histogram-only pass)
     set((const void*)k_prep<true, false, true, false, true, false>);
+    set((const void*)k_prep<true, true, true, false, false, false>);    // (counts plans: no bins)
+    set((const void*)k_prep<true, true, true, false, false, true>);
+    set((const void*)k_prep<true, false, true, false, false, true>);
     if (e != hipSuccess) {   // the large dynamic LDS was refused: the global-atomic histogram instead
       (void)hipGetLastError();
       pl->lds_hist = false;
@@ -969,7 +1033,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   rc = rc ? rc : dalloc(ctx, &pl->d_leaves, pw.leaves.size());
   rc = rc ? rc : dalloc(ctx, &pl->d_nodes, pw.nodes.size());
   rc = rc ? rc : dalloc(ctx, &pl->d_slices, pl->slices.size());
-  const size_t nbins = ((size_t)data->n + 3) / 4 * 4 + SCAN_PAD;   // k_scan_w's step loads overhang n
+  const size_t nbins = pl->cnt ? 4 : ((size_t)data->n + 3) / 4 * 4 + SCAN_PAD;   // k_scan_w's step loads overhang n
   rc = rc ? rc : dalloc(ctx, &pl->d_bins, nbins);
   rc = rc ? rc : dalloc(ctx, &pl->d_out, (size_t)pl->nrec);
   rc = rc ? rc : dalloc(ctx, &pl->d_err, 4);
@@ -1050,7 +1114,7 @@ int sfs2d_plan_run_phase(sfs2d_plan* pl, int phase, sfs2d_window* out_dev) {
   int rc = 0;
   if (phase == 0 || phase == 1) {
     HIPCHK(ctx, launch_prep(pl, true));
-    if (pl->tiles.empty() && (rc = mark(0))) return rc;
+    if (!prep_runs(pl) && (rc = mark(0))) return rc;
   } else if ((rc = mark(0))) {
     return rc;
   }
@@ -1339,7 +1403,7 @@ int sfs2d_plan_attach(sfs2d_plan* base, const sfs2d_params* prm, sfs2d_plan** ou
   sfs2d_plan* a = nullptr;
   int rc = plan_create(ctx, base->data, prm, base->sliced ? 1 : 0, &a);
   if (rc) return rc;
-  if (a->fused != base->fused || a->sliced != base->sliced || a->G != base->G) {
+  if (a->fused != base->fused || a->sliced != base->sliced || a->G != base->G || a->cnt != base->cnt) {
     plan_free(a); delete a;
     return set_err(ctx, SFS2D_E_ARG, "attached plan would take a different kernel path than its base");
   }
@@ -1511,6 +1575,7 @@ struct sfs2d_dist {
   bool to_root = false;   // ncclGather to rank 0 (else ncclAllGather)
   hipEvent_t ev_scan[2] = {nullptr, nullptr}, ev_comm[2] = {nullptr, nullptr};
   std::vector<hipEvent_t> ev_k;   // sfs2d_dist_scan_gather_streams: per-stream scan events, per-parity gather events
+  bool gath_rec[2] = {false, false};   // ... whether the parity's gather event has been recorded (by any call)
 };
 
 extern "C" {
@@ -1536,8 +1601,8 @@ int sfs2d_dist_create(sfs2d_ctx* ctx, const uint8_t* id128, int rank, int world,
   std::memcpy(id.internal, id128, NCCL_UNIQUE_ID_BYTES);
   sfs2d_dist* d = new sfs2d_dist();
   d->ctx = ctx; d->rank = rank; d->world = world;
-  d->to_root = r.gather != nullptr;
-  if (const char* ev = std::getenv("SFS2D_GATHER")) d->to_root = d->to_root && std::strcmp(ev, "all") != 0;
+  d->to_root = false;   // all-gather by default; gather-to-root opt-in (sfs2d_dist_set_gather)
+  if (const char* ev = std::getenv("SFS2D_GATHER")) d->to_root = r.gather != nullptr && std::strcmp(ev, "root") == 0;
   const ncclResult_t e = r.init_rank(&d->comm, world, id, rank);
   if (e != ncclSuccess) { delete d; return set_err(ctx, SFS2D_E_HIP, std::string("ncclCommInitRank: ") + r.errstr(e)); }
   for (int b = 0; b < 2; ++b) {
@@ -1599,6 +1664,12 @@ int sfs2d_dist_scan_gather_streams(sfs2d_dist* d, sfs2d_plan* const* plans, void
   }
   RcclApi& r = rccl();
   HIPCHK(ctx, hipSetDevice(ctx->device));
+  if ((int)d->ev_k.size() != 2 * nplans) {   // (another plan count: fresh events, after the earlier calls' work)
+    HIPCHK(ctx, hipDeviceSynchronize());
+    for (hipEvent_t e : d->ev_k) hipEventDestroy(e);
+    d->ev_k.clear();
+    d->gath_rec[0] = d->gath_rec[1] = false;
+  }
   while ((int)d->ev_k.size() < 2 * nplans) {
     hipEvent_t e = nullptr;
     HIPCHK(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1622,7 +1693,9 @@ int sfs2d_dist_scan_gather_streams(sfs2d_dist* d, sfs2d_plan* const* plans, void
     char* base = static_cast<char*>(outbuf) + (size_t)par * nplans * rows * rec;
     for (int k = 0; k < m && !rc; ++k) {
       ctx->stream = st(k);
-      if (k > 0 && g >= 2) HIPCHK(ctx, hipStreamWaitEvent(st(k), d->ev_k[nplans + par], 0));
+      // a stream k > 0 overwrites the tables the parity's last gather read (this call's group g - 2, or a
+      // previous call's: enqueued calls need no host synchronisation between them)
+      if (k > 0 && d->gath_rec[par]) HIPCHK(ctx, hipStreamWaitEvent(st(k), d->ev_k[nplans + par], 0));
       if ((rc = sfs2d_plan_run(plans[k], reinterpret_cast<sfs2d_window*>(base + (size_t)k * rows * rec)))) break;
       if (k > 0) HIPCHK(ctx, hipEventRecord(d->ev_k[k], st(k)));
     }
@@ -1636,6 +1709,7 @@ int sfs2d_dist_scan_gather_streams(sfs2d_dist* d, sfs2d_plan* const* plans, void
       break;
     }
     HIPCHK(ctx, hipEventRecord(d->ev_k[nplans + par], st(0)));
+    d->gath_rec[par] = true;
     done += m;
   }
   return rc;

@@ -123,6 +123,9 @@ struct KParams {
   int nchrom;
   int fst_e;             // Fst fixed point: sums of 2^fst_e-scaled terms (|term| <= 1), chosen per plan so
   double fst_scale;      // that the most SNPs a window can hold cannot overflow int64 (fst_fixed)
+  uint32_t nm1;          // the data set's last SNP index (counts-reading scans clamp their row loads to it)
+  uint32_t kmul;         // bytes (n2+1, 0, 1, 0): the 2D key x1*(n2+1) + x2 as one byte dot product
+  uint32_t n12, lim12;   // u16 pairs (n1, n2), (n1p-1, n2p-1): both folded 1D bins in packed 16-bit ops
 };
 
 struct Tile {   // k_prep work item: SNPs [begin, end) of chromosome chrom = [cb, ce), slots from sbase
@@ -414,6 +417,51 @@ __device__ __forceinline__ uint32_t classify_fast(const KParams& P, uint32_t c, 
          (last ? B_LAST : 0u);
 }
 
+// The bins word of one SNP straight from its packed counts, for the scan kernels of plans without a
+// position / variant_type filter ("counts" plans: k_prep writes no bins, the scans classify the
+// counts they stream).  Exactly classify()'s word wherever the plan runs without error: counts whose
+// key leaves the grid, or above 2*pop_size, make k_prep raise (ERR_GRID / ERR_KEY), and here only
+// keep the LDS indices in range (the key is clamped into the excluded last bin).
+//   a1 + a2 (one byte dot product) > n1p + n2p -> the fold swaps ref / alt in both populations: the
+//   (x1, x2) bytes are then bytes 0 and 2 of the counts, else bytes 1 and 3; k2 = x1 (n2+1) + x2 as
+//   one more dot product.
+__device__ __forceinline__ uint32_t cls_word(const KParams& P, uint32_t c) {
+  const bool sw = (int)__builtin_amdgcn_udot4(c, 0x01000100u, 0u, false) > P.fold_thr;
+  const uint32_t x = sw ? c : (c >> 8);
+  const uint32_t nb2m1 = (uint32_t)P.nb2 - 1u;
+  const uint32_t k2 = min(__builtin_amdgcn_udot4(x, P.kmul, 0u, false), nb2m1);
+  const uint32_t a1 = __builtin_amdgcn_ubfe(c, 8, 8), a2 = c >> 24;
+  const uint32_t g1 = min(a1, (uint32_t)P.n1 - a1), g2 = min(a2, (uint32_t)P.n2 - a2);
+  const uint32_t f1 = g1 - 1u < (uint32_t)(P.n1p - 1) ? g1 : 0u, f2 = g2 - 1u < (uint32_t)(P.n2p - 1) ? g2 : 0u;
+  return (k2 == nb2m1 ? B_LAST : k2) | (f1 << 16) | (f2 << 23) | B_VAR;
+}
+
+// cls_word's fields without the packing, for the scan kernels' SNP rows: the inner 2D key k2 (0: in no
+// inner bin; the excluded last bin and clamped out-of-grid keys included) and both folded inner 1D
+// bins, the latter in packed u16 arithmetic (v_perm, v_pk_sub / v_pk_min, a saturating v_pk_sub for the
+// range test: 7 operations for the two populations)
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ void cls_fields(const KParams& P, uint32_t c, uint32_t& k2, uint32_t& g1, uint32_t& g2) {
+  const bool sw = (int)__builtin_amdgcn_udot4(c, 0x01000100u, 0u, false) > P.fold_thr;
+  const uint32_t x = sw ? c : (c >> 8);
+  const uint32_t kk = __builtin_amdgcn_udot4(x, P.kmul, 0u, false);
+  k2 = kk < (uint32_t)P.nb2 - 1u ? kk : 0u;
+  const u16x2 a = as_u16x2(__builtin_amdgcn_perm(0u, c, 0x0c030c01u));      // (a1, a2)
+  const u16x2 g = __builtin_elementwise_min(a, as_u16x2(P.n12) - a);         // min(a, n - a)
+  // 1 <= g <= n_p - 1 <=> lim - (g - 1) > 0 (saturating); keep g there, 0 elsewhere
+  const u16x2 v = __builtin_elementwise_sub_sat(as_u16x2(P.lim12), g - (u16x2){1, 1});
+  const uint32_t gv = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(g, v * (u16x2){0xffff, 0xffff}));
+  g1 = gv & 0xffffu;
+  g2 = gv >> 16;
+}
+
+// the per-SNP source of the scan kernels: the bins k_prep wrote, or (CNT) the counts, classified
+template <bool CNT>
+__device__ __forceinline__ uint32_t snp_word(const KParams& P, const uint32_t* __restrict__ src, uint32_t i) {
+  return CNT ? cls_word(P, src[i]) : src[i];
+}
+
 __device__ __forceinline__ uint32_t bin_k2(uint32_t w) { return w & 0xffffu; }
 __device__ __forceinline__ uint32_t bin_g1(uint32_t w) { return (w >> 16) & 0x7fu; }
 __device__ __forceinline__ uint32_t bin_g2(uint32_t w) { return (w >> 23) & 0x7fu; }
@@ -701,10 +749,12 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
 
   constexpr uint32_t STEP = 4 * BLOCK1;
   const uint32_t ab = t.begin & ~3u, alast = (t.end - 1u) & ~3u;
+  // (a segmentation-only pass -- a supplied background, no bins, no Fst -- reads no counts)
+  constexpr bool NEED_C = DO_BG || DO_BINS || FST;
   for (uint32_t base = ab; base < t.end; base += STEP) {
     const uint32_t ia = base + 4 * threadIdx.x;
     const uint32_t il = min(ia, alast);
-    const uint4 ca = *reinterpret_cast<const uint4*>(counts + il);
+    const uint4 ca = NEED_C ? *reinterpret_cast<const uint4*>(counts + il) : make_uint4(0, 0, 0, 0);
     const uint4 pa = need_pos ? *reinterpret_cast<const uint4*>(pos + il) : make_uint4(0, 0, 0, 0);
     const uint2 aav = filt ? *reinterpret_cast<const uint2*>(ann + il) : make_uint2(0, 0);
     uint32_t wpa = 0, wna = 0;
@@ -786,10 +836,12 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
 // the 2D SFS, the excluded last bin included), terms by fst_snp, fp64 lane sums in a fixed order and
 // one DPP reduction (deterministic).  Used instead of k_prep's per-SNP fixed-point sums where the
 // GPU has idle capacity: extra workgroups of k_bg_slice (sliced plans), or k_fst_win alone.
-__device__ __forceinline__ void fst_windows(const uint32_t* __restrict__ counts, const uint32_t* __restrict__ bins,
-                                            const uint2* __restrict__ slots, const double2* __restrict__ rt,
-                                            double* __restrict__ fst_out, uint32_t nslots, uint32_t wave_id,
-                                            uint32_t nwaves) {
+// CNT: membership from the counts themselves (counts plans write no bins)
+template <bool CNT>
+__device__ __forceinline__ void fst_windows(const KParams& P, const uint32_t* __restrict__ counts,
+                                            const uint32_t* __restrict__ bins, const uint2* __restrict__ slots,
+                                            const double2* __restrict__ rt, double* __restrict__ fst_out,
+                                            uint32_t nslots, uint32_t wave_id, uint32_t nwaves) {
   const int lane = threadIdx.x & (WAVE - 1);
   for (uint32_t s = wave_id; s < nslots; s += nwaves) {
     const uint2 sr = slots[s];
@@ -806,12 +858,13 @@ __device__ __forceinline__ void fst_windows(const uint32_t* __restrict__ counts,
       for (int j = 0; j < 8; ++j) {
         const uint32_t i = r0 + 64 * j + lane;
         c[j] = i < e ? counts[i] : 0u;
-        w[j] = i < e ? bins[i] : 0u;
+        if (!CNT) w[j] = i < e ? bins[i] : 0u;
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         double nk, dk;
-        fst_snp(c[j], (bin_k2(w[j]) != 0u) | ((w[j] & B_LAST) != 0u), rt, nk, dk);
+        const uint32_t wj = CNT ? cls_word(P, c[j]) : w[j];   // (counts 0 past e: outside the set)
+        fst_snp(c[j], (bin_k2(wj) != 0u) | ((wj & B_LAST) != 0u), rt, nk, dk);
         sn += nk;
         sd += dk;
       }
@@ -823,13 +876,15 @@ __device__ __forceinline__ void fst_windows(const uint32_t* __restrict__ counts,
   }
 }
 
-__global__ __launch_bounds__(256) void k_fst_win(const uint32_t* __restrict__ counts, const uint32_t* __restrict__ bins,
-                                                 const uint2* __restrict__ slots, const double2* __restrict__ rt,
-                                                 double* __restrict__ fst_out, uint32_t nslots) {
+template <bool CNT>
+__global__ __launch_bounds__(256) void k_fst_win(KParams P, const uint32_t* __restrict__ counts,
+                                                 const uint32_t* __restrict__ bins, const uint2* __restrict__ slots,
+                                                 const double2* __restrict__ rt, double* __restrict__ fst_out,
+                                                 uint32_t nslots) {
   __shared__ double2 rl[RCPN];   // the (1/n, 1/(n(n-1))) table in LDS, as in k_bg_slice's Fst workgroups
   for (int k = threadIdx.x; k < RCPN; k += 256) rl[k] = rt[k];
   __syncthreads();
-  fst_windows(counts, bins, slots, rl, fst_out, nslots, blockIdx.x * 4u + (threadIdx.x >> 6), gridDim.x * 4u);
+  fst_windows<CNT>(P, counts, bins, slots, rl, fst_out, nslots, blockIdx.x * 4u + (threadIdx.x >> 6), gridDim.x * 4u);
 }
 
 // ------------------------------------------------------------------------------------------ K2
@@ -932,8 +987,11 @@ __global__ __launch_bounds__(KBLOCK) void k_bg_slice(KParams P, uint32_t* __rest
       double2* rl = reinterpret_cast<double2*>(acc8);
       for (int k = tid; k < RCPN; k += KBLOCK) rl[k] = rt[k];
       __syncthreads();
-      fst_windows(counts, bins, slots, rl, fst_out, nslots, (uint32_t)(s - nslices - 1) * (KBLOCK / WAVE) + (tid >> 6),
-                  (uint32_t)nfst * (KBLOCK / WAVE));
+      const uint32_t wid0 = (uint32_t)(s - nslices - 1) * (KBLOCK / WAVE) + (tid >> 6);
+      if (bins == counts)   // a counts plan (no bins): membership from the counts
+        fst_windows<true>(P, counts, bins, slots, rl, fst_out, nslots, wid0, (uint32_t)nfst * (KBLOCK / WAVE));
+      else
+        fst_windows<false>(P, counts, bins, slots, rl, fst_out, nslots, wid0, (uint32_t)nfst * (KBLOCK / WAVE));
     }
     return;
   }
@@ -1280,7 +1338,7 @@ struct TabFused {    // k_scan_w's own table: lp in LDS, counts summed from this
   }
 };
 
-template <int G, bool P16, int S1, class Tab>
+template <int G, bool P16, int S1, bool CNT, class Tab>
 __device__ __forceinline__ WinOut eval_exact(const KParams& P, const uint32_t* __restrict__ bins, uint32_t b,
                                              uint32_t e, const Tab& T, const BgHead& hb,
                                              const double* __restrict__ lnx, uint32_t* H2, uint32_t* H1a,
@@ -1289,7 +1347,7 @@ __device__ __forceinline__ WinOut eval_exact(const KParams& P, const uint32_t* _
   const bool floatv = hb.flags & BGF_FLOATV;
   uint32_t c_var = 0, c2 = 0, c_last = 0, c1a = 0, c1b = 0;
   for (uint32_t i = b + lane; i < e; i += G) {
-    const uint32_t w = bins[i];
+    const uint32_t w = snp_word<CNT>(P, bins, i);
     const uint32_t k2 = bin_k2(w), g1 = bin_g1(w), g2 = bin_g2(w);
     c_var += (w & B_VAR) ? 1u : 0u;
     c_last += (w & B_LAST) ? 1u : 0u;
@@ -1312,7 +1370,7 @@ __device__ __forceinline__ WinOut eval_exact(const KParams& P, const uint32_t* _
   double s2 = 0.0, sa = 0.0, sb = 0.0;
   bool q2 = true, qa = true, qb = true;   // x_k/N == p_k bitwise on every touched bin
   for (uint32_t i = b + lane; i < e; i += G) {
-    const uint32_t w = bins[i];
+    const uint32_t w = snp_word<CNT>(P, bins, i);
     const uint32_t k2 = bin_k2(w), g1 = bin_g1(w), g2 = bin_g2(w);
     if (k2) {
       const uint32_t x = h2_take<P16>(H2, k2);
@@ -1611,7 +1669,7 @@ __device__ __forceinline__ void fused_table(int nb2, int nh, int nt, int n1p, in
       leaves, nleaves, nodes, nnodes, nlevels, write_chrom, fsum, fst_out, ctr, cpar, leafsum, bg1d, sliced,  \
       gscr, nscr
 
-template <bool P16, bool FUSED, bool FST, bool GL>
+template <bool P16, bool FUSED, bool FST, bool GL, bool CNT>
 __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
   static_assert(!(GL && FUSED), "k_scan_gw reads finished tables");
   constexpr int NT = GL ? WAVE : SBLOCK;   // threads per workgroup
@@ -1650,10 +1708,15 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
       w.b = ch.cb + (ch.wid_lo + (s - ch.slot_lo)) * P.ws;
       w.e = w.b + P.ws;
     }
-    if (w.has) {   // the bins buffer has SCAN_PAD readable words past n; masked in the last step
-      const uint32_t* q = bins + w.b + lane;
+    if (w.has) {   // the bins buffer has SCAN_PAD readable words past n (counts: loads clamped to n); masked in the last step
+      if (CNT) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) w.u[j] = q[64 * j];
+        for (int j = 0; j < 8; ++j) w.u[j] = bins[min(w.b + (uint32_t)lane + 64u * j, P.nm1)];
+      } else {
+        const uint32_t* q = bins + w.b + lane;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w.u[j] = q[64 * j];
+      }
     }
   };
   // window schedule: one static window per wavefront, then the chromosome's pool counters (an
@@ -1799,34 +1862,41 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
     auto pair = [&](uint32_t w0, uint32_t w1, int j, bool keep) {
       w0 = 64 * j < lim ? w0 : 0u;   // SNPs past e are excluded (unconditional: cheaper than a guard)
       w1 = 64 * (j + 1) < lim ? w1 : 0u;
-      const uint32_t ww[2] = {w0, w1};
-      uint32_t rk[2], kk[2];
+      const uint32_t ww[2] = {w0, w1};   // (CNT: counts; 0 past e, in no spectrum)
+      uint32_t rk[2], kk[2], ov[2], xs[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const uint32_t w = ww[q];
-        const uint32_t k2 = bin_k2(w), g1 = bin_g1(w), g2 = bin_g2(w);
+        uint32_t k2, g1, g2;
+        if (CNT) cls_fields(P, w, k2, g1, g2);
+        else { k2 = bin_k2(w); g1 = bin_g1(w); g2 = bin_g2(w); }
         n2 += __popcll(__ballot(k2 != 0u));
         n1a += __popcll(__ballot(g1 != 0u));
         n1b += __popcll(__ballot(g2 != 0u));
         const uint32_t word = k2 ? (GL ? (k2 >> 2) : P16 ? (k2 >> 1) : k2) : trash;
-        // the byte / half's shift: the hardware reads shift operands' low five bits, so w << 3 (GL)
-        // or w << 4 serves without a mask
-        const uint32_t sh = GL ? (w << 3) : P16 ? (w << 4) : 0u;
+        // the byte / half's shift: the hardware reads shift operands' low five bits, so k2 << 3 (GL)
+        // or k2 << 4 serves without a mask (the bins word's low bits are k2's)
+        const uint32_t wk = CNT ? k2 : w;
+        const uint32_t sh = GL ? (wk << 3) : P16 ? (wk << 4) : 0u;
         uint32_t one2 = 1u;
         if (GL || P16) asm("v_lshlrev_b32 %0, %1, 1" : "=v"(one2) : "v"(sh));
-        const uint32_t old = atomicAdd(&W[word], k2 ? one2 : 0u);
-        if (GL) {   // (the trash word's low byte counts 1D increments: excluded SNPs take rank 0)
-          const uint32_t r = __builtin_amdgcn_ubfe(old, sh, 8);
-          rk[q] = k2 ? r : 0u;
-          ovf |= (k2 != 0u) & (r == 255u);
-        } else {
-          rk[q] = P16 ? __builtin_amdgcn_ubfe(old, sh, 16) : (k2 ? old : 0u);
-        }
+        ov[q] = atomicAdd(&W[word], k2 ? one2 : 0u);
+        xs[q] = sh;
         kk[q] = k2;
         if (keep) kw[(j + q) & 7] = word;
         const uint32_t u1 = g1 ? a1b + g1 * (4u * RG) : atr, u2 = g2 ? a2b + g2 * (4u * RG) : atr;
         __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u1, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u2, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {   // ranks after both SNPs' atomics are issued
+        if (GL) {   // (the trash word's low byte counts 1D increments: excluded SNPs take rank 0)
+          const uint32_t r = __builtin_amdgcn_ubfe(ov[q], xs[q], 8);
+          rk[q] = kk[q] ? r : 0u;
+          ovf |= (kk[q] != 0u) & (r == 255u);
+        } else {
+          rk[q] = P16 ? __builtin_amdgcn_ubfe(ov[q], xs[q], 16) : (kk[q] ? ov[q] : 0u);
+        }
       }
       double d[2], lp[2];
 #pragma unroll
@@ -1858,7 +1928,7 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
     }
     if (!P.fold || filt) {   // rare settings: unfolded (SNPs in the excluded last 2D bin), variant_type filter
       for (uint32_t i0 = cur.b; i0 < cur.e; i0 += WAVE) {   // wave-uniform trip count
-        const uint32_t w = i0 + lane < cur.e ? bins[i0 + lane] : 0u;
+        const uint32_t w = i0 + lane < cur.e ? snp_word<CNT>(P, bins, i0 + lane) : 0u;
         nlast += __popcll(__ballot((w & B_LAST) != 0u));
         nvar += __popcll(__ballot((w & B_VAR) != 0u));
       }
@@ -1938,7 +2008,7 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
       // rare: exact re-evaluation with the bin-by-bin proportionality test (histograms are clean)
       group_sync<WAVE>();
       if (FUSED) {
-        w = eval_exact<WAVE, P16, RG>(P, bins, cur.b, cur.e,
+        w = eval_exact<WAVE, P16, RG, CNT>(P, bins, cur.b, cur.e,
                                       TabFused{LPl, Rc, rs, P.nb2, P.n1, P.n2, P.n1p, P.h1a, P.h1b, P.t1a, P.t1b}, hb,
                                       lnx, W, H1a, H1b, nullptr, nullptr);
       } else if (GL) {
@@ -1951,12 +2021,12 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
           if (__builtin_amdgcn_readfirstlane(got) == 0u) break;
           slot = slot + 1u == (uint32_t)nscr ? 0u : slot + 1u;
         }
-        w = eval_exact<WAVE, false, RG>(P, bins, cur.b, cur.e, TabGlobal{tab + (size_t)bg * P.nt}, hb, lnx,
+        w = eval_exact<WAVE, false, RG, CNT>(P, bins, cur.b, cur.e, TabGlobal{tab + (size_t)bg * P.nt}, hb, lnx,
                                         gscr + (size_t)slot * P.nb2, H1a, H1b, nullptr, nullptr);
         __threadfence();   // the slot's words are clean again before it is released
         if (lane == 0) atomicExch(&lock[slot], 0u);
       } else {
-        w = eval_exact<WAVE, P16, RG>(P, bins, cur.b, cur.e, TabLocal{tab + (size_t)bg * P.nt, LPl}, hb, lnx, W,
+        w = eval_exact<WAVE, P16, RG, CNT>(P, bins, cur.b, cur.e, TabLocal{tab + (size_t)bg * P.nt, LPl}, hb, lnx, W,
                                       H1a, H1b, nullptr, nullptr);
       }
       if (lane == 0) atomicAdd(err_word + 1, 1u);   // statistics: windows that took the exact path
@@ -2081,7 +2151,7 @@ __device__ __forceinline__ void lds_copy_d(double* dst, const double* __restrict
 // batch of windows at once (flush), the rare exact re-evaluations included.  (Measured on config 3:
 // the loop is VALU-issue and LDS-latency bound at 4 waves per SIMD; the batched finish took it from
 // 405 to ~330 VALU instructions per window.)
-template <bool P16, bool FUSED, bool FST>
+template <bool P16, bool FUSED, bool FST, bool CNT>
 __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   constexpr int NWV = SBLOCK / WAVE;
   constexpr int SB = 4;    // windows per batch (see flush; LDS-limited)
@@ -2124,8 +2194,13 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       // (uniform base + a 32-bit lane offset: no per-lane 64-bit pointer stays live, which the exact
       // path's registers pushed to scratch -- 512 B of stores per wavefront)
       const uint32_t* q = bins + w.b;
+      if (CNT) {   // counts: no padding past n, the row loads are clamped to the last SNP (masked later)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) w.u[j] = q[(uint32_t)lane + 64u * j];
+        for (int j = 0; j < 8; ++j) w.u[j] = bins[min(w.b + (uint32_t)lane + 64u * j, P.nm1)];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w.u[j] = q[(uint32_t)lane + 64u * j];
+      }
     }
   };
   // window schedule: one static window per wavefront, then the chromosome's pool counters (an
@@ -2286,11 +2361,11 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       const uint32_t xe = xn != 0xffffu ? xb + xn : (mode_bp ? slots[xs].y : xb + P.ws);
       WinOut x;
       if (FUSED)
-        x = eval_exact<WAVE, P16, R1>(P, bins, xb, xe,
+        x = eval_exact<WAVE, P16, R1, CNT>(P, bins, xb, xe,
                                       TabFused{LPl, Rc, rs, P.nb2, P.n1, P.n2, P.n1p, P.h1a, P.h1b, P.t1a, P.t1b}, hb,
                                       lnx, W, H1a, H1b, nullptr, nullptr);
       else
-        x = eval_exact<WAVE, P16, R1>(P, bins, xb, xe, TabLocal{tab + (size_t)bg * P.nt, LPl}, hb, lnx, W, H1a, H1b,
+        x = eval_exact<WAVE, P16, R1, CNT>(P, bins, xb, xe, TabLocal{tab + (size_t)bg * P.nt, LPl}, hb, lnx, W, H1a, H1b,
                                       nullptr, nullptr);
       if (lane == 0) {
         write_rec(out + xs, ch.chrom, ch.wid_lo + (xs - ch.slot_lo), xb, xe, x, zflags);
@@ -2365,28 +2440,34 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       // more selects than the masking itself)
       w0 = 64 * j < lim ? w0 : 0u;
       w1 = 64 * (j + 1) < lim ? w1 : 0u;
-      const uint32_t ww[2] = {w0, w1};
-      uint32_t rk[2], kk[2];
+      const uint32_t ww[2] = {w0, w1};   // (CNT: counts; 0 past e, in no spectrum)
+      uint32_t rk[2], kk[2], ov[2], xs[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const uint32_t w = ww[q];
-        const uint32_t k2 = bin_k2(w), g1 = bin_g1(w), g2 = bin_g2(w);
+        uint32_t k2, g1, g2;
+        if (CNT) cls_fields(P, w, k2, g1, g2);
+        else { k2 = bin_k2(w); g1 = bin_g1(w); g2 = bin_g2(w); }
         n2 += __popcll(__ballot(k2 != 0u));
         n1a += __popcll(__ballot(g1 != 0u));
         n1b += __popcll(__ballot(g2 != 0u));
-        const uint32_t x = w << 4;   // low five bits: (k2 & 1) << 4, the u16 half's shift
+        const uint32_t x = (CNT ? k2 : w) << 4;   // low five bits: (k2 & 1) << 4, the u16 half's shift
         const uint32_t word = k2 ? (P16 ? (k2 >> 1) : k2) : trash;
         // (v_lshlrev_b32 / v_bfe_u32 read the shift's low five bits: no mask; C's << would need one)
         uint32_t one2 = 1u;
         if (P16) asm("v_lshlrev_b32 %0, %1, 1" : "=v"(one2) : "v"(x));
-        const uint32_t old = atomicAdd(&W[word], k2 ? one2 : 0u);
-        rk[q] = P16 ? __builtin_amdgcn_ubfe(old, x, 16) : (k2 ? old : 0u);
+        ov[q] = atomicAdd(&W[word], k2 ? one2 : 0u);
+        xs[q] = x;
         kk[q] = k2;
         if (keep) kw[(j + q) & 7] = word;
         const uint32_t u1 = g1 ? a1b + g1 * (4u * R1) : atr, u2 = g2 ? a2b + g2 * (4u * R1) : atr;
         __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u1, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u2, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
+      // the ranks once both SNPs' atomics are issued (extracted right after its own atomic, each rank's
+      // wait held the other SNP's work back: two LDS round trips per pair instead of one)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) rk[q] = P16 ? __builtin_amdgcn_ubfe(ov[q], xs[q], 16) : (kk[q] ? ov[q] : 0u);
       double d[2], lp[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
@@ -2418,7 +2499,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     MARK(22);
     if (!P.fold || filt) {   // rare settings: unfolded (SNPs in the excluded last 2D bin), variant_type filter
       for (uint32_t i0 = cur.b; i0 < cur.e; i0 += WAVE) {   // wave-uniform trip count
-        const uint32_t w = i0 + lane < cur.e ? bins[i0 + lane] : 0u;
+        const uint32_t w = i0 + lane < cur.e ? snp_word<CNT>(P, bins, i0 + lane) : 0u;
         nlast += __popcll(__ballot((w & B_LAST) != 0u));
         nvar += __popcll(__ballot((w & B_VAR) != 0u));
       }
@@ -2525,21 +2606,22 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   BLK_STAMP(1, 1);
 }
 
-template <bool P16, bool FUSED, bool FST>
+// CNT: `bins` is the counts array (counts plans): every scan classifies the counts it streams
+template <bool P16, bool FUSED, bool FST, bool CNT>
 __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_scan_w(SCAN_W_ARGS) {
   extern __shared__ double ldsd[];
-  scan_w_small<P16, FUSED, FST>(ldsd, SCAN_W_PASS);
+  scan_w_small<P16, FUSED, FST, CNT>(ldsd, SCAN_W_PASS);
 }
 
 // K3 for large grids, one wavefront per window (LDS: the wave's histograms only)
-template <bool P16, bool FST>
+template <bool P16, bool FST, bool CNT>
 __global__ __launch_bounds__(WAVE) void k_scan_gw(SCAN_W_ARGS) {
   extern __shared__ double ldsd[];
-  scan_w_body<P16, false, FST, true>(ldsd, SCAN_W_PASS);
+  scan_w_body<P16, false, FST, true, CNT>(ldsd, SCAN_W_PASS);
 }
 
 // K3 for large grids: one workgroup per window, exact evaluation.
-template <bool P16, bool FST>
+template <bool P16, bool FST, bool CNT>
 __global__ __launch_bounds__(BLOCK) void k_scan_g(KParams P, const uint32_t* __restrict__ bins,
                                                   const Chunk* __restrict__ chunks, uint2* __restrict__ slots,
                                                   const PL* __restrict__ tab, const BgHead* __restrict__ head,
@@ -2577,7 +2659,7 @@ __global__ __launch_bounds__(BLOCK) void k_scan_g(KParams P, const uint32_t* __r
       b = ch.cb + wid * P.ws;
       e = b + P.ws;
     }
-    const WinOut w = eval_exact<BLOCK, P16, 1>(P, bins, b, e, TabGlobal{T}, hb, lnx, H2, H1a, H1b, redd, redu);
+    const WinOut w = eval_exact<BLOCK, P16, 1, CNT>(P, bins, b, e, TabGlobal{T}, hb, lnx, H2, H1a, H1b, redd, redu);
     if (FST && threadIdx.x == 0) fst_out[s] = fst_take(fsum, s);
     if (threadIdx.x == 0) {
       write_rec(out + s, ch.chrom, wid, b, e, w, bg_zero_flags(hb));
@@ -2603,7 +2685,7 @@ __device__ uint32_t window_begin_back(const uint32_t* __restrict__ pos, long lon
 // Q9 helper (combined_scan's final block, twoDSFS_class.py:951-989): the window before the last
 // one, evaluated against the LAST window's chromosome background.  One wavefront; launched only
 // for plans with SFS2D_F_PREV_EXTRA.
-template <bool P16>
+template <bool P16, bool CNT>
 __global__ __launch_bounds__(WAVE) void k_scan_extra(KParams P, const uint32_t* __restrict__ bins,
                                                      const uint32_t* __restrict__ pos, uint32_t chrom_last,
                                                      const long long* __restrict__ chrom_off,
@@ -2632,7 +2714,7 @@ __global__ __launch_bounds__(WAVE) void k_scan_extra(KParams P, const uint32_t* 
     while (c2 > 0 && chrom_off[c2] >= (long long)pe) --c2;
     pc = (uint32_t)c2;
     pb = window_begin_back(pos, chrom_off[c2], pe, P.ws);
-    w = eval_exact<WAVE, P16, 1>(P, bins, pb, pe, TabGlobal{T}, hb, lnx, H2, H1a, H1b, nullptr, nullptr);
+    w = eval_exact<WAVE, P16, 1, CNT>(P, bins, pb, pe, TabGlobal{T}, hb, lnx, H2, H1a, H1b, nullptr, nullptr);
   } else {
     flags |= SFS2D_W_EMPTY;
   }

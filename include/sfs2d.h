@@ -156,7 +156,9 @@ int sfs2d_plan_run_many(sfs2d_plan* plan, int nruns, sfs2d_window* out_dev);
  * NULL = plan-owned).  Independent scans (replicates, data sets, repeated passes) overlap across the
  * streams; each plan's own runs stay ordered on its stream.  SFS2D_ENQ_THREADS=1 (distinct
  * streams): every plan's runs are enqueued by a host thread of its own, joined before return.  The
- * ctx stream is unchanged after. */
+ * ctx stream is unchanged after.  The runs are only enqueued: synchronise the passed streams before
+ * sfs2d_plan_read / _check / _fst_read / _destroy of these plans (those synchronise the ctx stream
+ * only). */
 int sfs2d_plan_run_streams(sfs2d_plan* const* plans, void* const* streams, sfs2d_window* const* outs, int nplans,
                            int nruns);
 /* copy the last run's records to host (synchronises the stream) */
@@ -215,10 +217,10 @@ int sfs2d_plan_destroy(sfs2d_plan* plan);
  * gather of step s); comm_stream NULL: each gather follows its scan on the library's stream (no
  * cross-stream events).  Steps are numbered from `first_step`.  Enqueue only: synchronise the
  * streams to wait; synchronise before switching between the two modes.
- * sfs2d_dist_set_gather: 1 (the default when RCCL has it) = one ncclGather to rank 0 per step (the
- * reference's results have one consumer; only rank 0's `gathered` buffers are written, the other
- * ranks' are left alone), 0 = ncclAllGather into every rank's buffers.  SFS2D_E_ARG for 1 when the
- * loaded RCCL lacks ncclGather. */
+ * sfs2d_dist_set_gather: 0 (the default) = ncclAllGather into every rank's buffers; 1 = one
+ * ncclGather to rank 0 per step (the reference's results have one consumer; only rank 0's `gathered`
+ * buffers are written, the other ranks' are left alone).  SFS2D_E_ARG for 1 when the loaded RCCL
+ * lacks ncclGather.  SFS2D_GATHER=root makes 1 the create-time default. */
 typedef struct sfs2d_dist sfs2d_dist;
 int sfs2d_dist_unique_id(uint8_t* id128);
 int sfs2d_dist_create(sfs2d_ctx* ctx, const uint8_t* id128, int rank, int world, sfs2d_dist** out);

@@ -26,13 +26,23 @@ def _expected_windows(p, ws):
     return np.concatenate(out)
 
 
+def _win(p, b, e):
+    from sfs2d.pack import PackedSNPs
+    return PackedSNPs(p.counts[b:e], p.pos[b:e], np.array([0, e - b]), ["w"], p.ann_id[b:e], list(p.ann_names),
+                      p.pop1, p.pop2)
+
+
 @pytest.mark.timeout(600)
 def test_config3_full_size_20kb_500kb_one_pass():
     from sfs2d import _lib as L
     from sfs2d.engine import Engine, ScanConfig
     from sfs2d.synth import synth_genome
+    import time
+    t0 = time.perf_counter()
+    log = lambda m: print(f"[config3 {time.perf_counter() - t0:6.1f}s] {m}", flush=True)
     p = synth_genome(NCHROM, PER, POP, POP, seed=777)   # the stream bench.py's roofline_hbm times
     assert p.n == 50_000_000
+    log("generated")
     eng = Engine.get(0)
     dev = eng.upload(p)
     base = eng.plan(dev, ScanConfig(n1p=POP, n2p=POP, window=20000, fst=True))
@@ -41,6 +51,7 @@ def test_config3_full_size_20kb_500kb_one_pass():
     base.check()
     big.check()
     tabs = {20000: (base.read(), base.read_fst()), 500000: (big.read(), big.read_fst())}
+    log("scanned")
     # per-chromosome backgrounds: inner 2D sums for every chromosome, bit-exact tables for three
     ocfg = O.Cfg(POP, POP)
     pick = [0, 13, 31]
@@ -54,6 +65,7 @@ def test_config3_full_size_20kb_500kb_one_pass():
             o2, o1, o1b = O.sfs2d(p, idx, ocfg), O.sfs1d(p, idx, 1, ocfg), O.sfs1d(p, idx, 2, ocfg)
             assert np.array_equal(np.asarray(h2), o2) and np.array_equal(u1, o1) and np.array_equal(u2, o1b), c
             bgo[c] = (o2, O.fold1d(o1), O.fold1d(o1b))
+    log("backgrounds")
     rng = np.random.default_rng(3)
     for ws, (recs, fst) in tabs.items():
         live = (recs["flags"] & L.W_EMPTY) == 0
@@ -70,8 +82,9 @@ def test_config3_full_size_20kb_500kb_one_pass():
         # oracle sample: 200 windows of the three chromosomes with oracle backgrounds
         cand = np.nonzero(np.isin(exp[:, 0], pick))[0]
         sample = np.sort(rng.choice(cand, 200, replace=False))
-        wins = [(int(exp[i, 0]), int(exp[i, 2]), int(exp[i, 3])) for i in sample]
-        ref = O.window_records(p, wins, ocfg, lambda c: bgo[c])
+        # (the oracle reads whole-array fields of its input: one small packed set per window)
+        ref = [O.window_records(_win(p, int(exp[i, 2]), int(exp[i, 3])), [(0, 0, int(exp[i, 3] - exp[i, 2]))], ocfg,
+                                lambda _c, c=int(exp[i, 0]): bgo[c])[0] for i in sample]
         for i, o in zip(sample, ref):
             r = body[i]
             for f, g in (("snp_count", "snp_count"), ("n2", "N2"), ("n1a", "N1a"), ("n1b", "N1b")):
@@ -81,8 +94,10 @@ def test_config3_full_size_20kb_500kb_one_pass():
         # Fst (this framework's Hudson estimator; parity vs its own oracle restatement)
         fl = fst[: len(live)][live[: len(fst)]]
         for i in sample[::4]:
-            want = O.window_fst(p, np.arange(exp[i, 2], exp[i, 3]), ocfg)
+            q = _win(p, int(exp[i, 2]), int(exp[i, 3]))
+            want = O.window_fst(q, np.arange(q.n), ocfg)
             a = float(fl[i])
             assert (np.isnan(a) if want is None else abs(a - want) <= 1e-12 + 1e-10 * abs(want)), (ws, i)
+        log(f"{ws} bp windows checked")
     base.close()
     dev.close()

@@ -116,8 +116,10 @@ def _records_vs_oracle(p, cfg_scan, ocfg, wins, bg_of, guards=True):
 
 
 @pytest.mark.parametrize("n1p,n2p,ws", [(25, 25, 20000), (18, 14, 7000), (50, 50, 20000), (100, 75, 100000),
-                                          (3, 2, 500), (25, 25, 500000)])
+                                          (3, 2, 500), (25, 25, 500000), (40, 40, 20000), (44, 30, 20000)])
 def test_records_per_chrom_bp(n1p, n2p, ws):
+    """(40 x 40, 44 x 30: grids under the small-grid limit whose k_scan_w workgroup does not fit the
+    LDS take the large-grid kernels.)"""
     from sfs2d import _lib as L
     from sfs2d.engine import ScanConfig
     from sfs2d.synth import synth_genome
