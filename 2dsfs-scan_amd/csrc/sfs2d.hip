@@ -876,6 +876,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
       oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<true, false, true, true>, SBLOCK, pl->scan_lds)
                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<false, false, true, true>, SBLOCK, pl->scan_lds);
     if (oe != hipSuccess || occ < 1) occ = 1;
+    if (prm->scan_wgs_per_cu > 0 && (int)prm->scan_wgs_per_cu < occ) occ = (int)prm->scan_wgs_per_cu;
     int64_t cap = (int64_t)occ * ctx->ncu;
     if (pl->gw) pl->nscr = (int)cap;   // one exact-path histogram per resident wavefront
     if (const char* ev = std::getenv("SFS2D_WGS")) cap = std::max<int64_t>(1, std::atoll(ev));   // tuning

@@ -724,7 +724,11 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         double nk, dk;
+#ifdef SFS2D_EXP_FSTCONST
+        nk = (double)(cc[k] & 1u); dk = fm[k] ? 1.0 : 0.0;   // experiment: no term arithmetic
+#else
         fst_snp(cc[k], fm[k], sh_rcp, nk, dk);
+#endif
         if (k && fw[k] != wc) {
           fst_add(wc, sn, sd);
           sn = 0.0; sd = 0.0; wc = fw[k];

@@ -56,7 +56,7 @@ class Params(C.Structure):
         ("n1p", C.c_int32), ("n2p", C.c_int32), ("fold", C.c_int32), ("window_mode", C.c_int32),
         ("window", C.c_int64), ("bg_mode", C.c_int32), ("ann_want", C.c_int32),
         ("has_start", C.c_int32), ("has_end", C.c_int32), ("start_pos", C.c_int64), ("end_pos", C.c_int64),
-        ("flags", C.c_uint32), ("reserved", C.c_uint32),
+        ("flags", C.c_uint32), ("scan_wgs_per_cu", C.c_uint32),
     ]
 
 

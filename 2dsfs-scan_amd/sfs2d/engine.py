@@ -29,6 +29,7 @@ class ScanConfig:
     end_position: Optional[int] = None
     prev_extra: bool = False
     fst: bool = False          # also compute Hudson's Fst per window slot (Plan.read_fst)
+    scan_wgs_per_cu: int = 0   # cap on scan workgroups per CU (0: all that fit; see sfs2d_params)
 
     def params(self) -> L.Params:
         p = L.Params()
@@ -42,6 +43,7 @@ class ScanConfig:
         p.has_end = 0 if self.end_position is None else 1
         p.end_pos = 0 if self.end_position is None else clamp(self.end_position)
         p.flags = (L.F_PREV_EXTRA if self.prev_extra else 0) | (L.F_FST if self.fst else 0)
+        p.scan_wgs_per_cu = int(self.scan_wgs_per_cu)
         return p
 
 

@@ -81,7 +81,9 @@ typedef struct {
   int32_t has_start, has_end; /* SFS position filter start_position / end_position (179-182) */
   int64_t start_pos, end_pos;
   uint32_t flags;         /* SFS2D_F_* */
-  uint32_t reserved;
+  uint32_t scan_wgs_per_cu; /* 0: the scan kernel's grid is one resident wave of workgroups (all that fit);
+                               k > 0: at most k workgroups per CU -- leaves CUs to the next pass's k_prep
+                               when independent passes overlap on several streams (sfs2d_plan_run_streams) */
 } sfs2d_params;
 
 /* one record per window slot (64 bytes) */
