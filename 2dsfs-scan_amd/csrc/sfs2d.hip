@@ -1253,6 +1253,37 @@ int sfs2d_plan_bg_buffer(sfs2d_plan* pl, void** dev_ptr, int64_t* nbytes) {
   return 0;
 }
 
+int sfs2d_plan_bg_words(const sfs2d_plan* pl, int64_t* replicas, int64_t* nchrom, int64_t* bins) {
+  if (!pl || !replicas || !nchrom || !bins) return SFS2D_E_ARG;
+  *replicas = pl->do_bg ? REPL : 0;
+  *nchrom = pl->do_bg ? pl->data->nchrom : 0;
+  *bins = pl->do_bg ? pl->K.nh : 0;
+  return 0;
+}
+
+int sfs2d_plan_bg_exchange(sfs2d_plan* pl, uint32_t* host_repl, uint32_t* host_sums, int to_device) {
+  if (!pl || !host_repl || !host_sums) return SFS2D_E_ARG;
+  sfs2d_ctx* ctx = pl->ctx;
+  if (!pl->do_bg) return set_err(ctx, SFS2D_E_ARG, "plan has no per-chromosome backgrounds");
+  if (pl->base) return set_err(ctx, SFS2D_E_ARG, "exchange the base plan's backgrounds");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  // this run's buffers: the replicas k_prep accumulated into and the per-chromosome inner 2D sums
+  // (the parities of sfs2d_plan_run_phase(plan, 1) of the run in progress)
+  uint32_t* r = pl->d_repl + (size_t)repl_par(pl) * REPL * pl->data->nchrom * pl->K.nh;
+  uint32_t* b = pl->d_bcount + (size_t)plan_par(pl) * pl->K.nchrom;
+  const size_t nr = (size_t)REPL * pl->data->nchrom * pl->K.nh * 4, nb = (size_t)pl->K.nchrom * 4;
+  hipStream_t st = CTX_STREAM(ctx);
+  if (to_device) {
+    HIPCHK(ctx, hipMemcpyAsync(r, host_repl, nr, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(b, host_sums, nb, hipMemcpyHostToDevice, st));
+  } else {
+    HIPCHK(ctx, hipMemcpyAsync(host_repl, r, nr, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(host_sums, b, nb, hipMemcpyDeviceToHost, st));
+  }
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  return 0;
+}
+
 int sfs2d_plan_fst_buffer(sfs2d_plan* pl, void** dev_ptr, int64_t* nslots) {
   if (!pl || !dev_ptr || !nslots) return SFS2D_E_ARG;
   if (!pl->fst) return set_err(pl->ctx, SFS2D_E_ARG, "plan was created without SFS2D_F_FST");

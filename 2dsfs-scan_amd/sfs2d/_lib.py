@@ -31,7 +31,7 @@ EXPORTS = [
     "sfs2d_plan_num_records", "sfs2d_plan_set_background", "sfs2d_plan_run", "sfs2d_plan_run_many", "sfs2d_plan_set_timing_sampled",
     "sfs2d_plan_set_timing_kernels",
     "sfs2d_plan_fst_read", "sfs2d_plan_fst_buffer", "sfs2d_plan_read",
-    "sfs2d_plan_bg_buffer", "sfs2d_plan_run_phase", "sfs2d_plan_check", "sfs2d_plan_time",
+    "sfs2d_plan_bg_buffer", "sfs2d_plan_bg_words", "sfs2d_plan_bg_exchange", "sfs2d_plan_run_phase", "sfs2d_plan_check", "sfs2d_plan_time",
     "sfs2d_plan_destroy", "sfs2d_scan", "sfs2d_plan_set_timing", "sfs2d_plan_timing_read",
     "sfs2d_plan_stats", "sfs2d_plan_grids", "sfs2d_plan_attach", "sfs2d_data_synth_sims",
     "sfs2d_data_read", "sfs2d_dist_unique_id", "sfs2d_dist_create", "sfs2d_dist_scan_gather",
@@ -111,6 +111,8 @@ def lib():
     L.sfs2d_plan_run_phase.argtypes = [vp, C.c_int, vp]
     L.sfs2d_plan_read.argtypes = [vp, vp, i64, C.POINTER(i64)]
     L.sfs2d_plan_bg_buffer.argtypes = [vp, C.POINTER(vp), C.POINTER(i64)]
+    L.sfs2d_plan_bg_words.argtypes = [vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)]
+    L.sfs2d_plan_bg_exchange.argtypes = [vp, vp, vp, C.c_int]
     L.sfs2d_plan_check.argtypes = [vp]
     L.sfs2d_plan_time.argtypes = [vp, C.c_int] + [C.POINTER(C.c_double)] * 4
     L.sfs2d_plan_destroy.argtypes = [vp]

@@ -23,6 +23,10 @@ import numpy as np
 
 from . import _lib as L
 
+# scan_records_split calls of this process: "split" (scans done split), "allreduce" (background
+# all-reduces), "fallback" (scans redone by whole chromosomes after an error)
+STATS = {"split": 0, "allreduce": 0, "fallback": 0}
+
 
 def shard_chromosomes(chrom_off: Sequence[int], world: int) -> List[Tuple[int, int]]:
     """Contiguous chromosome ranges [lo, hi) per rank, balanced by SNP count (greedy cuts at
@@ -113,9 +117,162 @@ def gather_tables(local: np.ndarray, world: int, device=None) -> List[np.ndarray
     return [allb[r, : ns[r]].copy().view(L.WINDOW_DTYPE).reshape(-1) for r in range(world)]
 
 
+def window_starts(p, cfg) -> np.ndarray:
+    """Global SNP indices where a window of the plan ``cfg`` starts (the cut candidates of a split):
+    fixed-bp windows start where (pos-1)//ws or the chromosome changes; SNP-count windows every S
+    SNPs from each chromosome's first (a chromosome's incomplete tail stays with its last window)."""
+    from . import _lib as LL
+    out = []
+    for c in range(p.nchrom):
+        lo, hi = int(p.chrom_off[c]), int(p.chrom_off[c + 1])
+        if hi <= lo:
+            continue
+        if cfg.window_mode == LL.WINDOW_BP:
+            w = (np.maximum(p.pos[lo:hi].astype(np.int64), 1) - 1) // int(cfg.window)
+            out.append(lo + np.concatenate([[0], np.nonzero(np.diff(w))[0] + 1]))
+        else:
+            S = int(cfg.window)
+            full = (hi - lo) // S
+            out.append(lo + S * np.arange(max(full, 1)))
+    return np.concatenate(out).astype(np.int64) if out else np.zeros(0, np.int64)
+
+
+def split_points(p, cfg, world: int) -> List[int]:
+    """Cuts 0 = c_0 <= c_1 <= ... <= c_world = n at window starts, c_k the one nearest k n / world:
+    rank r scans SNPs [c_r, c_r+1) -- whole windows, chromosomes cut wherever that balances the
+    SNPs.  With the Q9 helper (cfg.prev_extra) the last non-empty rank keeps >= 2 windows (the helper
+    re-evaluates the window before the last one of the scan, against the last chromosome's
+    background)."""
+    n = p.n
+    starts = window_starts(p, cfg)
+    cuts = [0]
+    for k in range(1, world):
+        t = n * k / world
+        j = int(np.searchsorted(starts, t))
+        cand = [int(starts[i]) for i in (j - 1, j) if 0 <= i < len(starts)]
+        c = min(cand, key=lambda x: abs(x - t)) if cand else n
+        cuts.append(max(cuts[-1], min(c, n)))
+    cuts.append(n)
+    if cfg.prev_extra and len(starts) >= 2:
+        last_ok = int(starts[-2])
+        cuts = [0] + [min(c, last_ok) for c in cuts[1:-1]] + [n]
+    return cuts
+
+
+def _merge_split(tables, cuts, c0s, prev_extra, snp_window=0, chrom_off=None):
+    """Rank tables (each numbered locally: chromosome 0 = the rank's first, SNPs from its cut) -> the
+    global table: every rank's non-empty records in rank order (a window never spans two ranks),
+    then the Q9 helper record of the last non-empty rank.  Empty bp slots are dropped (the post-pass
+    skips them).  SNP-count windows (snp_window = S) of a part that starts inside a chromosome are
+    renumbered from the windows before the cut (bp windows are numbered by position already)."""
+    parts, extra = [], None
+    for r, t in enumerate(tables):
+        t = np.asarray(t, dtype=L.WINDOW_DTYPE).copy()
+        if not len(t):
+            continue
+        live = (t["flags"] & L.W_EMPTY) == 0
+        if snp_window:
+            first = live & (t["chrom"] == 0)
+            t["wid"][first] += np.uint32((cuts[r] - int(chrom_off[c0s[r]])) // snp_window)
+        t["chrom"] += np.uint32(c0s[r])
+        t["begin"][live] += np.uint32(cuts[r])
+        t["end"][live] += np.uint32(cuts[r])
+        is_x = (t["flags"] & L.W_EXTRA) != 0
+        parts.append(t[live & ~is_x])
+        if prev_extra and is_x.any():
+            e = t[is_x]
+            e["wid"][(e["flags"] & L.W_EMPTY) == 0] += np.uint32(cuts[r])   # the helper's wid: a SNP index
+            extra = e
+    out = np.concatenate(parts) if parts else np.zeros(0, dtype=L.WINDOW_DTYPE)
+    return np.concatenate([out, extra]) if extra is not None else out
+
+
 def _comm_device(device):
     import torch.distributed as dist
     return f"cuda:{device}" if dist.get_backend() == "nccl" else None
+
+
+def _agree(err, size, world):
+    """One collective: (any rank failed?, the largest `size` reported)."""
+    import torch.distributed as dist
+    got = [None] * world
+    dist.all_gather_object(got, (err is not None, int(size)))
+    return any(g[0] for g in got), max(g[1] for g in got)
+
+
+def _allreduce_sum(v: np.ndarray, comm_device):
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cpu") if comm_device is None else torch.device(comm_device)
+    t = torch.from_numpy(np.ascontiguousarray(v, np.int64)).to(dev)
+    dist.all_reduce(t)
+    return t.cpu().numpy()
+
+
+def whole_scan(split_scan):
+    """The one-rank scan of a split-scan job factory: its own histograms are the totals."""
+    def scan(sub, cfg, bg):
+        job = split_scan(sub, cfg, bg)
+        return job.finish(job.partial())
+    return scan
+
+
+def scan_records_split(p, cfg, bg, split_scan, device: int = 0, comm_device="auto") -> np.ndarray:
+    """One scan of ``p`` split over the default process group at window boundaries (split_points):
+    rank r scans SNPs [c_r, c_r+1) -- chromosomes cut wherever that balances the SNPs, so one
+    chromosome spreads over all ranks.  With per-chromosome backgrounds every chromosome's histograms
+    are the sum of its parts': between k_prep and the scan each rank's partial histograms are summed
+    over the ranks (one all-reduce of int64 words, SURVEY 8(e) collective (1)).
+
+    ``split_scan(sub, cfg, bg)`` makes a rank's job over its part ``sub`` (chromosomes numbered from
+    the part's first): ``job.partial()`` runs k_prep and returns the part's histograms as an int64
+    array (one row per chromosome of ``sub``; None without per-chromosome backgrounds), and
+    ``job.finish(total)`` writes the summed rows back, scans and returns the records.  Every rank
+    returns the global record table (sfs2d.post reads it like one plan's).  When any rank fails, the
+    whole scan is redone sharded by whole chromosomes (scan_records), which raises the error the
+    reference raises on every rank (a chromosome's first bad SNP decides it, and it may sit in another
+    rank's part)."""
+    import dataclasses
+
+    import torch.distributed as dist
+    rank, world = dist.get_rank(), dist.get_world_size()
+    if comm_device == "auto":
+        comm_device = _comm_device(device)
+    cuts = split_points(p, cfg, world)
+    lo, hi = cuts[rank], cuts[rank + 1]
+    last = max((r for r in range(world) if cuts[r + 1] > cuts[r]), default=-1)
+    sub, c0 = p.slice_snps(lo, hi)
+    c0s = [p.slice_snps(cuts[r], cuts[r + 1])[1] for r in range(world)]
+    job, part, err = None, None, None
+    if hi > lo:
+        try:
+            job = split_scan(sub, dataclasses.replace(cfg, prev_extra=bool(cfg.prev_extra) and rank == last), bg)
+            part = job.partial()
+        except Exception as e:  # noqa: BLE001  (every rank takes the fallback below)
+            err = e
+    failed, width = _agree(err, -1 if part is None else np.asarray(part).shape[1], world)
+    local = np.zeros(0, dtype=L.WINDOW_DTYPE)
+    if not failed:
+        total = None
+        if width > 0:
+            g = np.zeros((p.nchrom, width), np.int64)
+            if part is not None:
+                g[c0:c0 + len(part)] = part
+            total = _allreduce_sum(g.reshape(-1), comm_device).reshape(p.nchrom, width)
+            STATS["allreduce"] += 1
+        if job is not None:
+            try:
+                local = job.finish(None if total is None else total[c0:c0 + sub.nchrom])
+            except Exception as e:  # noqa: BLE001
+                err = e
+        failed, _ = _agree(err, 0, world)
+    if failed:
+        STATS["fallback"] += 1
+        return scan_records(p, cfg, bg, whole_scan(split_scan), device, comm_device)
+    STATS["split"] += 1
+    tables = gather_tables(local, world, comm_device)
+    return _merge_split(tables, cuts, c0s, bool(cfg.prev_extra),
+                        int(cfg.window) if cfg.window_mode == L.WINDOW_SNPS else 0, p.chrom_off)
 
 
 def scan_records(p, cfg, bg, scan_local, device: int = 0, comm_device="auto") -> np.ndarray:

@@ -288,6 +288,74 @@ class Plan:
             pass
 
 
+class SplitJob:
+    """A rank's part of a scan split over ranks at window boundaries (sfs2d.dist.scan_records_split):
+    its SNPs uploaded, one plan, k_prep run alone (``partial``: this part's per-chromosome background
+    histograms), the summed histograms written back and the scan run (``finish``)."""
+
+    def __init__(self, eng: Engine, sub: PackedSNPs, cfg: ScanConfig, bg=None):
+        self.eng, self.cfg, self.nchrom = eng, cfg, sub.nchrom
+        self.dev = eng.upload(sub)
+        self.pl = None
+        try:
+            self.pl = Plan(eng, self.dev, cfg)
+            if cfg.bg_mode == L.BG_SUPPLIED:
+                self.pl.set_background(*bg)
+        except Exception:
+            self.close()
+            raise
+        self.shape = None
+
+    def _words(self):
+        r, c, b = C.c_int64(), C.c_int64(), C.c_int64()
+        self.eng.check(self.eng.lib.sfs2d_plan_bg_words(self.pl.h, C.byref(r), C.byref(c), C.byref(b)))
+        return r.value, c.value, b.value
+
+    def partial(self) -> Optional[np.ndarray]:
+        """int64 [nchrom, bins + 1]: the part's histograms (replicas summed) and inner 2D sums; None for a
+        supplied background (nothing to exchange)."""
+        if self.cfg.bg_mode != L.BG_PER_CHROM:
+            return None
+        self.pl.run(phase=1)
+        r, c, b = self._words()
+        self.shape = (r, c, b)
+        repl = np.zeros(r * c * b, np.uint32)
+        sums = np.zeros(c, np.uint32)
+        self.eng.check(self.eng.lib.sfs2d_plan_bg_exchange(self.pl.h, L.ptr(repl), L.ptr(sums), 0))
+        h = repl.reshape(r, c, b).sum(axis=0, dtype=np.int64)
+        return np.concatenate([h, sums.astype(np.int64)[:, None]], axis=1)
+
+    def finish(self, total: Optional[np.ndarray]) -> np.ndarray:
+        """Scan with the summed histograms ``total`` (partial()'s layout) and return the records."""
+        try:
+            if total is None or self.shape is None:
+                self.pl.run()
+            else:
+                r, c, b = self.shape
+                t = np.asarray(total, np.int64)
+                if t.shape != (c, b + 1):
+                    raise ValueError(f"summed histograms have shape {t.shape}, the plan's are {(c, b + 1)}")
+                if t.size and (t.min() < 0 or t.max() >= 1 << 32):
+                    raise L.Sfs2dError(L.E_ARG, "summed background histograms overflow uint32")
+                repl = np.zeros((r, c, b), np.uint32)
+                repl[0] = t[:, :b]
+                sums = np.ascontiguousarray(t[:, b], np.uint32)
+                self.eng.check(self.eng.lib.sfs2d_plan_bg_exchange(self.pl.h, L.ptr(repl), L.ptr(sums), 1))
+                self.pl.run(phase=2)
+            self.pl.check()
+            return self.pl.read()
+        finally:
+            self.close()
+
+    def close(self):
+        if self.pl is not None:
+            self.pl.close()
+            self.pl = None
+        if self.dev is not None:
+            self.dev.close()
+            self.dev = None
+
+
 class Dist:
     """One rank's RCCL communicator in the native library (sfs2d_dist_*): back-to-back scans of a
     plan, each gathering the fixed-stride window tables of every rank to rank 0 (ncclGather; or

@@ -117,6 +117,18 @@ class PackedSNPs:
         return PackedSNPs(lo | (lo << np.uint32(16)), self.pos, self.chrom_off, list(self.chrom_names),
                           self.ann_id, list(self.ann_names), pop, pop)
 
+    def slice_snps(self, lo: int, hi: int):
+        """(SNPs [lo, hi) of the scan order as a data set of the chromosomes they touch, index of its
+        first chromosome here): a rank's part of a data set split at window boundaries (sfs2d.dist)."""
+        if hi <= lo:
+            return PackedSNPs(self.counts[:0], self.pos[:0], np.zeros(1, np.int64), [], self.ann_id[:0],
+                              list(self.ann_names), self.pop1, self.pop2), 0
+        c0 = int(np.searchsorted(self.chrom_off, lo, side="right")) - 1
+        c1 = int(np.searchsorted(self.chrom_off, hi, side="left"))      # chromosomes c0 .. c1-1
+        off = np.clip(self.chrom_off[c0:c1 + 1], lo, hi) - lo
+        return PackedSNPs(self.counts[lo:hi], self.pos[lo:hi], off, list(self.chrom_names[c0:c1]),
+                          self.ann_id[lo:hi], list(self.ann_names), self.pop1, self.pop2), c0
+
     def subset_chroms(self, idx) -> "PackedSNPs":
         idx = list(idx)
         parts_c, parts_p, parts_a, offs = [], [], [], [0]

@@ -180,6 +180,11 @@ def _scan_local(p, cfg, bg):
         dev.close()
 
 
+def _split_scan(p, cfg, bg):
+    from sfs2d.engine import SplitJob
+    return SplitJob(Engine.get(DEVICE), p, cfg, bg)
+
+
 def process_windows_batch(replicates, bg_2d_sfs, bg_p1_sfs, bg_p2_sfs, window_size, pop1, pop2, pop1_size,
                           pop2_size, start_position=None, end_position=None, variant_type=None, distributed=False):
     """``process_window`` (sims_scan.py:451-590) over many replicate data sets in ONE scan launch:
@@ -188,7 +193,8 @@ def process_windows_batch(replicates, bg_2d_sfs, bg_p1_sfs, bg_p2_sfs, window_si
     replicate (in order) whose window has no SNP / an empty background raises ZeroDivisionError, as
     the reference's loop over replicates would (sims_scan.py:619-622).  ``distributed``: the
     replicates' chromosomes are sharded over the torch.distributed group (one process per GPU, all
-    ranks calling with the same arguments; every rank returns the whole list)."""
+    ranks calling with the same arguments; every rank returns the whole list), split at window
+    boundaries balanced by SNPs (sfs2d.dist.scan_records_split)."""
     packs = [_pack(d, pop1, pop2) for d in replicates]
     if not packs:
         return []
@@ -200,7 +206,7 @@ def process_windows_batch(replicates, bg_2d_sfs, bg_p1_sfs, bg_p2_sfs, window_si
     bg = _bg_arrays(bg_2d_sfs, bg_p1_sfs, bg_p2_sfs, pop1_size, pop2_size)
     if distributed:
         from sfs2d import dist as D
-        recs = D.scan_records(data, cfg, bg, _scan_local, DEVICE)
+        recs = D.scan_records_split(data, cfg, bg, _split_scan, DEVICE)
     else:
         recs = _scan_local(data, cfg, bg)
     chrom = recs["chrom"].astype(np.int64)

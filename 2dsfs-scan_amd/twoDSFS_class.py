@@ -79,8 +79,11 @@ class LikelihoodInference_jointSFS:
                  distributed=False):
         """The reference's constructor (twoDSFS_class.py:21-33), plus ``device`` (the GPU of this
         process) and ``distributed``: with a torch.distributed process group (one process per GPU),
-        every window scan is sharded by chromosome over the group and every rank returns the whole
-        result (sfs2d.dist.scan_records); all ranks must make the same calls."""
+        every window scan is split over the group at window boundaries balanced by SNPs -- one
+        chromosome spread over several ranks, its background histograms all-reduced -- and every rank
+        returns the whole result (sfs2d.dist.scan_records_split); ``distributed="chromosomes"`` shards
+        whole chromosomes instead (no collective before the scan; sfs2d.dist.scan_records).  All
+        ranks must make the same calls."""
         self.vcf_filename = vcf_filename
         self.popinfo_filename = popinfo_filename
         self.pop1 = pop1
@@ -121,8 +124,14 @@ class LikelihoodInference_jointSFS:
     def _scan(self, p: PackedSNPs, cfg: ScanConfig, bg=None):
         if self.distributed:
             from sfs2d import dist as D
-            return D.scan_records(p, cfg, bg, self._scan_local, self.device)
+            if self.distributed == "chromosomes":
+                return D.scan_records(p, cfg, bg, self._scan_local, self.device)
+            return D.scan_records_split(p, cfg, bg, self._split_scan, self.device)
         return self._scan_local(p, cfg, bg)
+
+    def _split_scan(self, p: PackedSNPs, cfg: ScanConfig, bg=None):
+        from sfs2d.engine import SplitJob
+        return SplitJob(self._engine(), p, cfg, bg)
 
     def _scan_local(self, p: PackedSNPs, cfg: ScanConfig, bg=None):
         eng = self._engine()

@@ -46,15 +46,15 @@ WS = 20000
 def algorithmic_bytes(n_snp, n_slots, n_win, which):
     """Bytes each kernel must move (DESIGN.md "Kernels"), counted from its inputs and outputs.
 
-    k_prep ("k1"): reads counts + positions (8 B/SNP), writes the packed per-SNP bins (4 B/SNP) and
-    the window slot table (8 B/window).  k_scan_w ("k3"): reads the bins (4 B/SNP), the slot record
-    (8 B/slot) and the slot's Fst sums (16 B/slot), writes one 64-B record and one 8-B Fst value
-    per slot.  "pipeline": SURVEY.md 8(d)'s per-unit figure for a whole step -- 8 B/SNP for the scan
-    pass + 4 B/SNP for the background pass over the same stream + 64 B per output window."""
+    k_prep ("k1"): reads counts + positions (8 B/SNP), writes the window slot table (8 B/window) (a
+    counts plan stores no per-SNP bins).  k_scan_w ("k3"): reads the counts (4 B/SNP), the slot
+    record (8 B/slot) and the slot's Fst sums (16 B/slot), writes one 64-B record and one 8-B Fst
+    value per slot.  "pipeline": SURVEY.md 8(d)'s per-unit figure for a whole step -- 8 B/SNP for
+    the scan pass + 4 B/SNP for the background pass over the same stream + 64 B per output window."""
     if which == "k3":
         return 4 * n_snp + (8 + 16 + 64 + 8) * n_slots
     if which == "k1":
-        return 12 * n_snp + 8 * n_win
+        return 8 * n_snp + 8 * n_win
     if which == "pipeline":
         return 12 * n_snp + 64 * n_win
     raise ValueError(which)
@@ -140,8 +140,36 @@ def hbm_stream_roofline(eng, steps=5):
            "pipeline_ms": wall * 1e3,
            "pipeline_bytes_note": "SURVEY 8(d): 12 B/SNP + 64 B/window per run over the wall time of back-to-back runs",
            "windows": nwin, "windows_per_s": nwin / tk,
-           "workload": "config 3 stream on 1 GPU: 32 chrom x 1.5625e6 SNPs, 20 kb, per-chromosome bg"}
+           "workload": "config 3 stream on 1 GPU: 32 chrom x 1.5625e6 SNPs, 20 kb, per-chromosome bg, T2D + T1D + Fst"}
     pl.close()
+    # T2D + T1D (the reference's statistics, no Fst) as independent passes overlapped on 2 HIP streams,
+    # the scan kernel capped at one workgroup per CU so that the next pass's bandwidth-bound k_prep
+    # runs beside the previous pass's compute-bound scan (profiles/r03h_streams_wgs.txt); with Fst,
+    # k_prep is VALU-heavy too and one stream is the fastest
+    import torch
+    streams = [torch.cuda.current_stream().cuda_stream, torch.cuda.Stream().cuda_stream]
+    cfg2 = ScanConfig(n1p=POP, n2p=POP, window=WS, fst=False, scan_wgs_per_cu=1)
+    plans = [eng.plan(dev, cfg2) for _ in range(2)]
+    outs = [torch.zeros((plans[0].nrec, 64), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    ptrs = [o.data_ptr() for o in outs]
+    from sfs2d.engine import Plan
+    Plan.run_streams(plans, streams, 8, ptrs)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    Plan.run_streams(plans, streams, 8 * steps, ptrs)
+    torch.cuda.synchronize()
+    wo = (time.perf_counter() - t0) / (8 * steps)
+    for q in plans:
+        q.check()
+    if not torch.equal(outs[0], outs[1]):
+        raise RuntimeError("config-3 overlapped passes disagree")
+    out["t2d_t1d_overlapped"] = {
+        "pipeline_GBs": bp / wo / 1e9, "pipeline_frac": bp / wo / 1e9 / HBM_PEAK_GBS, "pipeline_ms": wo * 1e3,
+        "windows_per_s": nwin / wo,
+        "note": "T2D + T1D only (the reference's statistics; Hudson Fst not computed): 2 plans on 2 HIP streams, "
+                "passes overlapped, scan kernel capped at 1 workgroup per CU; SURVEY 8(d) bytes over the time per pass"}
+    for q in plans:
+        q.close()
     dev.close()
     return out
 

@@ -168,6 +168,16 @@ int sfs2d_plan_read(sfs2d_plan* plan, sfs2d_window* out_host, int64_t cap, int64
 /* device pointers of the plan's per-chromosome background histogram replicas (uint32), for a
  * multi-GPU all-reduce between sfs2d_plan_run_phase(plan, 1) and (plan, 2). */
 int sfs2d_plan_bg_buffer(sfs2d_plan* plan, void** dev_ptr, int64_t* nbytes);
+/* Multi-GPU split of a chromosome over ranks (sfs2d/dist.py): between sfs2d_plan_run_phase(plan, 1)
+ * (k_prep: this rank's part of every chromosome's background histograms) and (plan, 2) (tables and
+ * scan), every rank reads its partial histograms -- replicas x nchrom x bins uint32 words, laid out
+ * [replica][chromosome][bin] (the consumer sums the replicas), and nchrom uint32 per-chromosome inner
+ * 2D sums (sizes: sfs2d_plan_bg_words) -- sums them over the ranks (the SURVEY 8(e) all-reduce) and
+ * writes the totals back (to_device = 1).  Synchronous.  Replaces the whole-chromosome background
+ * loops of calculate_2d_sfs / calculate_1d_sfs (twoDSFS_class.py:140-232, 398-444) when one
+ * chromosome's SNPs are held by several ranks.  Plans without per-chromosome backgrounds: all 0. */
+int sfs2d_plan_bg_words(const sfs2d_plan* plan, int64_t* replicas, int64_t* nchrom, int64_t* bins);
+int sfs2d_plan_bg_exchange(sfs2d_plan* plan, uint32_t* host_repl, uint32_t* host_sums, int to_device);
 /* Fst of the last run per window slot (NaN: no qualifying SNP / empty slot); plans with SFS2D_F_FST */
 int sfs2d_plan_fst_read(sfs2d_plan* plan, double* out_host, int64_t cap);
 int sfs2d_plan_fst_buffer(sfs2d_plan* plan, void** dev_ptr, int64_t* nslots);

@@ -71,6 +71,7 @@ def snp_records(p, S, ocfg, bg_of_chrom):
     for k, ((c, sp, ep, b, e), o) in enumerate(zip(wins, ref)):
         r = recs[k]
         r["chrom"], r["begin"], r["end"] = c, b, e
+        r["wid"] = (b - int(p.chrom_off[c])) // S          # the window's index in its chromosome
         _fill(r, o, _bgflags(*bg_of_chrom(c), ocfg.n1p, ocfg.n2p))
         recs[k] = r
     return recs

@@ -165,11 +165,84 @@ def check_dist_results(got, golden):
     return n
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_drivers_vs_reference(golden, tmp_path, world):
+@pytest.mark.parametrize("world,mode", [(2, "split"), (3, "split"), (2, "chromosomes")])
+def test_sharded_drivers_vs_reference(golden, tmp_path, world, mode):
     """Every golden driver call (combined_scan, scan_chooseChr, scan_precomputed_BG, both bySNPs
     drivers, T1D_scan / T2D_scan, the sims batch) through the drop-in modules with distributed=True
-    over `world` gloo ranks: shard, per-rank scan (the oracle's records in place of the GPU's),
-    collective error handling, gather, merge, post-pass -- equal to the reference's outputs."""
-    got = run_dist_workers("fake", world, str(tmp_path / "out.json"))
+    over `world` gloo ranks: split at window boundaries (chromosomes cut across ranks, background
+    histograms all-reduced) or sharded by whole chromosomes, per-rank scan (the oracle's records in
+    place of the GPU's), collective error handling, gather, merge, post-pass -- equal to the
+    reference's outputs."""
+    env = {"SFS2D_TEST_DIST": "chromosomes"} if mode == "chromosomes" else None
+    got = run_dist_workers("fake", world, str(tmp_path / "out.json"), env_extra=env)
     assert check_dist_results(got, golden) >= 40
+    st = got["_stats"]
+    if mode == "split":
+        # most calls ran split (the error cases fall back to whole chromosomes), with all-reduces
+        assert st["split"] >= 30 and st["allreduce"] >= 10, st
+        assert st["fallback"] <= 12, st
+
+
+def test_split_error_falls_back_to_whole_chromosomes(tmp_path):
+    """A count error in each rank's part of one chromosome: the error the reference raises (its
+    whole-chromosome 2D background comes first: ValueError) on every rank, via the fallback."""
+    got = run_dist_workers("fake", 2, str(tmp_path / "out.json"), extra=("errors",))
+    for fn in ("combined_scan", "scan_perChr_bySNPs"):
+        assert got[fn]["ref"] == "ValueError"
+        assert not got[fn]["ok"] and got[fn]["error"] == "ValueError", got[fn]
+    assert got["_stats"]["fallback"] == 2, got["_stats"]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_single_chromosome_split_equals_one_rank_cpu(tmp_path, world):
+    got = run_dist_workers("fake", world, str(tmp_path / "out.json"), extra=("single",))
+    check_single(got)
+
+
+def check_single(got):
+    for name in ("bp_perchrom", "bp_perchrom_nofold_filters", "snp_perchrom", "bp_supplied"):
+        assert got[name]["equal"] and got[name]["windows"] > 50, (name, got[name])
+    assert got["_stats"]["split"] == 4 and got["_stats"]["allreduce"] == 3 and got["_stats"]["fallback"] == 0
+
+
+def test_split_points_whole_windows_balanced():
+    from sfs2d.engine import ScanConfig
+    p = synth_genome(3, [4000, 300, 2500], 25, 25, seed=21)
+    for mode, w in ((L.WINDOW_BP, 20000), (L.WINDOW_SNPS, 300)):
+        for pe in (False, True):
+            cfg = ScanConfig(n1p=25, n2p=25, window_mode=mode, window=w, prev_extra=pe)
+            starts = set(D.window_starts(p, cfg).tolist())
+            for world in (1, 2, 3, 4, 7, 64):
+                cuts = D.split_points(p, cfg, world)
+                assert cuts[0] == 0 and cuts[-1] == p.n and len(cuts) == world + 1
+                assert all(a <= b for a, b in zip(cuts, cuts[1:]))
+                assert all(c in starts for c in cuts[1:-1] if c < p.n)
+                if world <= 4:
+                    assert max(b - a for a, b in zip(cuts, cuts[1:])) <= p.n / world + 2 * (w if mode == L.WINDOW_SNPS else 400)
+                if pe:   # the last non-empty rank holds the last two windows
+                    last = max(r for r in range(world) if cuts[r + 1] > cuts[r])
+                    assert cuts[last] <= sorted(starts)[-2]
+
+
+def test_split_merge_equals_single_plan():
+    """Per-part tables (oracle records over each rank's SNP range, backgrounds of the whole
+    chromosomes) merged = one plan's table minus its empty slots."""
+    from sfs2d.engine import ScanConfig
+    p = synth_genome(2, [3000, 2000], 25, 25, seed=8)
+    ocfg = O.Cfg(25, 25)
+    bgs = O.chrom_backgrounds(p, ocfg)
+    for world in (2, 3, 5):
+        cfg = ScanConfig(n1p=25, n2p=25, window=20000, prev_extra=True)
+        cuts = D.split_points(p, cfg, world)
+        last = max(r for r in range(world) if cuts[r + 1] > cuts[r])
+        tabs, c0s = [], []
+        for r in range(world):
+            sub, c0 = p.slice_snps(cuts[r], cuts[r + 1])
+            c0s.append(c0)
+            tabs.append(FR.bp_records(sub, 20000, ocfg, lambda c, c0=c0: bgs[c0 + c], prev_extra=(r == last))
+                        if sub.n else np.zeros(0, dtype=L.WINDOW_DTYPE))
+        merged = D._merge_split(tabs, cuts, c0s, True)
+        full = FR.bp_records(p, 20000, ocfg, lambda c: bgs[c], prev_extra=True)
+        full = full[((full["flags"] & L.W_EMPTY) == 0) | ((full["flags"] & L.W_EXTRA) != 0)]
+        assert _same(merged, full), world
+        assert list(post.combined_scan(merged, p, 20000, post.num_slots(merged))) == list(O.combined_scan(p, 20000, ocfg))
