@@ -190,6 +190,7 @@ struct sfs2d_plan {
   std::vector<sfs2d_plan*> attached;
   uint32_t fst_m = 0;             // attached Fst: base windows per window (their sums add)
   bool fst_win = false;           // Fst by window kernels (fst_windows) instead of k_prep's sums
+  bool fst_scan = false;          // Fst summed by k_scan_w itself (counts plans, small grids): k_prep has no Fst work
   int nfst = 0;                   // k_bg_slice's extra Fst workgroups
 };
 
@@ -249,7 +250,7 @@ int repl_par(const sfs2d_plan* pl) { return pl->fused ? plan_par(pl) : 0; }
 // what the scan kernels stream per SNP: the bins k_prep wrote, or (counts plans) the counts themselves
 const uint32_t* scan_src(const sfs2d_plan* pl) { return pl->cnt ? pl->data->counts : pl->d_bins; }
 
-template <bool P16, bool FUSED, bool FST, bool CNT>
+template <bool P16, bool FUSED, int FST, bool CNT>
 void launch_scan_w(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
   hipExtLaunchKernelGGL((k_scan_w<P16, FUSED, FST, CNT>), dim3((unsigned)pl->chunks.size()), dim3(SBLOCK), pl->scan_lds,
                      CTX_STREAM(pl->ctx), pl->kev[4], pl->kev[5], 0, pl->K, scan_src(pl), pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
@@ -283,6 +284,13 @@ hipError_t launch_scan_c(sfs2d_plan* pl, sfs2d_window* out) {
     if (pl->fst) launch_scan_gw<P16, true, CNT>(pl, out, per_chrom, bp);
     else launch_scan_gw<P16, false, CNT>(pl, out, per_chrom, bp);
   } else if (pl->G == WAVE) {
+    if constexpr (CNT) {
+      if (pl->fst_scan) {
+        if (pl->fused) launch_scan_w<P16, true, 2, CNT>(pl, out, per_chrom, bp);
+        else launch_scan_w<P16, false, 2, CNT>(pl, out, per_chrom, bp);
+        return hipGetLastError();
+      }
+    }
     if (pl->fused) {
       if (pl->fst && !pl->fst_win) launch_scan_w<P16, true, true, CNT>(pl, out, per_chrom, bp);
       else launch_scan_w<P16, true, false, CNT>(pl, out, per_chrom, bp);
@@ -317,7 +325,7 @@ hipError_t launch_prep3(sfs2d_plan* pl) {
 template <bool B, bool S, bool L, bool N, bool F>
 hipError_t launch_prep2(sfs2d_plan* pl) {
   // Fst sums with a plan's pass (the bins pass, or a counts plan's bins-less one); not in sfs2d_bg_hist
-  if (pl->fst && !pl->fst_win && (N || pl->cnt)) return launch_prep3<B, S, L, N, F, true>(pl);
+  if (pl->fst && !pl->fst_win && !pl->fst_scan && (N || pl->cnt)) return launch_prep3<B, S, L, N, F, true>(pl);
   return launch_prep3<B, S, L, N, F, false>(pl);
 }
 
@@ -331,7 +339,7 @@ hipError_t launch_prep1(sfs2d_plan* pl) {
 // supplied background, SNP-count windows, no Fst sums)
 hipError_t launch_prep_cnt(sfs2d_plan* pl) {
   const bool L = pl->lds_hist;
-  const bool fs = pl->fst && !pl->fst_win;
+  const bool fs = pl->fst && !pl->fst_win && !pl->fst_scan;
   if (pl->do_bg && pl->do_seg)
     return L ? launch_prep1<true, true, true, false>(pl) : launch_prep1<true, true, false, false>(pl);
   if (pl->do_bg) return L ? launch_prep1<true, false, true, false>(pl) : launch_prep1<true, false, false, false>(pl);
@@ -342,7 +350,7 @@ hipError_t launch_prep_cnt(sfs2d_plan* pl) {
 
 // whether a plan run launches k_prep at all
 bool prep_runs(const sfs2d_plan* pl) {
-  return !pl->tiles.empty() && (!pl->cnt || pl->do_bg || pl->do_seg || (pl->fst && !pl->fst_win));
+  return !pl->tiles.empty() && (!pl->cnt || pl->do_bg || pl->do_seg || (pl->fst && !pl->fst_win && !pl->fst_scan));
 }
 
 hipError_t launch_prep(sfs2d_plan* pl, bool bins) {
@@ -831,9 +839,27 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   pl->fused = small && !pl->sliced;
   // Fst of sliced fixed-bp plans: by extra k_bg_slice workgroups (the GPU is mostly idle during
   // that latency-bound kernel) instead of k_prep's per-SNP sums (config 2: k_prep -3 us)
-  pl->fst_win = pl->sliced && bp && (prm->flags & SFS2D_F_FST);
-  pl->nfst = pl->fst_win ? (int)std::min<int64_t>(1024, std::max<int64_t>(1, (pl->nslots + 7) / 8)) : 0;   // ~1 window per wave
   pl->fst = (prm->flags & SFS2D_F_FST) != 0;
+  // Fst of counts plans on the small-grid path is summed by k_scan_w over the rows it streams
+  // (fst_scan): k_prep then has no Fst work and stays bandwidth-bound (config 3: 147 -> 83 us) while
+  // the scan, bound by its LDS pipe and VALU issue, grows (143 -> 210 us; an LDS copy of the
+  // reciprocal table: 262 us).  One pass alone is ~2% slower than with k_prep's sums, but passes
+  // overlapped on streams gain (config 2, 3 streams: 14.0 -> 12.8 us per pass; config 3, 2 streams
+  // capped at 1 scan workgroup per CU: 293 -> 281 us), and an attached plan can then have Fst on any
+  // window (profiles/r03k_fst_scan.txt).  SFS2D_FST_SCAN=0: k_prep's fixed-point sums / k_bg_slice's
+  // Fst workgroups instead (attached Fst then needs fixed-bp windows the base's divide)
+  pl->fst_scan = false;
+  if (pl->fst && pl->cnt && pl->G == WAVE && !pl->gw) {
+    const char* ev = std::getenv("SFS2D_FST_SCAN");
+    pl->fst_scan = !(ev && ev[0] == '0');
+    if (pl->fst_scan) {   // its variant's static LDS must fit beside the dynamic
+      hipFuncAttributes fa{};
+      const void* f = pl->p16 ? (const void*)k_scan_w<true, true, 2, true> : (const void*)k_scan_w<false, true, 2, true>;
+      if (hipFuncGetAttributes(&fa, f) != hipSuccess || pl->scan_lds + fa.sharedSizeBytes > 160 * 1024) pl->fst_scan = false;
+    }
+  }
+  pl->fst_win = pl->sliced && bp && pl->fst && !pl->fst_scan;
+  pl->nfst = pl->fst_win ? (int)std::min<int64_t>(1024, std::max<int64_t>(1, (pl->nslots + 7) / 8)) : 0;   // ~1 window per wave
   if (pl->scan_lds > 64 * 1024) {
     const int lds = (int)pl->scan_lds;
     const hipFuncAttribute A = hipFuncAttributeMaxDynamicSharedMemorySize;
@@ -845,6 +871,8 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
                           (const void*)k_scan_w<true, false, false, true>, (const void*)k_scan_w<false, false, false, true>,
                           (const void*)k_scan_w<true, true, true, true>, (const void*)k_scan_w<false, true, true, true>,
                           (const void*)k_scan_w<true, false, true, true>, (const void*)k_scan_w<false, false, true, true>,
+                          (const void*)k_scan_w<true, true, 2, true>, (const void*)k_scan_w<false, true, 2, true>,
+                          (const void*)k_scan_w<true, false, 2, true>, (const void*)k_scan_w<false, false, 2, true>,
                           (const void*)k_scan_g<true, false, false>, (const void*)k_scan_g<false, false, false>,
                           (const void*)k_scan_g<true, true, false>, (const void*)k_scan_g<false, true, false>,
                           (const void*)k_scan_g<true, false, true>, (const void*)k_scan_g<false, false, true>,
@@ -869,6 +897,12 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
     if (pl->gw)
       oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<true, true, true>, WAVE, pl->scan_lds)
                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<false, true, true>, WAVE, pl->scan_lds);
+    else if (pl->fst_scan && pl->fused)
+      oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<true, true, 2, true>, SBLOCK, pl->scan_lds)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<false, true, 2, true>, SBLOCK, pl->scan_lds);
+    else if (pl->fst_scan)
+      oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<true, false, 2, true>, SBLOCK, pl->scan_lds)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<false, false, 2, true>, SBLOCK, pl->scan_lds);
     else if (pl->fused)
       oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<true, true, true, true>, SBLOCK, pl->scan_lds)
                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<false, true, true, true>, SBLOCK, pl->scan_lds);
@@ -962,7 +996,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
     // the LDS histogram must fit beside the static LDS of the k_prep variant that will run: the Fst
     // variant (Fst not taken from k_bg_slice) holds ~20 KB of window sums and reciprocals, so e.g.
     // pop_size 95 / 95 (148 KB of histogram) takes the global-atomic histogram with Fst
-    const bool kfst = (prm->flags & SFS2D_F_FST) && !pl->fst_win;
+    const bool kfst = (prm->flags & SFS2D_F_FST) && !pl->fst_win && !pl->fst_scan;
     hipFuncAttributes fa{};
     const hipError_t ae = kfst ? hipFuncGetAttributes(&fa, (const void*)k_prep<true, true, true, true, false, true>)
                                : hipFuncGetAttributes(&fa, (const void*)k_prep<true, true, true, true, false, false>);
@@ -1421,23 +1455,24 @@ int sfs2d_plan_attach(sfs2d_plan* base, const sfs2d_params* prm, sfs2d_plan** ou
       (prm->has_start && prm->start_pos != b.start_pos) || (prm->has_end && prm->end_pos != b.end_pos))
     return set_err(ctx, SFS2D_E_ARG, "an attached plan may differ from its base only in the window and flags");
   const bool bp = prm->window_mode == SFS2D_WINDOW_BP;
-  uint32_t m = 0;
-  if (prm->flags & SFS2D_F_FST) {
-    const bool base_bp = b.window_mode == SFS2D_WINDOW_BP;
-    if (!bp)
-      return set_err(ctx, SFS2D_E_ARG, "attached Fst needs fixed-bp windows");
-    if (!base->sliced) {   // fused bases: the base's k_prep sums, added per attached window
-      if (!(b.flags & SFS2D_F_FST) || !base_bp || prm->window % b.window != 0)
-        return set_err(ctx, SFS2D_E_ARG, "attached Fst needs a fixed-bp Fst base plan whose window divides this one's");
-      m = (uint32_t)(prm->window / b.window);
-    }
-  }
   sfs2d_plan* a = nullptr;
   int rc = plan_create(ctx, base->data, prm, base->sliced ? 1 : 0, &a);
   if (rc) return rc;
   if (a->fused != base->fused || a->sliced != base->sliced || a->G != base->G || a->cnt != base->cnt) {
     plan_free(a); delete a;
     return set_err(ctx, SFS2D_E_ARG, "attached plan would take a different kernel path than its base");
+  }
+  // Fst of an attached plan: its own scan's sums (fst_scan), else the base's k_prep sums added per
+  // attached window (fused bases) or k_fst_win on the attached slots (sliced bases)
+  uint32_t m = 0;
+  if ((prm->flags & SFS2D_F_FST) && !a->fst_scan) {
+    const bool base_bp = b.window_mode == SFS2D_WINDOW_BP;
+    const char* why = nullptr;
+    if (!bp) why = "attached Fst needs fixed-bp windows";
+    else if (!base->sliced && (!(b.flags & SFS2D_F_FST) || base->fst_scan || !base_bp || prm->window % b.window != 0))
+      why = "attached Fst needs a fixed-bp Fst base plan whose window divides this one's";
+    if (why) { plan_free(a); delete a; return set_err(ctx, SFS2D_E_ARG, why); }
+    if (!base->sliced) m = (uint32_t)(prm->window / b.window);
   }
   HIPCHK(ctx, hipSetDevice(ctx->device));
   hipFree(a->d_bins); hipFree(a->d_repl); hipFree(a->d_bcount);
@@ -1459,7 +1494,7 @@ int sfs2d_plan_attach(sfs2d_plan* base, const sfs2d_params* prm, sfs2d_plan** ou
   }
   a->base = base;
   a->fst_m = m;
-  a->fst_win = base->sliced && (prm->flags & SFS2D_F_FST);   // k_fst_win on the attached slots
+  a->fst_win = base->sliced && (prm->flags & SFS2D_F_FST) && !a->fst_scan;   // k_fst_win on the attached slots
   a->nfst = 0;
   rc = 0;
   std::vector<uint32_t> sb(a->slot_base_h.begin(), a->slot_base_h.end());

@@ -2155,14 +2155,20 @@ __device__ __forceinline__ void lds_copy_d(double* dst, const double* __restrict
 // batch of windows at once (flush), the rare exact re-evaluations included.  (Measured on config 3:
 // the loop is VALU-issue and LDS-latency bound at 4 waves per SIMD; the batched finish took it from
 // 405 to ~330 VALU instructions per window.)
-template <bool P16, bool FUSED, bool FST, bool CNT>
+// FST: 0 no Fst; 1 k_prep's fixed-point sums of the slot, read and cleared; 2 (counts plans) Hudson's
+// terms summed here, per SNP of the rows the window streams anyway (fst_snp on the counts in registers,
+// membership = an inner 2D bin; the unfolded last bin in the rare pass), fp64 lane sums in a fixed order
+// and two wave sums per window: k_prep then runs without the Fst work (DESIGN.md "Fst placement")
+template <bool P16, bool FUSED, int FST, bool CNT>
 __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
+  constexpr bool FSTIN = FST == 2;
+  static_assert(!FSTIN || CNT, "Fst in the scan reads the counts");
   constexpr int NWV = SBLOCK / WAVE;
   constexpr int SB = 4;    // windows per batch (see flush; LDS-limited)
   __shared__ BgHead sh_hb;
   __shared__ double sh_bd[NWV][3][SB];      // batch: the three sums of window j
   __shared__ uint32_t sh_bu[NWV][5][SB];    // batch: slot, begin, n2 | n2_all, n1a | n1b, nsnp | nvar
-  __shared__ unsigned long long sh_bf[NWV][FST ? 2 : 1][SB];   // batch (FST): k_prep's Fst sums of the slot
+  __shared__ unsigned long long sh_bf[NWV][FST ? 2 : 1][SB];   // batch (FST): the slot's Fst sums (FST 2: fp64 bits)
   STAMP(10);
   BLK_STAMP(1, 0);
   const int tid = threadIdx.x;
@@ -2170,6 +2176,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   const int lane = tid & (WAVE - 1);
   const Chunk ch = chunks[blockIdx.x];
   const int bg = bg_per_chrom ? (int)ch.chrom : 0;
+  const double2* rtg = reinterpret_cast<const double2*>(dfg + 2 * LNT);   // FSTIN: (1/n, 1/(n(n-1))) (k_init_lnx)
 
   // LDS: lp table (nt, rounded up to even: the histograms are 16-B aligned) | D | F | histograms
   double* LPl = ldsd;
@@ -2344,7 +2351,11 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     if (mine && !exact)
       write_rec(out + Bs, ch.chrom, wid, empty ? 0u : Bsb, empty ? 0u : Bse, w, empty ? SFS2D_W_EMPTY : zflags);
     if (mine) {
-      if (FST) {   // k_prep's fixed-point sums of the slot (read in the window), cleared for the next run
+      if (FSTIN) {   // the window's own sums
+        const double fx = __longlong_as_double((long long)sh_bf[wv][0][jl]);
+        const double fy = __longlong_as_double((long long)sh_bf[wv][FST ? 1 : 0][jl]);
+        fst_out[Bs] = fy != 0.0 ? fx / fy : __builtin_nan("");
+      } else if (FST) {   // k_prep's fixed-point sums of the slot (read in the window), cleared for the next run
         const long long fx = (long long)sh_bf[wv][0][jl], fy = (long long)sh_bf[wv][FST ? 1 : 0][jl];
         fst_out[Bs] = fy != 0 ? (double)fx / (double)fy : __builtin_nan("");
         reinterpret_cast<ulonglong2*>(fsum)[Bs] = make_ulonglong2(0ull, 0ull);
@@ -2437,6 +2448,11 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     const int lim = (int)nsnp - lane;
     const bool clampd = nsnp > (uint32_t)(LNT - 1);   // some rank may pass the D table
     double acc2 = 0.0;
+    // FSTIN: this lane's sums of A1 + A2, p1 + p2 and p1 p2 (fst_snp's num = A1 + A2 - 2 p1 p2,
+    // den = p1 + p2 - 2 p1 p2, summed per part).  Every SNP takes part: those outside the 2D SFS --
+    // bin (0,0) or, folded, both populations fixed for the alternative allele, and the unfolded last
+    // bin -- have num = den = 0, as have SNPs with fewer than 2 called alleles (table entries 0)
+    double fA = 0.0, fP = 0.0, fM = 0.0;
     uint32_t n2 = 0, n1a = 0, n1b = 0, nlast = 0, nvar = 0;
     uint32_t kw[8];   // the 2D words of the first 8 rows, cleared after the window
     auto pair = [&](uint32_t w0, uint32_t w1, int j, bool keep) {
@@ -2467,6 +2483,17 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
         const uint32_t u1 = g1 ? a1b + g1 * (4u * R1) : atr, u2 = g2 ? a2b + g2 * (4u * R1) : atr;
         __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u1, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u2, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (FSTIN) {   // (SNPs past e: counts 0, no called allele, terms 0)
+          const uint32_t a1 = __builtin_amdgcn_ubfe(w, 8, 8), a2 = w >> 24;
+          // (1/n, 1/(n(n-1))) from the global table (L1-resident; an LDS copy measured slower: the
+          // loop's LDS pipe is its bottleneck, profiles/r03k_fst_scan.txt)
+          const double2 q1 = rtg[__builtin_amdgcn_udot4(w, 0x0101u, 0u, false)];        // n1 = r1 + a1
+          const double2 q2 = rtg[__builtin_amdgcn_udot4(w, 0x01010000u, 0u, false)];    // n2 = r2 + a2
+          const double p1 = (double)a1 * q1.x, p2 = (double)a2 * q2.x;
+          fA += fma((double)__umul24(a1, a1 - 1u), q1.y, (double)__umul24(a2, a2 - 1u) * q2.y);
+          fP += p1 + p2;
+          fM = fma(p1, p2, fM);
+        }
       }
       // the ranks once both SNPs' atomics are issued (extracted right after its own atomic, each rank's
       // wait held the other SNP's work back: two LDS round trips per pair instead of one)
@@ -2510,7 +2537,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     }
     if (!filt) nvar = nsnp;
     ulonglong2 fq = make_ulonglong2(0ull, 0ull);   // this window's Fst sums (k_prep): their latency under the window
-    if (FST && lane == 0) fq = reinterpret_cast<const ulonglong2*>(fsum)[s];
+    if (FST == 1 && lane == 0) fq = reinterpret_cast<const ulonglong2*>(fsum)[s];
     if (it == 0) STAMP(12);
     MARK(23);
     group_sync<WAVE>();
@@ -2587,6 +2614,11 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       sa = wave_sum_all(acca);
       sb = wave_sum_all(accb);
     }
+    if (FSTIN) {
+      const double m2 = 2.0 * fM;
+      fq = make_ulonglong2((unsigned long long)__double_as_longlong(wave_sum_all(fA - m2)),
+                           (unsigned long long)__double_as_longlong(wave_sum_all(fP - m2)));
+    }
     MARK(26);
     put(s, cur.b, nsnp, n2, n1a, n1b, nvar, nlast, s2, sa, sb, fq);
     ++jb;
@@ -2611,7 +2643,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
 }
 
 // CNT: `bins` is the counts array (counts plans): every scan classifies the counts it streams
-template <bool P16, bool FUSED, bool FST, bool CNT>
+template <bool P16, bool FUSED, int FST, bool CNT>
 __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_scan_w(SCAN_W_ARGS) {
   extern __shared__ double ldsd[];
   scan_w_small<P16, FUSED, FST, CNT>(ldsd, SCAN_W_PASS);

@@ -87,11 +87,42 @@ def test_repeated_runs_identical():
             base.check()
             outs.append([pl.read().tobytes() for pl in (base, a1, a2)] + [a1.read_fst().tobytes()])
         assert outs[0] == outs[1] == outs[2]
-        with pytest.raises(Exception):   # Fst on SNP-count windows
-            base.attach(ScanConfig(n1p=25, n2p=25, window_mode=L.WINDOW_SNPS, window=300, fst=True))
+        # Fst on SNP-count windows: a counts plan's scan sums its own Fst (fst_scan)
+        a3 = base.attach(ScanConfig(n1p=25, n2p=25, window_mode=L.WINDOW_SNPS, window=300, fst=True))
+        base.run()
+        base.check()
+        f3, r3 = a3.read_fst(), a3.read()
+        from oracle import sfs_oracle as O
+        wins = O.snp_windows(p, 300)[0]
+        assert len(wins) == len(r3) and list(r3["begin"]) == [w[3] for w in wins]
+        for (c, sp, ep, b, e), f in zip(wins, f3):
+            v = O.window_fst(p, np.arange(b, e), O.Cfg(25, 25))
+            assert (v is None and np.isnan(f)) or abs(f - v) <= 1e-10 * max(1.0, abs(v)), (b, f, v)
         with pytest.raises(Exception):   # a different grid
             base.attach(ScanConfig(n1p=20, n2p=25, window=500000))
         base.close()
         assert not a1.h and not a2.h
+    finally:
+        dev.close()
+
+
+def test_attach_fst_without_fst_scan(monkeypatch):
+    """SFS2D_FST_SCAN=0 (Fst from k_prep's sums or k_fst_win): attached Fst needs fixed-bp windows."""
+    from sfs2d import _lib as L
+    from sfs2d.engine import Engine, ScanConfig
+    from sfs2d.synth import synth_genome
+    monkeypatch.setenv("SFS2D_FST_SCAN", "0")
+    p = synth_genome(2, [30000, 12000], 25, 25, seed=7)
+    eng = Engine.get(0)
+    dev = eng.upload(p)
+    try:
+        base = eng.plan(dev, ScanConfig(n1p=25, n2p=25, window=20000, prev_extra=True, fst=True))
+        with pytest.raises(Exception):
+            base.attach(ScanConfig(n1p=25, n2p=25, window_mode=L.WINDOW_SNPS, window=300, fst=True))
+        a = base.attach(ScanConfig(n1p=25, n2p=25, window=100000, fst=True))
+        base.run()
+        base.check()
+        assert np.isfinite(a.read_fst()).any()
+        base.close()
     finally:
         dev.close()
