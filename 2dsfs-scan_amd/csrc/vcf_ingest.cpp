@@ -17,7 +17,6 @@
 // Errors stop at the first offending line in file order, as the reference's exception would.
 #include <zlib.h>
 
-#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <climits>
@@ -547,62 +546,89 @@ int sfs2d_vcf_read(const char* vcf_path, const char* popmap_path, int nthreads, 
     }
     const auto t2 = Clock::now();
 
-    // dict merge in file order
+    // dict merge in file order: a key's slot is its first record's place, its values the last
+    // record's.  Keys are sharded by hash over T threads; each thread walks every record in file
+    // order, keeps those of its shard in an open-addressing table of its own and marks, per record,
+    // whether it is its key's first and (first records) where the key's last values are: disjoint
+    // writes, no locks.  A prefix over the first-record flags (file order) then numbers the slots.
     int64_t total = 0;
-    for (auto& p : parts) total += (int64_t)p.hash.size();
-    size_t cap = 16;
-    while (cap < (size_t)total * 2) cap <<= 1;
-    std::vector<int64_t> table(cap, -1);        // slot id per bucket
-    std::vector<int32_t> src_part;              // per slot: where its current values come from
-    std::vector<int64_t> src_rec;
-    std::vector<int32_t> first_part;            // per slot: the first record (its key text)
-    std::vector<int64_t> first_rec;
-    src_part.reserve(total); src_rec.reserve(total); first_part.reserve(total); first_rec.reserve(total);
-    for (size_t pi = 0; pi < parts.size(); ++pi) {
-      const Part& p = parts[pi];
-      for (size_t r = 0; r < p.hash.size(); ++r) {
-        const uint64_t h = p.hash[r];
-        const char* k = p.keys.data() + p.key_off[r];
-        const size_t kl = (size_t)(p.key_off[r + 1] - p.key_off[r]);
-        size_t b = h & (cap - 1);
-        for (;;) {
-          const int64_t s = table[b];
-          if (s < 0) {
-            table[b] = (int64_t)src_part.size();
-            src_part.push_back((int32_t)pi); src_rec.push_back((int64_t)r);
-            first_part.push_back((int32_t)pi); first_rec.push_back((int64_t)r);
-            break;
+    std::vector<int64_t> base(parts.size() + 1, 0);
+    for (size_t pi = 0; pi < parts.size(); ++pi) base[pi + 1] = base[pi] + (int64_t)parts[pi].hash.size();
+    total = base.back();
+    auto rec_id = [](size_t pi, int64_t r) { return ((int64_t)pi << 40) | r; };   // (part, record)
+    std::vector<uint8_t> is_first((size_t)total, 0);
+    std::vector<int64_t> last_of((size_t)total, -1);   // first records: (part, record) of the key's last record
+    {
+      const int S = std::max(1, std::min<int>(T, (int)std::max<int64_t>(1, total / 65536)));
+      auto shard = [&](int t) {
+        size_t cap = 16;
+        while (cap < (size_t)(total / S + 1) * 2) cap <<= 1;
+        std::vector<int64_t> table(cap, -1);   // bucket -> (part, record) of the key's first record
+        for (size_t pi = 0; pi < parts.size(); ++pi) {
+          const Part& p = parts[pi];
+          for (size_t r = 0; r < p.hash.size(); ++r) {
+            const uint64_t h = p.hash[r];
+            if ((int)((h >> 40) % (uint64_t)S) != t) continue;
+            const char* k = p.keys.data() + p.key_off[r];
+            const size_t kl = (size_t)(p.key_off[r + 1] - p.key_off[r]);
+            size_t bk = h & (cap - 1);
+            for (;;) {
+              const int64_t g = table[bk];
+              if (g < 0) {
+                const int64_t gi = base[pi] + (int64_t)r;
+                table[bk] = rec_id(pi, (int64_t)r);
+                is_first[(size_t)gi] = 1;
+                last_of[(size_t)gi] = rec_id(pi, (int64_t)r);
+                break;
+              }
+              const size_t qp = (size_t)(g >> 40);
+              const Part& q = parts[qp];
+              const int64_t fr = g & ((int64_t(1) << 40) - 1);
+              const size_t ql = (size_t)(q.key_off[fr + 1] - q.key_off[fr]);
+              if (q.hash[fr] == h && ql == kl && std::memcmp(q.keys.data() + q.key_off[fr], k, kl) == 0) {
+                last_of[(size_t)(base[qp] + fr)] = rec_id(pi, (int64_t)r);   // dict assignment: values replaced
+                break;
+              }
+              bk = (bk + 1) & (cap - 1);
+            }
           }
-          const Part& q = parts[first_part[s]];
-          const int64_t fr = first_rec[s];
-          const size_t ql = (size_t)(q.key_off[fr + 1] - q.key_off[fr]);
-          if (q.hash[fr] == h && ql == kl && std::memcmp(q.keys.data() + q.key_off[fr], k, kl) == 0) {
-            src_part[s] = (int32_t)pi; src_rec[s] = (int64_t)r;   // dict assignment: values replaced
-            break;
-          }
-          b = (b + 1) & (cap - 1);
         }
-      }
+      };
+      std::vector<std::thread> th;
+      for (int t = 1; t < S; ++t) th.emplace_back(shard, t);
+      shard(0);
+      for (auto& x : th) x.join();
     }
+    std::vector<int64_t> first_id, src_id;   // per slot: (part, record) of its first / last record
+    first_id.reserve((size_t)total);
+    src_id.reserve((size_t)total);
+    for (size_t pi = 0; pi < parts.size(); ++pi)
+      for (int64_t r = 0; r < (int64_t)parts[pi].hash.size(); ++r)
+        if (is_first[(size_t)(base[pi] + r)]) {
+          first_id.push_back(rec_id(pi, r));
+          src_id.push_back(last_of[(size_t)(base[pi] + r)]);
+        }
+    std::vector<uint8_t>().swap(is_first);
+    std::vector<int64_t>().swap(last_of);
+    auto part_of = [](int64_t id) { return (size_t)(id >> 40); };
+    auto rec_of = [](int64_t id) { return id & ((int64_t(1) << 40) - 1); };
     auto* v = new sfs2d_vcf();
-    const int64_t n = (int64_t)src_part.size();
+    const int64_t n = (int64_t)first_id.size();
     v->n = n;
     v->pops = pops;
     const int P = C.P;
     v->chrom.resize(n); v->ann.resize(n); v->pos.resize(n); v->pos_off.resize(n + 1);
     v->alleles.resize(2 * n); v->calls.resize((size_t)n * 2 * P);
+    // chromosome and annotation ids in first-appearance order over the slots (sequential; the runs of
+    // one chromosome compare a string view), positions' text offsets (a prefix)
     std::unordered_map<std::string, int32_t> cix, aix;
     std::vector<std::vector<int32_t>> amap(parts.size());
-    for (size_t pi = 0; pi < parts.size(); ++pi) {
-      amap[pi].resize(parts[pi].ann_names.size(), -1);
-    }
+    for (size_t pi = 0; pi < parts.size(); ++pi) amap[pi].resize(parts[pi].ann_names.size(), -1);
     v->pos_off[0] = 0;
-    v->pos_blob.reserve((size_t)n * 8);
     int32_t last_cid = -1;
     for (int64_t s = 0; s < n; ++s) {
-      // key text (chrom, POS) from the first record; values from the last
-      const Part& f = parts[first_part[s]];
-      const int64_t fr = first_rec[s];
+      const Part& f = parts[part_of(first_id[s])];
+      const int64_t fr = rec_of(first_id[s]);
       const char* k = f.keys.data() + f.key_off[fr];
       const size_t kl = (size_t)(f.key_off[fr + 1] - f.key_off[fr]);
       const uint32_t cl = f.chrom_len[fr];
@@ -623,22 +649,12 @@ int sfs2d_vcf_read(const char* vcf_path, const char* popmap_path, int nthreads, 
         last_cid = cid;
       }
       v->chrom[s] = cid;
-      const char* ps = cl == UINT32_MAX ? k + kl : k + cl + 1;
-      const size_t pl = cl == UINT32_MAX ? 0 : kl - cl - 1;
-      v->pos_blob.append(ps, pl);
-      v->pos_off[s + 1] = (int64_t)v->pos_blob.size();
-      int64_t x = 0;
-      bool okp = pl > 0 && pl <= 18;
-      for (size_t i = 0; okp && i < pl; ++i) {
-        if (ps[i] < '0' || ps[i] > '9') okp = false;
-        else x = x * 10 + (ps[i] - '0');
-      }
-      v->pos[s] = okp ? x : INT64_MIN;
-      const Part& p = parts[src_part[s]];
-      const int64_t r = src_rec[s];
-      int32_t& am = amap[src_part[s]][p.ann[r]];
+      v->pos_off[s + 1] = v->pos_off[s] + (int64_t)(cl == UINT32_MAX ? 0 : kl - cl - 1);
+      const size_t sp = part_of(src_id[s]);
+      const Part& p = parts[sp];
+      int32_t& am = amap[sp][p.ann[rec_of(src_id[s])]];
       if (am < 0) {
-        const std::string& an = p.ann_names[p.ann[r]];
+        const std::string& an = p.ann_names[p.ann[rec_of(src_id[s])]];
         auto at = aix.find(an);
         if (at == aix.end()) {
           am = (int32_t)v->anns.size();
@@ -649,9 +665,40 @@ int sfs2d_vcf_read(const char* vcf_path, const char* popmap_path, int nthreads, 
         }
       }
       v->ann[s] = am;
-      v->alleles[2 * s] = p.alle[2 * r];
-      v->alleles[2 * s + 1] = p.alle[2 * r + 1];
-      std::memcpy(&v->calls[(size_t)s * 2 * P], &p.calls[(size_t)r * 2 * P], sizeof(int32_t) * 2 * P);
+    }
+    // the rest per slot, in parallel: position text and value, alleles, calls
+    v->pos_blob.resize((size_t)v->pos_off[n]);
+    {
+      const int W = std::max(1, std::min<int>(T, (int)std::max<int64_t>(1, n / 16384)));
+      auto fill = [&](int t) {
+        const int64_t lo = n * t / W, hi = n * (t + 1) / W;
+        for (int64_t s = lo; s < hi; ++s) {
+          const Part& f = parts[part_of(first_id[s])];
+          const int64_t fr = rec_of(first_id[s]);
+          const char* k = f.keys.data() + f.key_off[fr];
+          const size_t kl = (size_t)(f.key_off[fr + 1] - f.key_off[fr]);
+          const uint32_t cl = f.chrom_len[fr];
+          const char* ps = cl == UINT32_MAX ? k + kl : k + cl + 1;
+          const size_t pl = (size_t)(v->pos_off[s + 1] - v->pos_off[s]);
+          if (pl) std::memcpy(&v->pos_blob[(size_t)v->pos_off[s]], ps, pl);
+          int64_t x = 0;
+          bool okp = pl > 0 && pl <= 18;
+          for (size_t i = 0; okp && i < pl; ++i) {
+            if (ps[i] < '0' || ps[i] > '9') okp = false;
+            else x = x * 10 + (ps[i] - '0');
+          }
+          v->pos[s] = okp ? x : INT64_MIN;
+          const Part& p = parts[part_of(src_id[s])];
+          const int64_t r = rec_of(src_id[s]);
+          v->alleles[2 * s] = p.alle[2 * r];
+          v->alleles[2 * s + 1] = p.alle[2 * r + 1];
+          std::memcpy(&v->calls[(size_t)s * 2 * P], &p.calls[(size_t)r * 2 * P], sizeof(int32_t) * 2 * P);
+        }
+      };
+      std::vector<std::thread> th;
+      for (int t = 1; t < W; ++t) th.emplace_back(fill, t);
+      fill(0);
+      for (auto& x : th) x.join();
     }
     v->text_bytes = (int64_t)C.n;
     for (auto& p : parts) v->lines += p.lines;

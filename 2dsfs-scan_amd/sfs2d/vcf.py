@@ -18,7 +18,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 from dataclasses import dataclass
-from typing import List
+from typing import List, Sequence
 
 import numpy as np
 
@@ -69,6 +69,38 @@ def _view(ptr, dtype, count):
         return np.zeros(0, dtype)
     buf = (C.c_char * (count * np.dtype(dtype).itemsize)).from_address(ptr)
     return np.frombuffer(buf, dtype=dtype).copy()
+
+
+class _PosTexts(Sequence):
+    """POS texts of the records, decoded from the library's blob on first use (the packed path reads
+    only the numeric positions, so a million-record ingest builds no per-record strings)."""
+
+    def __init__(self, blob: bytes, pos_off: np.ndarray):
+        self._blob, self._off, self._list = blob, pos_off, None
+
+    def _all(self) -> List[str]:
+        if self._list is None:
+            text = self._blob.decode("utf-8", "surrogateescape")
+            po = self._off.tolist()
+            if len(text) == len(self._blob):   # ASCII: character offsets are byte offsets
+                self._list = [text[po[i]:po[i + 1]] for i in range(len(po) - 1)]
+            else:
+                self._list = [self._blob[po[i]:po[i + 1]].decode("utf-8", "surrogateescape") for i in range(len(po) - 1)]
+        return self._list
+
+    def __len__(self):
+        return len(self._off) - 1
+
+    def __getitem__(self, i):
+        if self._list is None and isinstance(i, int):
+            k = i + len(self) if i < 0 else i
+            if not 0 <= k < len(self):
+                raise IndexError(i)
+            return self._blob[int(self._off[k]):int(self._off[k + 1])].decode("utf-8", "surrogateescape")
+        return self._all()[i]
+
+    def __iter__(self):
+        return iter(self._all())
 
 
 @dataclass
@@ -179,13 +211,7 @@ def read_vcf(vcf_filename, popinfo_filename, nthreads: int = 0) -> VcfTable:
         pos = _view(ptrs[1].value, np.int64, n)
         pos_off = _view(ptrs[3].value, np.int64, n + 1)
         blob = C.string_at(ptrs[2].value, int(pos_off[-1])) if n and pos_off[-1] else b""
-        pos_text = blob.decode("utf-8", "surrogateescape")
-        if len(pos_text) == len(blob):   # ASCII: character offsets are byte offsets
-            po = pos_off.tolist()
-            texts = [pos_text[po[i]:po[i + 1]] for i in range(n)]
-        else:
-            po = pos_off.tolist()
-            texts = [blob[po[i]:po[i + 1]].decode("utf-8", "surrogateescape") for i in range(n)]
+        texts = _PosTexts(blob, pos_off)
         ann = _view(ptrs[4].value, np.int32, n)
         alle = _view(ptrs[5].value, np.uint8, 2 * n).reshape(n, 2)
         calls = _view(ptrs[6].value, np.int32, n * P * 2).reshape(n, P, 2)
