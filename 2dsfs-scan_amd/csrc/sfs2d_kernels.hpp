@@ -2177,6 +2177,9 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   const Chunk ch = chunks[blockIdx.x];
   const int bg = bg_per_chrom ? (int)ch.chrom : 0;
   const double2* rtg = reinterpret_cast<const double2*>(dfg + 2 * LNT);   // FSTIN: (1/n, 1/(n(n-1))) (k_init_lnx)
+  // CNT: the counts as a buffer resource of n words (loads past n return 0; n < 2^30, plan_create)
+  const __amdgpu_buffer_rsrc_t crs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bins), (short)0, (int)((P.nm1 + 1u) * 4u), 0x00020000);
 
   // LDS: lp table (nt, rounded up to even: the histograms are 16-B aligned) | D | F | histograms
   double* LPl = ldsd;
@@ -2205,9 +2208,11 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       // (uniform base + a 32-bit lane offset: no per-lane 64-bit pointer stays live, which the exact
       // path's registers pushed to scratch -- 512 B of stores per wavefront)
       const uint32_t* q = bins + w.b;
-      if (CNT) {   // counts: no padding past n, the row loads are clamped to the last SNP (masked later)
+      if (CNT) {   // counts, no padding past n: buffer loads, range-checked (0 past n; masked later),
+                   // one lane offset and the rows in the instruction's immediate offset
+        const int vo = (int)((w.b + (uint32_t)lane) * 4u);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) w.u[j] = bins[min(w.b + (uint32_t)lane + 64u * j, P.nm1)];
+        for (int j = 0; j < 8; ++j) w.u[j] = __builtin_amdgcn_raw_buffer_load_b32(crs, vo + 256 * j, 0, 0);
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) w.u[j] = q[(uint32_t)lane + 64u * j];
@@ -2519,12 +2524,24 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       const uint32_t* qb = bins + cur.b;
       uint32_t ln = (uint32_t)lane;
       asm volatile("" : "+v"(ln));   // (else bins + lane is hoisted out of the window loop and spilled)
-      uint32_t x0 = 64 * 8 < lim ? qb[ln + 64 * 8] : 0u, x1 = 64 * 9 < lim ? qb[ln + 64 * 9] : 0u;
-      for (int j = 8; 64 * j < (int)nsnp; j += 2) {
-        const uint32_t w0 = x0, w1 = x1;
-        x0 = 64 * (j + 2) < lim ? qb[ln + 64u * (j + 2)] : 0u;
-        x1 = 64 * (j + 3) < lim ? qb[ln + 64u * (j + 3)] : 0u;
-        pair(w0, w1, j, false);
+      if (CNT) {   // buffer loads (range-checked: no clamp), rows masked in pair()
+        int vo = (int)((cur.b + ln) * 4u) + 256 * 8;
+        uint32_t x0 = __builtin_amdgcn_raw_buffer_load_b32(crs, vo, 0, 0), x1 = __builtin_amdgcn_raw_buffer_load_b32(crs, vo + 256, 0, 0);
+        for (int j = 8; 64 * j < (int)nsnp; j += 2) {
+          const uint32_t w0 = x0, w1 = x1;
+          vo += 512;
+          x0 = __builtin_amdgcn_raw_buffer_load_b32(crs, vo, 0, 0);
+          x1 = __builtin_amdgcn_raw_buffer_load_b32(crs, vo + 256, 0, 0);
+          pair(w0, w1, j, false);
+        }
+      } else {
+        uint32_t x0 = 64 * 8 < lim ? qb[ln + 64 * 8] : 0u, x1 = 64 * 9 < lim ? qb[ln + 64 * 9] : 0u;
+        for (int j = 8; 64 * j < (int)nsnp; j += 2) {
+          const uint32_t w0 = x0, w1 = x1;
+          x0 = 64 * (j + 2) < lim ? qb[ln + 64u * (j + 2)] : 0u;
+          x1 = 64 * (j + 3) < lim ? qb[ln + 64u * (j + 3)] : 0u;
+          pair(w0, w1, j, false);
+        }
       }
     }
     MARK(22);
