@@ -725,7 +725,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   pl->slot_base_h = slot_base;
   // counts plan: no filter (the scan kernels classify counts without positions / annotations);
   // SFS2D_CNT=0 forces the bins pipeline (comparison)
-  pl->cnt = prm->ann_want < 0 && !prm->has_start && !prm->has_end && data->n < (int64_t(1) << 30);   // (buffer loads: n words < 4 GB)
+  pl->cnt = prm->ann_want < 0 && !prm->has_start && !prm->has_end;
   if (const char* ev = std::getenv("SFS2D_CNT")) pl->cnt = pl->cnt && ev[0] != '0';
   pl->K.nm1 = data->n > 0 ? (uint32_t)(data->n - 1) : 0u;
   pl->K.kmul = (uint32_t)(pl->K.n2 + 1) | (1u << 16);

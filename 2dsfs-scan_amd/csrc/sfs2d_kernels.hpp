@@ -462,6 +462,14 @@ __device__ __forceinline__ uint32_t snp_word(const KParams& P, const uint32_t* _
   return CNT ? cls_word(P, src[i]) : src[i];
 }
 
+// counts plans: a window's rows as a buffer resource based at its first SNP b, n - b words long (the
+// range check returns 0 past the data set's last SNP: no clamp, no per-row address arithmetic; the
+// rows sit in the loads' immediate offsets).  b is wave-uniform: the descriptor is scalar work.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t count_rows(const uint32_t* counts, uint32_t b, uint32_t nm1) {
+  const uint32_t left = min(nm1 + 1u - b, 0x3fffffffu);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(counts + b), (short)0, (int)(left * 4u), 0x00020000);
+}
+
 __device__ __forceinline__ uint32_t bin_k2(uint32_t w) { return w & 0xffffu; }
 __device__ __forceinline__ uint32_t bin_g1(uint32_t w) { return (w >> 16) & 0x7fu; }
 __device__ __forceinline__ uint32_t bin_g2(uint32_t w) { return (w >> 23) & 0x7fu; }
@@ -1712,10 +1720,11 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
       w.b = ch.cb + (ch.wid_lo + (s - ch.slot_lo)) * P.ws;
       w.e = w.b + P.ws;
     }
-    if (w.has) {   // the bins buffer has SCAN_PAD readable words past n (counts: loads clamped to n); masked in the last step
+    if (w.has) {   // the bins buffer has SCAN_PAD readable words past n (counts: buffer loads, 0 past n); masked in the last step
       if (CNT) {
+        const __amdgpu_buffer_rsrc_t rr = count_rows(bins, w.b, P.nm1);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) w.u[j] = bins[min(w.b + (uint32_t)lane + 64u * j, P.nm1)];
+        for (int j = 0; j < 8; ++j) w.u[j] = __builtin_amdgcn_raw_buffer_load_b32(rr, lane * 4 + 256 * j, 0, 0);
       } else {
         const uint32_t* q = bins + w.b + lane;
 #pragma unroll
@@ -1921,13 +1930,26 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
     for (int j = 0; j < 8; j += 2)
       if (64 * j < (int)nsnp) pair(cur.u[j], cur.u[j + 1], j, true);
     if (nsnp > 8 * WAVE) {
-      const uint32_t* qb = bins + cur.b + lane;
-      uint32_t x0 = 64 * 8 < lim ? qb[64 * 8] : 0u, x1 = 64 * 9 < lim ? qb[64 * 9] : 0u;
-      for (int j = 8; 64 * j < (int)nsnp; j += 2) {
-        const uint32_t w0 = x0, w1 = x1;
-        x0 = 64 * (j + 2) < lim ? qb[64 * (j + 2)] : 0u;   // one pair ahead
-        x1 = 64 * (j + 3) < lim ? qb[64 * (j + 3)] : 0u;
-        pair(w0, w1, j, false);
+      if (CNT) {   // buffer loads (range-checked), rows masked in pair()
+        const __amdgpu_buffer_rsrc_t rr = count_rows(bins, cur.b, P.nm1);
+        int vo = lane * 4 + 256 * 8;
+        uint32_t x0 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo, 0, 0), x1 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo + 256, 0, 0);
+        for (int j = 8; 64 * j < (int)nsnp; j += 2) {
+          const uint32_t w0 = x0, w1 = x1;
+          vo += 512;
+          x0 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo, 0, 0);   // one pair ahead
+          x1 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo + 256, 0, 0);
+          pair(w0, w1, j, false);
+        }
+      } else {
+        const uint32_t* qb = bins + cur.b + lane;
+        uint32_t x0 = 64 * 8 < lim ? qb[64 * 8] : 0u, x1 = 64 * 9 < lim ? qb[64 * 9] : 0u;
+        for (int j = 8; 64 * j < (int)nsnp; j += 2) {
+          const uint32_t w0 = x0, w1 = x1;
+          x0 = 64 * (j + 2) < lim ? qb[64 * (j + 2)] : 0u;   // one pair ahead
+          x1 = 64 * (j + 3) < lim ? qb[64 * (j + 3)] : 0u;
+          pair(w0, w1, j, false);
+        }
       }
     }
     if (!P.fold || filt) {   // rare settings: unfolded (SNPs in the excluded last 2D bin), variant_type filter
@@ -2177,9 +2199,6 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   const Chunk ch = chunks[blockIdx.x];
   const int bg = bg_per_chrom ? (int)ch.chrom : 0;
   const double2* rtg = reinterpret_cast<const double2*>(dfg + 2 * LNT);   // FSTIN: (1/n, 1/(n(n-1))) (k_init_lnx)
-  // CNT: the counts as a buffer resource of n words (loads past n return 0; n < 2^30, plan_create)
-  const __amdgpu_buffer_rsrc_t crs =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(bins), (short)0, (int)((P.nm1 + 1u) * 4u), 0x00020000);
 
   // LDS: lp table (nt, rounded up to even: the histograms are 16-B aligned) | D | F | histograms
   double* LPl = ldsd;
@@ -2208,11 +2227,10 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       // (uniform base + a 32-bit lane offset: no per-lane 64-bit pointer stays live, which the exact
       // path's registers pushed to scratch -- 512 B of stores per wavefront)
       const uint32_t* q = bins + w.b;
-      if (CNT) {   // counts, no padding past n: buffer loads, range-checked (0 past n; masked later),
-                   // one lane offset and the rows in the instruction's immediate offset
-        const int vo = (int)((w.b + (uint32_t)lane) * 4u);
+      if (CNT) {   // counts, no padding past n: range-checked buffer loads (0 past n; masked later)
+        const __amdgpu_buffer_rsrc_t rr = count_rows(bins, w.b, P.nm1);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) w.u[j] = __builtin_amdgcn_raw_buffer_load_b32(crs, vo + 256 * j, 0, 0);
+        for (int j = 0; j < 8; ++j) w.u[j] = __builtin_amdgcn_raw_buffer_load_b32(rr, lane * 4 + 256 * j, 0, 0);
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) w.u[j] = q[(uint32_t)lane + 64u * j];
@@ -2525,13 +2543,14 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       uint32_t ln = (uint32_t)lane;
       asm volatile("" : "+v"(ln));   // (else bins + lane is hoisted out of the window loop and spilled)
       if (CNT) {   // buffer loads (range-checked: no clamp), rows masked in pair()
-        int vo = (int)((cur.b + ln) * 4u) + 256 * 8;
-        uint32_t x0 = __builtin_amdgcn_raw_buffer_load_b32(crs, vo, 0, 0), x1 = __builtin_amdgcn_raw_buffer_load_b32(crs, vo + 256, 0, 0);
+        const __amdgpu_buffer_rsrc_t rr = count_rows(bins, cur.b, P.nm1);
+        int vo = (int)(ln * 4u) + 256 * 8;
+        uint32_t x0 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo, 0, 0), x1 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo + 256, 0, 0);
         for (int j = 8; 64 * j < (int)nsnp; j += 2) {
           const uint32_t w0 = x0, w1 = x1;
           vo += 512;
-          x0 = __builtin_amdgcn_raw_buffer_load_b32(crs, vo, 0, 0);
-          x1 = __builtin_amdgcn_raw_buffer_load_b32(crs, vo + 256, 0, 0);
+          x0 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo, 0, 0);
+          x1 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo + 256, 0, 0);
           pair(w0, w1, j, false);
         }
       } else {

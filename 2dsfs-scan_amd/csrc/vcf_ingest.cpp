@@ -22,6 +22,7 @@
 #include <climits>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <string_view>
@@ -558,8 +559,11 @@ int sfs2d_vcf_read(const char* vcf_path, const char* popmap_path, int nthreads, 
     auto rec_id = [](size_t pi, int64_t r) { return ((int64_t)pi << 40) | r; };   // (part, record)
     std::vector<uint8_t> is_first((size_t)total, 0);
     std::vector<int64_t> last_of((size_t)total, -1);   // first records: (part, record) of the key's last record
+    // >= 64k records per shard thread (SFS2D_VCF_MERGE_CHUNK overrides: the tests use tiny shards)
+    int64_t chunk = 65536;
+    if (const char* ev = std::getenv("SFS2D_VCF_MERGE_CHUNK")) chunk = std::max<int64_t>(1, std::atoll(ev));
     {
-      const int S = std::max(1, std::min<int>(T, (int)std::max<int64_t>(1, total / 65536)));
+      const int S = std::max(1, std::min<int>(T, (int)std::max<int64_t>(1, total / chunk)));
       auto shard = [&](int t) {
         size_t cap = 16;
         while (cap < (size_t)(total / S + 1) * 2) cap <<= 1;
@@ -669,7 +673,7 @@ int sfs2d_vcf_read(const char* vcf_path, const char* popmap_path, int nthreads, 
     // the rest per slot, in parallel: position text and value, alleles, calls
     v->pos_blob.resize((size_t)v->pos_off[n]);
     {
-      const int W = std::max(1, std::min<int>(T, (int)std::max<int64_t>(1, n / 16384)));
+      const int W = std::max(1, std::min<int>(T, (int)std::max<int64_t>(1, n / std::max<int64_t>(1, chunk / 4))));
       auto fill = [&](int t) {
         const int64_t lo = n * t / W, hi = n * (t + 1) / W;
         for (int64_t s = lo; s < hi; ++s) {

@@ -108,6 +108,67 @@ def cpu_baseline(p):
                                    "sample": f"oracle/sfs_oracle.combined_scan on the same stream ({dt1:.1f} s)"}}
 
 
+def end_to_end(n_rec=1_000_000, nchrom=8, seed=3):
+    """The reference script's job end to end (twoDSFS_class.py:1910-2040: make_data_dict_vcf, then
+    combined_scan at 20 kb and 500 kb and scan_perChr_bySNPs at 500 SNPs, save_csv_stats) as this
+    framework runs it (python -m sfs2d): a synthetic BGZF VCF of n_rec records x 32 samples (18 uv +
+    14 bv, the reference's popmap shape) -> native ingest -> packed upload -> one k_prep pass + three
+    scans (multi_scan) -> three CSVs.  Wall time from the file on disk to the CSVs written."""
+    import tempfile
+    import zlib
+    import struct
+    from sfs2d import cli
+    rng = np.random.default_rng(seed)
+    samples = [f"S{i}" for i in range(32)]
+    d = tempfile.mkdtemp(prefix="sfs2d_e2e_")
+    vcf, pm = os.path.join(d, "synth.vcf.gz"), os.path.join(d, "popmap.txt")
+    with open(pm, "w") as fh:
+        fh.write("".join(f"{x}\t{'uv' if i < 18 else 'bv'}\n" for i, x in enumerate(samples)))
+    t0 = time.perf_counter()
+    gts = np.frombuffer(b"0/0\t0/1\t1/1\t./.\t1/0\t", dtype="S4")
+    g = gts[rng.choice(5, size=(n_rec, 32), p=[0.5, 0.2, 0.15, 0.05, 0.1])].view(np.uint8).reshape(n_rec, 128)
+    g[:, -1] = ord("\n")
+    per = n_rec // nchrom
+    pos = np.concatenate([np.cumsum(rng.integers(1, 110, per)) for _ in range(nchrom)] +
+                         [np.cumsum(rng.integers(1, 110, n_rec - per * nchrom))])
+    chrom = [f"chr{min(i // per, nchrom - 1) + 1}" for i in range(n_rec)]
+    pre = [f"{c}\t{q}\t.\tA\tG\t.\tPASS\tPR\tGT\t".encode() for c, q in zip(chrom, pos.tolist())]
+    body = b"".join(a + b for a, b in zip(pre, (bytes(r) for r in g)))
+    head = ("##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t" + "\t".join(samples) + "\n").encode()
+    text = head + body
+    out = bytearray()
+    for i in range(0, len(text), 65280):   # BGZF blocks (SAM spec 4.1), then the EOF block
+        chunk = text[i:i + 65280]
+        c = zlib.compressobj(1, zlib.DEFLATED, -15)
+        cd = c.compress(chunk) + c.flush()
+        out += (b"\x1f\x8b\x08\x04" + b"\x00" * 4 + b"\x00\xff" + struct.pack("<H", 6) + b"BC" +
+                struct.pack("<HH", 2, 18 + len(cd) + 8 - 1) + cd + struct.pack("<II", zlib.crc32(chunk), len(chunk)))
+    out += bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+    with open(vcf, "wb") as fh:
+        fh.write(out)
+    t_gen = time.perf_counter() - t0
+    args = [vcf, pm, "--window", "20000", "--window", "500000", "--snp-window", "500",
+            "--out-prefix", os.path.join(d, "stats")]
+    import contextlib
+    import io
+    cli.main(args)   # warm: library loads, first HIP context / plan allocations
+    err = io.StringIO()
+    t0 = time.perf_counter()
+    with contextlib.redirect_stderr(err):
+        outs = cli.main(args)
+    wall = time.perf_counter() - t0
+    rows = sum(max(0, sum(1 for _ in open(o)) - 1) for o in outs)
+    stages = [ln for ln in err.getvalue().splitlines() if ln.startswith(("ingest", "multi_scan"))]
+    for f in os.listdir(d):
+        os.remove(os.path.join(d, f))
+    os.rmdir(d)
+    return {"wall_s": wall, "records": n_rec, "records_per_s": n_rec / wall, "csv_rows": rows,
+            "vcf_bytes": len(out), "stages": stages, "generate_s": t_gen,
+            "workload": f"synthetic BGZF VCF, {n_rec} records x 32 samples (18 uv + 14 bv), {nchrom} chromosomes; "
+                        "python -m sfs2d --window 20000 --window 500000 --snp-window 500 (the reference "
+                        "script's three scans) from the file on disk to the three CSVs written, second run"}
+
+
 def hbm_stream_roofline(eng, steps=5):
     """BASELINE config 3 on one GPU (5e7 SNPs, 32 chromosomes, ~600 MB read): past the MALL."""
     from sfs2d.engine import ScanConfig
@@ -212,6 +273,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-hbm-stream", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the VCF -> CSV end-to-end timing")
     ap.add_argument("--streams", type=int, default=3,
                     help="consecutive steps round-robin over this many plans, each on its own HIP stream "
                          "(independent passes overlap; sfs2d_plan_run_streams)")
@@ -391,6 +453,8 @@ def main():
             line["roofline_hbm"] = hbm_stream_roofline(eng)
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(p)
+        if not args.no_e2e and world == 1:
+            line["end_to_end_vcf_csv"] = end_to_end()
         print(json.dumps(line), flush=True)
     for q in plans[::-1]:
         q.close()

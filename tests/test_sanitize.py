@@ -21,7 +21,8 @@ GOLD = os.path.join(HERE, "golden")
 SRC = os.path.join(REPO, "2dsfs-scan_amd", "csrc")
 FLAGS = ["-O1", "-g", "-fno-omit-frame-pointer"]
 ENV = dict(os.environ, ASAN_OPTIONS="halt_on_error=1:detect_leaks=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
-           TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1")
+           TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1",
+           SFS2D_VCF_MERGE_CHUNK="61")   # the dict merge sharded over every thread even on small inputs
 
 pytestmark = pytest.mark.skipif(shutil.which("g++") is None or shutil.which("gcc") is None, reason="no host compiler")
 

@@ -130,8 +130,12 @@ def write_popmap(path, mapping):
     open(path, "w").write("".join(f"{s}\t{p}\n" for s, p in mapping))
 
 
-@pytest.mark.parametrize("late", [False, True])
-def test_threads_and_oracle(tmp_path, late):
+@pytest.mark.parametrize("late,merge_chunk", [(False, None), (True, None), (False, "97")])
+def test_threads_and_oracle(tmp_path, monkeypatch, late, merge_chunk):
+    """Thread-count independence; merge_chunk: the dict merge sharded over many threads (97-record
+    shards instead of 64k) -- duplicate keys across shards and parse chunks keep dict semantics."""
+    if merge_chunk:
+        monkeypatch.setenv("SFS2D_VCF_MERGE_CHUNK", merge_chunk)
     raw = synth_vcf(40000, SAMPLES, seed=5, late_header=late)
     path = str(tmp_path / "s.vcf.gz")
     open(path, "wb").write(gzip.compress(raw, 1))
