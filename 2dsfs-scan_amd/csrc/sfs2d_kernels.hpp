@@ -135,6 +135,9 @@ struct Tile {   // k_prep work item: SNPs [begin, end) of chromosome chrom = [cb
 constexpr int SCAN_PAD = 512;   // readable words past the end of the per-SNP bins (k_scan_w prefetch)
 constexpr int CTR_POOLS = 8;     // k_scan_w dynamic window pools per chromosome
 constexpr int CTR_STRIDE = 16;   // one 64-B line per pool counter
+#ifndef SFS2D_PREP_PREFETCH
+#define SFS2D_PREP_PREFETCH 1
+#endif
 #ifndef SFS2D_FST_LDS
 #define SFS2D_FST_LDS 256
 #endif
@@ -763,19 +766,44 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
   const uint32_t ab = t.begin & ~3u, alast = (t.end - 1u) & ~3u;
   // (a segmentation-only pass -- a supplied background, no bins, no Fst -- reads no counts)
   constexpr bool NEED_C = DO_BG || DO_BINS || FST;
-  for (uint32_t base = ab; base < t.end; base += STEP) {
+  // the step's vectors (and the wave-edge neighbour positions) are loaded one step ahead: HBM-sized
+  // streams keep two steps of loads in flight per wave (SFS2D_PREP_PREFETCH=0 at compile time: one)
+  struct StepIn {
+    uint4 c, p;
+    uint2 a;
+    uint32_t xp, xn;
+  };
+  auto load_step = [&](uint32_t base) {
+    StepIn x;
     const uint32_t ia = base + 4 * threadIdx.x;
     const uint32_t il = min(ia, alast);
-    const uint4 ca = NEED_C ? *reinterpret_cast<const uint4*>(counts + il) : make_uint4(0, 0, 0, 0);
-    const uint4 pa = need_pos ? *reinterpret_cast<const uint4*>(pos + il) : make_uint4(0, 0, 0, 0);
-    const uint2 aav = filt ? *reinterpret_cast<const uint2*>(ann + il) : make_uint2(0, 0);
+    x.c = NEED_C ? *reinterpret_cast<const uint4*>(counts + il) : make_uint4(0, 0, 0, 0);
+    x.p = need_pos ? *reinterpret_cast<const uint4*>(pos + il) : make_uint4(0, 0, 0, 0);
+    x.a = filt ? *reinterpret_cast<const uint2*>(ann + il) : make_uint2(0, 0);
+    x.xp = 0;
+    x.xn = 0;
+    if (DO_SEG) {   // neighbour positions at the wave edges and past the tile end
+      const bool edge_next = lane == WAVE - 1 || ia + 4 >= t.end;
+      if (lane == 0 && ia > 0) x.xp = pos[min(ia, alast + 4u) - 1];
+      if (edge_next && ia + 4 < t.ce) x.xn = pos[ia + 4];
+    }
+    return x;
+  };
+  StepIn nxt = load_step(ab);
+  for (uint32_t base = ab; base < t.end; base += STEP) {
+    const uint32_t ia = base + 4 * threadIdx.x;
+#if SFS2D_PREP_PREFETCH
+    const StepIn cur = nxt;
+    if (base + STEP < t.end) nxt = load_step(base + STEP);   // block-uniform
+#else
+    const StepIn cur = base == ab ? nxt : load_step(base);
+#endif
+    const uint4 ca = cur.c, pa = cur.p;
+    const uint2 aav = cur.a;
     uint32_t wpa = 0, wna = 0;
     if (DO_SEG) {
-      // neighbour positions at the wave edges and past the tile end, loaded with the vectors
-      uint32_t xa_prev = 0, xa_next = 0;
+      const uint32_t xa_prev = cur.xp, xa_next = cur.xn;
       const bool edge_next = lane == WAVE - 1 || ia + 4 >= t.end;
-      if (lane == 0 && ia > 0) xa_prev = pos[min(ia, alast + 4u) - 1];
-      if (edge_next && ia + 4 < t.ce) xa_next = pos[ia + 4];
       wpa = __shfl_up(wid_fast(P, pa.w), 1, WAVE);
       wna = __shfl_down(wid_fast(P, pa.x), 1, WAVE);
       if (lane == 0) wpa = wid_fast(P, xa_prev);
