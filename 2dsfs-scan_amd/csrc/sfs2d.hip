@@ -100,7 +100,7 @@ struct sfs2d_ctx {
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   double* d_lnx = nullptr;
-  double* d_df = nullptr;   // D(r), F(x) (LNT each), then (1/k, 1/(k(k-1))) pairs (RCPN)
+  double* d_df = nullptr;   // D(r), F(x) (LNT each), then (1/k, 1/(k(k-1))) pairs (RCPN), then Fst (p, A) by (alt, ref) (FSTAR)
   std::string err;
   std::mutex err_mu;
 };
@@ -457,11 +457,11 @@ int sfs2d_ctx_create(int device, sfs2d_ctx** out) {
   c->stream = c->own;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) c->ncu = prop.multiProcessorCount;
-  if (dalloc(c, &c->d_lnx, LNX_N) || dalloc(c, &c->d_df, 2 * LNT + 2 * RCPN)) {
+  if (dalloc(c, &c->d_lnx, LNX_N) || dalloc(c, &c->d_df, 2 * LNT + 2 * RCPN + 2 * FSTAR)) {
     hipFree(c->d_lnx); hipStreamDestroy(c->own); delete c; return SFS2D_E_NOMEM;
   }
   hipLaunchKernelGGL(k_init_lnx, dim3(LNX_N / 256), dim3(256), 0, c->stream, c->d_lnx, c->d_df, c->d_df + LNT,
-                     c->d_df + 2 * LNT);
+                     c->d_df + 2 * LNT, c->d_df + 2 * LNT + 2 * RCPN);
   if (hipStreamSynchronize(c->stream) != hipSuccess) {
     hipFree(c->d_lnx); hipFree(c->d_df); hipStreamDestroy(c->own); delete c; return SFS2D_E_HIP;
   }

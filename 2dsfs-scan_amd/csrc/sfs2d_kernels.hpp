@@ -57,6 +57,7 @@ constexpr int KBLOCK = 512;       // k_bg_slice workgroup
 constexpr int LNX_N = 1 << 20;    // ln(k) table for k < LNX_N (bin counts / window totals)
 constexpr int LNT = 512;          // D(r) and x ln x tables staged in LDS by k_scan_w
 constexpr int RCPN = 512;         // (1/k, 1/(k(k-1))) for k < 512 (Fst: called allele counts ref + alt <= 510), after the LNT tables
+constexpr int FSTAR = 65536;      // Fst per population and SNP: (p, A) by (alt, ref) = one u16 half of the counts word, after RCPN
 constexpr int REPL = 4;           // replicas of the per-chromosome background histograms
 constexpr int PW_MAX_LEAVES = 1024;  // numpy pairwise leaves (64-128 values each): grids up to 255 x 255 (u8 counts)
 constexpr int LEAVES_PER_SLICE = 4;
@@ -459,6 +460,28 @@ __device__ __forceinline__ void cls_fields(const KParams& P, uint32_t c, uint32_
   g2 = gv >> 16;
 }
 
+// k_scan_w's per-SNP classification: cls_fields' k2, and both folded 1D bins packed (u16 pairs, times BS)
+// with no range test -- the excluded bins 0 (fixed in the population) and n_p (MAF 1/2) are counted like the
+// others and dropped at the window's end; counts above 2 pop_size (an error k_prep reports) clamp to n_p
+template <uint32_t BS>   // gp in bytes: the bins times BS (the LDS bytes per 1D bin)
+__device__ __forceinline__ void cls_k2g(const KParams& P, uint32_t c, uint32_t& k2, uint32_t& gp) {
+  const bool sw = (int)__builtin_amdgcn_udot4(c, 0x01000100u, 0u, false) > P.fold_thr;
+  const uint32_t x = sw ? c : (c >> 8);
+  const uint32_t kk = __builtin_amdgcn_udot4(x, P.kmul, 0u, false);
+  k2 = kk < (uint32_t)P.nb2 - 1u ? kk : 0u;
+  const u16x2 a = as_u16x2(__builtin_amdgcn_perm(0u, c, 0x0c030c01u));      // (a1, a2)
+  const u16x2 g = __builtin_elementwise_min(a, as_u16x2(P.n12) - a);         // min(a, n - a)
+  const u16x2 np = {(unsigned short)P.n1p, (unsigned short)P.n2p};
+  gp = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(g, np) * (u16x2){(unsigned short)BS, (unsigned short)BS});
+}
+
+// k_scan_w: the same over the window [b, e) only: loads past the window's end return 0 (SNPs in no
+// spectrum, no called allele), so the rows need no masking
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t window_rows(const uint32_t* counts, uint32_t b, uint32_t e, uint32_t nm1) {
+  const uint32_t left = min(min(e, nm1 + 1u) - b, 0x3fffffffu);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(counts + b), (short)0, (int)(left * 4u), 0x00020000);
+}
+
 // the per-SNP source of the scan kernels: the bins k_prep wrote, or (CNT) the counts, classified
 template <bool CNT>
 __device__ __forceinline__ uint32_t snp_word(const KParams& P, const uint32_t* __restrict__ src, uint32_t i) {
@@ -481,12 +504,19 @@ __device__ __forceinline__ uint32_t bin_g2(uint32_t w) { return (w >> 23) & 0x7f
 
 // ln k for k < LNX_N; F(x) = x ln x for x < LNT; D(r) = F(r+1) - F(r) for r < LNT-1 and
 // D(LNT-1) = 0 (k_scan_w adds the ranks from LNT-1 on per bin, as F(x) - F(LNT-1))
-__global__ void k_init_lnx(double* lnx, double* dtab, double* ftab, double* rtab) {
+__global__ void k_init_lnx(double* lnx, double* dtab, double* ftab, double* rtab, double* artab) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < LNX_N) lnx[i] = i ? log((double)i) : 0.0;
   if (i < RCPN) {   // Fst: (1/n, 1/(n(n-1))) per called allele count n; 0 below n = 2 (not in the set)
     rtab[2 * i] = i >= 2 ? 1.0 / (double)i : 0.0;
     rtab[2 * i + 1] = i >= 2 ? 1.0 / ((double)i * (double)(i - 1)) : 0.0;
+  }
+  if (i < FSTAR) {   // Fst: one population's (p, A) = (a / n, a(a-1) / (n(n-1))) by i = a << 8 | r (n = r + a),
+                     // both 0 below n = 2 -- fst_snp's p and A, from the same reciprocals
+    const uint32_t a = (uint32_t)i >> 8, n = a + ((uint32_t)i & 0xffu);
+    const double r1 = n >= 2u ? 1.0 / (double)n : 0.0, r2 = n >= 2u ? 1.0 / ((double)n * (double)(n - 1u)) : 0.0;
+    artab[2 * i] = (double)a * r1;
+    artab[2 * i + 1] = (double)(a * (a - 1u)) * r2;
   }
   if (i < LNT) {
     const double a = i ? (double)i * log((double)i) : 0.0;
@@ -2174,6 +2204,47 @@ __device__ __forceinline__ void wave_sum_halves_all(double v, double& a, double&
   b = swap32_d(v, true);
 }
 
+// the window's five fp64 sums at once, as a reduce-scatter: each lane swap exchanges halves of two
+// values (one swap and one add per pair of values instead of per value), and the DPP row steps add two
+// interleaved values (even lanes one, odd lanes the other).  In: a (summed over the wave), h (summed over
+// lanes 0-31 and over lanes 32-63 separately), f1, f2 (over the wave).  Out, in the lane's own register:
+// lane 0 sum(a), lane 16 sum(f1), lane 32 sum(f2), lane 33 sum(h, lanes 0-31), lane 48 sum(h, lanes
+// 32-63).  A fixed tree: deterministic.  (Separate replicated sums took ~70 VALU instructions per window,
+// this ~35.)
+__device__ __forceinline__ void swap32_pair(double x, double y, double& xo, double& yo) {
+  const unsigned long long u = __double_as_longlong(x), v = __double_as_longlong(y);
+  const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)u, (uint32_t)v, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(u >> 32), (uint32_t)(v >> 32), false, false);
+  xo = __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));   // [x lo | y lo]
+  yo = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));   // [x hi | y hi]
+}
+__device__ __forceinline__ void swap16_pair(double x, double y, double& xo, double& yo) {
+  const unsigned long long u = __double_as_longlong(x), v = __double_as_longlong(y);
+  const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)u, (uint32_t)v, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(u >> 32), (uint32_t)(v >> 32), false, false);
+  xo = __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));   // rows x0 y0 x2 y2
+  yo = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));   // rows x1 y1 x3 y3
+}
+__device__ __forceinline__ double wave_sum5(double a, double h, double f1, double f2, uint32_t lane) {
+  double x, y;
+  swap32_pair(a, f2, x, y);
+  const double r1 = x + y;                       // lanes 0-31: a, 32-63: f2 (32-lane partials)
+  swap32_pair(f1, h, x, y);
+  const double r2 = lane < 32 ? x + y : y;       // lanes 0-31: f1 partial, 32-63: h (own, upper half)
+  const double r3 = x;                           // lanes 32-63: h of lanes 0-31
+  swap16_pair(r1, r2, x, y);
+  const double q = x + y;                        // rows: a, f1, f2, h upper (16-lane partials)
+  swap16_pair(r3, r3, x, y);
+  const double t = x + y;                        // rows 2, 3: h lower
+  const bool odd = lane & 1u;
+  double z = odd ? t : q;
+  z += mdpp_d<0xB1>(odd ? q : t);                // quad_perm [1,0,3,2]: even lanes q, odd lanes t
+  z += mdpp_d<0x4E>(z);                          // quad_perm [2,3,0,1]
+  z += mdpp_d<0x124>(z);                         // row_ror:4 (keeps lane parity)
+  z += mdpp_d<0x128>(z);                         // row_ror:8
+  return z;
+}
+
 // v_writelane_b32 (the LLVM intrinsic: this clang has no builtin for it): lane l (uniform) of `old`
 // takes the uniform value v; the compiler puts the lane select in M0
 extern "C" __device__ int sfs2d_llvm_writelane(int v, int l, int old) __asm("llvm.amdgcn.writelane.i32");
@@ -2226,7 +2297,9 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   const int lane = tid & (WAVE - 1);
   const Chunk ch = chunks[blockIdx.x];
   const int bg = bg_per_chrom ? (int)ch.chrom : 0;
-  const double2* rtg = reinterpret_cast<const double2*>(dfg + 2 * LNT);   // FSTIN: (1/n, 1/(n(n-1))) (k_init_lnx)
+  // FSTIN: one population's (p, A) by the (alt, ref) half of the counts word (k_init_lnx; L1-resident: the
+  // called counts cluster near 2 pop_size)
+  const double2* artg = reinterpret_cast<const double2*>(dfg + 2 * LNT + 2 * RCPN);
 
   // LDS: lp table (nt, rounded up to even: the histograms are 16-B aligned) | D | F | histograms
   double* LPl = ldsd;
@@ -2256,7 +2329,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       // path's registers pushed to scratch -- 512 B of stores per wavefront)
       const uint32_t* q = bins + w.b;
       if (CNT) {   // counts, no padding past n: range-checked buffer loads (0 past n; masked later)
-        const __amdgpu_buffer_rsrc_t rr = count_rows(bins, w.b, P.nm1);
+        const __amdgpu_buffer_rsrc_t rr = window_rows(bins, w.b, w.e, P.nm1);
 #pragma unroll
         for (int j = 0; j < 8; ++j) w.u[j] = __builtin_amdgcn_raw_buffer_load_b32(rr, lane * 4 + 256 * j, 0, 0);
       } else {
@@ -2352,20 +2425,18 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   }
   if (!active) return;
   const bool filt = P.ann_want >= 0;
-  const bool half1d = P.n1p <= 33 && P.n2p <= 33;
+  const bool half1d = P.n1p <= 31 && P.n2p <= 31;   // bins 0..n_p of each population on lanes 0-31 / 32-63
   const uint32_t zflags = bg_zero_flags(hb);
   const bool nan2 = hb.flags & BGF_NAN2, nan1a = hb.flags & BGF_NAN1A, nan1b = hb.flags & BGF_NAN1B;
   uint32_t* const H1a_l = H1a + rep;   // this lane's replica column of the 1D histograms
   uint32_t* const H1b_l = H1b + rep;
   const uint32_t trash = (uint32_t)(h2w + h1w + h1wb + lane);   // the lane's trash word (index from W)
-  uint32_t* const T_l = W + trash;
   const uint32_t one1 = P16 ? 0x10000u : 1u;   // 1D increment (P16: upper halves, see the window loop)
   // the 1D atomics' LDS byte addresses: per-lane bases kept opaque, so that a bin's address is one
   // v_lshl_add (the compiler otherwise re-splits base + replica + bin into three operations)
   typedef __attribute__((address_space(3))) uint32_t lds_u32;
   uint32_t a1b = (uint32_t)(uintptr_t)((lds_u32*)H1a_l), a2b = (uint32_t)(uintptr_t)((lds_u32*)H1b_l);
-  uint32_t atr = (uint32_t)(uintptr_t)((lds_u32*)T_l);
-  asm volatile("" : "+v"(a1b), "+v"(a2b), "+v"(atr));
+  asm volatile("" : "+v"(a1b), "+v"(a2b));
   // ---- batched finish.  Lane j of the B* registers holds the j-th window this wavefront has
   // scanned since the last flush (slot, SNP range, counts, the three sums); per window only the
   // sums' wave reductions run, and the T values, the zero / NaN rules, the Fst value and the 64-B
@@ -2441,18 +2512,40 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     }
     jb = 0;
   };
-  // window jb of the batch (lane 0 stores it; the values are wave-uniform)
+  // window jb of the batch: its integers (lane 0)
+  auto put_u = [&](uint32_t slot, uint32_t b, uint32_t nsnp, uint32_t n2, uint32_t n1a, uint32_t n1b, uint32_t nvar,
+                   uint32_t nlast) {
+    sh_bu[wv][0][jb] = slot;
+    sh_bu[wv][1][jb] = b;
+    sh_bu[wv][2][jb] = min(n2, 0xffffu) | (min(n2 + nlast, 0xffffu) << 16);
+    sh_bu[wv][3][jb] = min(n1a, 0xffffu) | (min(n1b, 0xffffu) << 16);
+    sh_bu[wv][4][jb] = min(nsnp, 0xffffu) | (min(nvar, 0xffffu) << 16);
+  };
   auto put = [&](uint32_t slot, uint32_t b, uint32_t nsnp, uint32_t n2, uint32_t n1a, uint32_t n1b, uint32_t nvar,
                  uint32_t nlast, double s2, double sa, double sb, ulonglong2 fq) {
     if (lane == 0) {
       sh_bd[wv][0][jb] = s2; sh_bd[wv][1][jb] = sa; sh_bd[wv][2][jb] = sb;
       if (FST) { sh_bf[wv][0][jb] = fq.x; sh_bf[wv][FST ? 1 : 0][jb] = fq.y; }
-      sh_bu[wv][0][jb] = slot;
-      sh_bu[wv][1][jb] = b;
-      sh_bu[wv][2][jb] = min(n2, 0xffffu) | (min(n2 + nlast, 0xffffu) << 16);
-      sh_bu[wv][3][jb] = min(n1a, 0xffffu) | (min(n1b, 0xffffu) << 16);
-      sh_bu[wv][4][jb] = min(nsnp, 0xffffu) | (min(nvar, 0xffffu) << 16);
+      put_u(slot, b, nsnp, n2, n1a, n1b, nvar, nlast);
     }
+  };
+  // the sums from wave_sum5's lanes (FSTIN: the Fst sums too; FST 1: k_prep's, lane 0)
+  // put5's store: the five lanes wave_sum5 leaves the sums in each store to their own batch array
+  // (one store, the lane's LDS address computed here and kept opaque: per-lane selects in the loop
+  // became a branch tree)
+  typedef __attribute__((address_space(3))) double lds_f64;
+  constexpr unsigned long long OWN5 = 1ull | (1ull << 33) | (1ull << 48) | (FSTIN ? (1ull << 16) | (1ull << 32) : 0ull);
+  uint32_t sdst;
+  {
+    double* d = lane == 0 ? &sh_bd[wv][0][0] : lane == 33 ? &sh_bd[wv][1][0] : lane == 48 ? &sh_bd[wv][2][0]
+              : lane == 16 ? reinterpret_cast<double*>(&sh_bf[wv][0][0])
+                           : reinterpret_cast<double*>(&sh_bf[wv][FST ? 1 : 0][0]);
+    sdst = (uint32_t)(uintptr_t)((lds_f64*)d);
+  }
+  asm volatile("" : "+v"(sdst));
+  auto put5 = [&](double v, ulonglong2 fq) {
+    if ((OWN5 >> lane) & 1ull) ((lds_f64*)(uintptr_t)(sdst + 8u * jb))[0] = v;
+    if (FST == 1 && lane == 0) { sh_bf[wv][0][jb] = fq.x; sh_bf[wv][FST ? 1 : 0][jb] = fq.y; }
   };
 
 
@@ -2490,11 +2583,11 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     // prefetched registers (a row wholly past e is skipped; SNPs past e are w = 0, outside every
     // spectrum).  Per SNP: the 2D LDS atomic (u16 halves) returns the SNP's rank r in its bin and the
     // SNP adds D(r) - lp_k (telescoping: sum_k x_k ln x_k = sum_i D(r_i)); the folded 1D bins are
-    // counted in lane & 3 replicas.  An SNP outside a spectrum adds to the lane's own trash word
-    // (shared words instead -- bin (0,0), the folded bin 0 -- cost 60% more LDS bank-conflict cycles):
-    // 0 for the 2D spectrum, so the word's low half stays 0 and gives rank 0, D(0) = 0, LPl[0] = 0;
-    // 0x10000 for the 1D spectra, whose counts live in the upper u16 halves.  Counts are wave-uniform
-    // ballot counts.
+    // counted in lane & 3 replicas, every SNP slot in one bin of each (the excluded bins 0 and n_p too:
+    // dropped at the window's end, which derives n1a / n1b from them).  An SNP outside the 2D spectrum
+    // adds 0 to the lane's own trash word (a shared word instead -- bin (0,0) -- cost 60% more LDS
+    // bank-conflict cycles), whose low half stays 0 and gives rank 0, D(0) = 0, LPl[0] = 0.  n2 is a
+    // wave-uniform ballot count.
     const uint32_t nsnp = cur.e - cur.b;
     const int lim = (int)nsnp - lane;
     const bool clampd = nsnp > (uint32_t)(LNT - 1);   // some rank may pass the D table
@@ -2506,22 +2599,26 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     double fA = 0.0, fP = 0.0, fM = 0.0;
     uint32_t n2 = 0, n1a = 0, n1b = 0, nlast = 0, nvar = 0;
     uint32_t kw[8];   // the 2D words of the first 8 rows, cleared after the window
-    auto pair = [&](uint32_t w0, uint32_t w1, int j, bool keep) {
-      // SNPs past the window's end: w = 0 (unconditional: a guard on the window's last rows cost
-      // more selects than the masking itself)
-      w0 = 64 * j < lim ? w0 : 0u;
-      w1 = 64 * (j + 1) < lim ? w1 : 0u;
-      const uint32_t ww[2] = {w0, w1};   // (CNT: counts; 0 past e, in no spectrum)
+    // FSTIN: the pair's (p, A) of both populations from the global (alt, ref) table, issued before the
+    // next rows' loads so that waiting for them leaves those in flight (loads complete in order)
+    auto fst_load = [&](uint32_t w0, uint32_t w1, double2 (&fq)[4]) {
+      if (FSTIN) {
+        fq[0] = artg[w0 & 0xffffu]; fq[1] = artg[w0 >> 16];
+        fq[2] = artg[w1 & 0xffffu]; fq[3] = artg[w1 >> 16];
+      }
+    };
+    // SNPs past the window's end: w = 0 (unconditional: a guard on the window's last rows cost more
+    // selects than the masking itself); w = 0 is in no spectrum and has no called allele
+    auto pair = [&](uint32_t w0, uint32_t w1, int j, bool keep, const double2 (&fq)[4]) {
+      const uint32_t ww[2] = {w0, w1};   // (CNT: counts)
       uint32_t rk[2], kk[2], ov[2], xs[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const uint32_t w = ww[q];
-        uint32_t k2, g1, g2;
-        if (CNT) cls_fields(P, w, k2, g1, g2);
-        else { k2 = bin_k2(w); g1 = bin_g1(w); g2 = bin_g2(w); }
-        n2 += __popcll(__ballot(k2 != 0u));
-        n1a += __popcll(__ballot(g1 != 0u));
-        n1b += __popcll(__ballot(g2 != 0u));
+        uint32_t k2, gp;   // gp: the folded 1D bins of both populations (u16 pair; excluded ones included)
+        if (CNT) cls_k2g<4 * R1>(P, w, k2, gp);
+        else { k2 = bin_k2(w); gp = (bin_g1(w) | (bin_g2(w) << 16)) * (4u * R1); }
+        n2 += 64u - (uint32_t)__popcll(__ballot(k2 == 0u));   // (the compare the selects below use)
         const uint32_t x = (CNT ? k2 : w) << 4;   // low five bits: (k2 & 1) << 4, the u16 half's shift
         const uint32_t word = k2 ? (P16 ? (k2 >> 1) : k2) : trash;
         // (v_lshlrev_b32 / v_bfe_u32 read the shift's low five bits: no mask; C's << would need one)
@@ -2531,19 +2628,21 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
         xs[q] = x;
         kk[q] = k2;
         if (keep) kw[(j + q) & 7] = word;
-        const uint32_t u1 = g1 ? a1b + g1 * (4u * R1) : atr, u2 = g2 ? a2b + g2 * (4u * R1) : atr;
+        // every SNP slot adds to one bin of each folded 1D spectrum (no range test, no trash select: the
+        // window's end drops bins 0 and n_p and counts n1a / n1b from them)
+        const uint32_t u1 = a1b + (gp & 0xffffu), u2 = a2b + (gp >> 16);
         __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u1, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u2, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (FSTIN) {   // (SNPs past e: counts 0, no called allele, terms 0)
-          const uint32_t a1 = __builtin_amdgcn_ubfe(w, 8, 8), a2 = w >> 24;
-          // (1/n, 1/(n(n-1))) from the global table (L1-resident; an LDS copy measured slower: the
-          // loop's LDS pipe is its bottleneck, profiles/r03k_fst_scan.txt)
-          const double2 q1 = rtg[__builtin_amdgcn_udot4(w, 0x0101u, 0u, false)];        // n1 = r1 + a1
-          const double2 q2 = rtg[__builtin_amdgcn_udot4(w, 0x01010000u, 0u, false)];    // n2 = r2 + a2
-          const double p1 = (double)a1 * q1.x, p2 = (double)a2 * q2.x;
-          fA += fma((double)__umul24(a1, a1 - 1u), q1.y, (double)__umul24(a2, a2 - 1u) * q2.y);
-          fP += p1 + p2;
-          fM = fma(p1, p2, fM);
+      }
+      if (FSTIN) {   // (SNPs past e: counts 0, no called allele, terms 0)
+        // five fp64 operations per SNP on the table's (p, A) (computed from (1/n, 1/(n(n-1))) they took
+        // ~20 VALU instructions in a VALU-bound loop; an LDS table measured slower: the loop's LDS pipe
+        // is busy, profiles/r03k_fst_scan.txt)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          fA += fq[2 * q].y + fq[2 * q + 1].y;
+          fP += fq[2 * q].x + fq[2 * q + 1].x;
+          fM = fma(fq[2 * q].x, fq[2 * q + 1].x, fM);
         }
       }
       // the ranks once both SNPs' atomics are issued (extracted right after its own atomic, each rank's
@@ -2564,30 +2663,39 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     MARK(19);
 #pragma unroll
     for (int j = 0; j < 8; j += 2)
-      if (64 * j < (int)nsnp) pair(cur.u[j], cur.u[j + 1], j, true);
+      if (64 * j < (int)nsnp) {
+        // (CNT: the loads past the window's end returned 0)
+        const uint32_t w0 = (CNT || 64 * j < lim) ? cur.u[j] : 0u, w1 = (CNT || 64 * (j + 1) < lim) ? cur.u[j + 1] : 0u;
+        double2 fq[4];
+        fst_load(w0, w1, fq);
+        pair(w0, w1, j, true, fq);
+      }
     MARK(20);
     if (nsnp > 8 * WAVE) {   // rows 8 on (windows of > 512 SNPs), streamed one pair ahead
       const uint32_t* qb = bins + cur.b;
       uint32_t ln = (uint32_t)lane;
       asm volatile("" : "+v"(ln));   // (else bins + lane is hoisted out of the window loop and spilled)
       if (CNT) {   // buffer loads (range-checked: no clamp), rows masked in pair()
-        const __amdgpu_buffer_rsrc_t rr = count_rows(bins, cur.b, P.nm1);
+        const __amdgpu_buffer_rsrc_t rr = window_rows(bins, cur.b, cur.e, P.nm1);
         int vo = (int)(ln * 4u) + 256 * 8;
         uint32_t x0 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo, 0, 0), x1 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo + 256, 0, 0);
         for (int j = 8; 64 * j < (int)nsnp; j += 2) {
-          const uint32_t w0 = x0, w1 = x1;
+          const uint32_t w0 = x0, w1 = x1;   // (0 past the window's end)
+          double2 fq[4];
+          fst_load(w0, w1, fq);
           vo += 512;
           x0 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo, 0, 0);
           x1 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo + 256, 0, 0);
-          pair(w0, w1, j, false);
+          pair(w0, w1, j, false, fq);
         }
       } else {
         uint32_t x0 = 64 * 8 < lim ? qb[ln + 64 * 8] : 0u, x1 = 64 * 9 < lim ? qb[ln + 64 * 9] : 0u;
         for (int j = 8; 64 * j < (int)nsnp; j += 2) {
-          const uint32_t w0 = x0, w1 = x1;
+          const uint32_t w0 = 64 * j < lim ? x0 : 0u, w1 = 64 * (j + 1) < lim ? x1 : 0u;
           x0 = 64 * (j + 2) < lim ? qb[ln + 64u * (j + 2)] : 0u;
           x1 = 64 * (j + 3) < lim ? qb[ln + 64u * (j + 3)] : 0u;
-          pair(w0, w1, j, false);
+          double2 fq[4];
+          pair(w0, w1, j, false, fq);
         }
       }
     }
@@ -2635,56 +2743,74 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     MARK(24);
     // 1D spectra: one lane per folded inner bin reads (and clears) its R1 replicas; with <= 32 inner
     // bins per population, lanes 0-31 take population 1 and lanes 32-63 population 2 (acca)
+    // (every SNP slot of the rows -- 128 per pair, masked ones included -- is counted in one bin of each
+    // spectrum: n1a / n1b = slots - bin 0 - bin n_p)
     double acca = 0.0, accb = 0.0;
     constexpr uint32_t S1 = P16 ? 16u : 0u;
+    const uint32_t slots = 128u * ((nsnp + 127u) / 128u);
     if (half1d) {
       const bool pa = lane < 32;
-      const int k = 1 + (lane & 31);
-      if (k <= (pa ? P.n1p : P.n2p) - 1) {
+      const int k = lane & 31, np = pa ? P.n1p : P.n2p;
+      uint32_t x = 0;
+      if (k <= np) {
         uint4* q = reinterpret_cast<uint4*>((pa ? H1a : H1b) + k * R1);
         const uint4 v = *q;
         *q = make_uint4(0, 0, 0, 0);
-        const uint32_t x = (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
-        acca = x ? xlnx(x, Ft, lnx) - (double)x * LPl[(pa ? P.t1a : P.t1b) + k] : 0.0;
+        x = (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
+        if (k >= 1 && k < np && x) acca = xlnx(x, Ft, lnx) - (double)x * LPl[(pa ? P.t1a : P.t1b) + k];
       }
+      n1a = slots - (uint32_t)__builtin_amdgcn_readlane((int)x, 0) - (uint32_t)__builtin_amdgcn_readlane((int)x, P.n1p);
+      n1b = slots - (uint32_t)__builtin_amdgcn_readlane((int)x, 32) -
+            (uint32_t)__builtin_amdgcn_readlane((int)x, 32 + P.n2p);
     } else {
+      uint32_t xa[2] = {0u, 0u}, xb[2] = {0u, 0u};
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int k = 1 + lane + WAVE * j;
-        if (k <= P.n1p - 1) {
+        const int k = lane + WAVE * j;
+        if (k <= P.n1p) {
           uint4* q = reinterpret_cast<uint4*>(H1a + k * R1);
           const uint4 v = *q;
           *q = make_uint4(0, 0, 0, 0);
           const uint32_t x = (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
-          acca += x ? xlnx(x, Ft, lnx) - (double)x * LPl[P.t1a + k] : 0.0;
+          xa[j] = x;
+          if (k >= 1 && k < P.n1p && x) acca += xlnx(x, Ft, lnx) - (double)x * LPl[P.t1a + k];
         }
-        if (k <= P.n2p - 1) {
+        if (k <= P.n2p) {
           uint4* q = reinterpret_cast<uint4*>(H1b + k * R1);
           const uint4 v = *q;
           *q = make_uint4(0, 0, 0, 0);
           const uint32_t x = (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
-          accb += x ? xlnx(x, Ft, lnx) - (double)x * LPl[P.t1b + k] : 0.0;
+          xb[j] = x;
+          if (k >= 1 && k < P.n2p && x) accb += xlnx(x, Ft, lnx) - (double)x * LPl[P.t1b + k];
         }
       }
+      const uint32_t ea = P.n1p >= WAVE ? (uint32_t)__builtin_amdgcn_readlane((int)xa[1], P.n1p - WAVE)
+                                        : (uint32_t)__builtin_amdgcn_readlane((int)xa[0], P.n1p);
+      const uint32_t eb = P.n2p >= WAVE ? (uint32_t)__builtin_amdgcn_readlane((int)xb[1], P.n2p - WAVE)
+                                        : (uint32_t)__builtin_amdgcn_readlane((int)xb[0], P.n2p);
+      n1a = slots - (uint32_t)__builtin_amdgcn_readlane((int)xa[0], 0) - ea;
+      n1b = slots - (uint32_t)__builtin_amdgcn_readlane((int)xb[0], 0) - eb;
     }
     if (it == 0) STAMP(13);
     MARK(25);
     // the sums, replicated in every lane (fixed trees: deterministic), into lane jb of the batch
-    const double s2 = wave_sum_all(acc2);
-    double sa, sb;
     if (half1d) {
-      wave_sum_halves_all(acca, sa, sb);
-    } else {
-      sa = wave_sum_all(acca);
-      sb = wave_sum_all(accb);
-    }
-    if (FSTIN) {
       const double m2 = 2.0 * fM;
-      fq = make_ulonglong2((unsigned long long)__double_as_longlong(wave_sum_all(fA - m2)),
-                           (unsigned long long)__double_as_longlong(wave_sum_all(fP - m2)));
+      const double v = wave_sum5(acc2, acca, FSTIN ? fA - m2 : 0.0, FSTIN ? fP - m2 : 0.0, (uint32_t)lane);
+      MARK(26);
+      put5(v, fq);
+      if (lane == 0) put_u(s, cur.b, nsnp, n2, n1a, n1b, nvar, nlast);
+    } else {
+      const double s2 = wave_sum_all(acc2);
+      const double sa = wave_sum_all(acca), sb = wave_sum_all(accb);
+      if (FSTIN) {
+        const double m2 = 2.0 * fM;
+        fq = make_ulonglong2((unsigned long long)__double_as_longlong(wave_sum_all(fA - m2)),
+                             (unsigned long long)__double_as_longlong(wave_sum_all(fP - m2)));
+      }
+      MARK(26);
+      put(s, cur.b, nsnp, n2, n1a, n1b, nvar, nlast, s2, sa, sb, fq);
     }
-    MARK(26);
-    put(s, cur.b, nsnp, n2, n1a, n1b, nvar, nlast, s2, sa, sb, fq);
     ++jb;
     group_sync<WAVE>();
     if (it == 0) STAMP(14);

@@ -116,10 +116,14 @@ def _records_vs_oracle(p, cfg_scan, ocfg, wins, bg_of, guards=True):
 
 
 @pytest.mark.parametrize("n1p,n2p,ws", [(25, 25, 20000), (18, 14, 7000), (50, 50, 20000), (100, 75, 100000),
-                                          (3, 2, 500), (25, 25, 500000), (40, 40, 20000), (44, 30, 20000)])
+                                          (3, 2, 500), (25, 25, 500000), (40, 40, 20000), (44, 30, 20000),
+                                          (31, 31, 20000), (32, 31, 20000), (60, 8, 20000), (8, 60, 20000),
+                                          (70, 5, 20000)])
 def test_records_per_chrom_bp(n1p, n2p, ws):
     """(40 x 40, 44 x 30: grids under the small-grid limit whose k_scan_w workgroup does not fit the
-    LDS take the large-grid kernels.)"""
+    LDS take the large-grid kernels.  31 x 31: the largest populations whose folded 1D bins 0..n_p k_scan_w
+    reads on half a wave each; 32 x 31, 60 x 8, 8 x 60: its one-bin-per-lane path, bins 0 and n_p of a
+    population in different lanes; 70 x 5: bin n_p in the second register.)"""
     from sfs2d import _lib as L
     from sfs2d.engine import ScanConfig
     from sfs2d.synth import synth_genome
