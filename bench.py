@@ -199,38 +199,43 @@ def hbm_stream_roofline(eng, steps=5):
            "k2_ms": k2,
            "pipeline_GBs": bp / tk / 1e9, "pipeline_frac": bp / tk / 1e9 / HBM_PEAK_GBS,
            "pipeline_ms": wall * 1e3,
-           "pipeline_bytes_note": "SURVEY 8(d): 12 B/SNP + 64 B/window per run over the wall time of back-to-back runs",
+           "pipeline_bytes_note": "SURVEY 8(d): 12 B/SNP + 64 B/window per run over the wall time of back-to-back "
+                                  "runs of one plan on one stream (passes overlapped: the 'overlapped' entry)",
            "windows": nwin, "windows_per_s": nwin / tk,
            "workload": "config 3 stream on 1 GPU: 32 chrom x 1.5625e6 SNPs, 20 kb, per-chromosome bg, T2D + T1D + Fst"}
     pl.close()
-    # T2D + T1D (the reference's statistics, no Fst) as independent passes overlapped on 2 HIP streams,
-    # the scan kernel capped at one workgroup per CU so that the next pass's bandwidth-bound k_prep
-    # runs beside the previous pass's compute-bound scan (profiles/r03h_streams_wgs.txt); with Fst,
-    # k_prep is VALU-heavy too and one stream is the fastest
+    # independent passes overlapped on 2 HIP streams (the bench's own mode), the scan kernel capped at one
+    # workgroup per CU so that the next pass's bandwidth-bound k_prep runs beside the previous pass's
+    # compute-bound scan (profiles/r03h_streams_wgs.txt): with Fst (the metric's statistics) and without
+    # (T2D + T1D, the reference's statistics)
     import torch
-    streams = [torch.cuda.current_stream().cuda_stream, torch.cuda.Stream().cuda_stream]
-    cfg2 = ScanConfig(n1p=POP, n2p=POP, window=WS, fst=False, scan_wgs_per_cu=1)
-    plans = [eng.plan(dev, cfg2) for _ in range(2)]
-    outs = [torch.zeros((plans[0].nrec, 64), dtype=torch.uint8, device="cuda") for _ in range(2)]
-    ptrs = [o.data_ptr() for o in outs]
     from sfs2d.engine import Plan
-    Plan.run_streams(plans, streams, 8, ptrs)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    Plan.run_streams(plans, streams, 8 * steps, ptrs)
-    torch.cuda.synchronize()
-    wo = (time.perf_counter() - t0) / (8 * steps)
-    for q in plans:
-        q.check()
-    if not torch.equal(outs[0], outs[1]):
-        raise RuntimeError("config-3 overlapped passes disagree")
-    out["t2d_t1d_overlapped"] = {
-        "pipeline_GBs": bp / wo / 1e9, "pipeline_frac": bp / wo / 1e9 / HBM_PEAK_GBS, "pipeline_ms": wo * 1e3,
-        "windows_per_s": nwin / wo,
-        "note": "T2D + T1D only (the reference's statistics; Hudson Fst not computed): 2 plans on 2 HIP streams, "
-                "passes overlapped, scan kernel capped at 1 workgroup per CU; SURVEY 8(d) bytes over the time per pass"}
-    for q in plans:
-        q.close()
+    streams = [torch.cuda.current_stream().cuda_stream, torch.cuda.Stream().cuda_stream]
+    for key, fst in (("overlapped", True), ("t2d_t1d_overlapped", False)):
+        cfg2 = ScanConfig(n1p=POP, n2p=POP, window=WS, fst=fst, scan_wgs_per_cu=1)
+        plans = [eng.plan(dev, cfg2) for _ in range(2)]
+        outs = [torch.zeros((plans[0].nrec, 64), dtype=torch.uint8, device="cuda") for _ in range(2)]
+        ptrs = [o.data_ptr() for o in outs]
+        Plan.run_streams(plans, streams, 8, ptrs)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        Plan.run_streams(plans, streams, 8 * steps, ptrs)
+        torch.cuda.synchronize()
+        wo = (time.perf_counter() - t0) / (8 * steps)
+        for q in plans:
+            q.check()
+        if not torch.equal(outs[0], outs[1]):
+            raise RuntimeError("config-3 overlapped passes disagree")
+        if fst and not np.array_equal(plans[0].read_fst(), plans[1].read_fst(), equal_nan=True):
+            raise RuntimeError("config-3 overlapped passes disagree (Fst)")
+        out[key] = {
+            "pipeline_GBs": bp / wo / 1e9, "pipeline_frac": bp / wo / 1e9 / HBM_PEAK_GBS, "pipeline_ms": wo * 1e3,
+            "windows_per_s": nwin / wo,
+            "note": ("T2D + T1D + Fst" if fst else "T2D + T1D only (the reference's statistics; Hudson Fst not computed)")
+                    + ": 2 plans on 2 HIP streams, passes overlapped, scan kernel capped at 1 workgroup per CU; "
+                      "SURVEY 8(d) bytes over the time per pass"}
+        for q in plans:
+            q.close()
     dev.close()
     return out
 
