@@ -475,24 +475,18 @@ __device__ __forceinline__ void cls_k2g(const KParams& P, uint32_t c, uint32_t& 
   gp = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(g, np) * (u16x2){(unsigned short)BS, (unsigned short)BS});
 }
 
-// k_scan_w: the same over the window [b, e) only: loads past the window's end return 0 (SNPs in no
-// spectrum, no called allele), so the rows need no masking
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t window_rows(const uint32_t* counts, uint32_t b, uint32_t e, uint32_t nm1) {
-  const uint32_t left = min(min(e, nm1 + 1u) - b, 0x3fffffffu);
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(counts + b), (short)0, (int)(left * 4u), 0x00020000);
-}
-
 // the per-SNP source of the scan kernels: the bins k_prep wrote, or (CNT) the counts, classified
 template <bool CNT>
 __device__ __forceinline__ uint32_t snp_word(const KParams& P, const uint32_t* __restrict__ src, uint32_t i) {
   return CNT ? cls_word(P, src[i]) : src[i];
 }
 
-// counts plans: a window's rows as a buffer resource based at its first SNP b, n - b words long (the
-// range check returns 0 past the data set's last SNP: no clamp, no per-row address arithmetic; the
-// rows sit in the loads' immediate offsets).  b is wave-uniform: the descriptor is scalar work.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t count_rows(const uint32_t* counts, uint32_t b, uint32_t nm1) {
-  const uint32_t left = min(nm1 + 1u - b, 0x3fffffffu);
+// counts plans: a window's rows as a buffer resource based at its first SNP b, covering [b, e) (and
+// not past the data set's last SNP): the range check returns 0 past the window's end -- an SNP in no
+// spectrum with no called allele -- so the rows need no masking, no clamp and no per-row address
+// arithmetic (the rows sit in the loads' immediate offsets).  b, e are wave-uniform: scalar work.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t window_rows(const uint32_t* counts, uint32_t b, uint32_t e, uint32_t nm1) {
+  const uint32_t left = min(min(e, nm1 + 1u) - b, 0x3fffffffu);
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(counts + b), (short)0, (int)(left * 4u), 0x00020000);
 }
 
@@ -1780,7 +1774,7 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
     }
     if (w.has) {   // the bins buffer has SCAN_PAD readable words past n (counts: buffer loads, 0 past n); masked in the last step
       if (CNT) {
-        const __amdgpu_buffer_rsrc_t rr = count_rows(bins, w.b, P.nm1);
+        const __amdgpu_buffer_rsrc_t rr = window_rows(bins, w.b, w.e, P.nm1);
 #pragma unroll
         for (int j = 0; j < 8; ++j) w.u[j] = __builtin_amdgcn_raw_buffer_load_b32(rr, lane * 4 + 256 * j, 0, 0);
       } else {
@@ -1931,8 +1925,12 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
     bool ovf = false;   // GL: some u8 bin of this lane wrapped
     uint32_t kw[8];   // the 2D words of the first 8 steps, cleared after the window
     auto pair = [&](uint32_t w0, uint32_t w1, int j, bool keep) {
-      w0 = 64 * j < lim ? w0 : 0u;   // SNPs past e are excluded (unconditional: cheaper than a guard)
-      w1 = 64 * (j + 1) < lim ? w1 : 0u;
+      // SNPs past e are excluded (unconditional: cheaper than a guard; CNT: the window-ranged loads
+      // returned 0 there)
+      if (!CNT) {
+        w0 = 64 * j < lim ? w0 : 0u;
+        w1 = 64 * (j + 1) < lim ? w1 : 0u;
+      }
       const uint32_t ww[2] = {w0, w1};   // (CNT: counts; 0 past e, in no spectrum)
       uint32_t rk[2], kk[2], ov[2], xs[2];
 #pragma unroll
@@ -1941,7 +1939,7 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
         uint32_t k2, g1, g2;
         if (CNT) cls_fields(P, w, k2, g1, g2);
         else { k2 = bin_k2(w); g1 = bin_g1(w); g2 = bin_g2(w); }
-        n2 += __popcll(__ballot(k2 != 0u));
+        n2 += 64u - (uint32_t)__popcll(__ballot(k2 == 0u));   // (the compare the selects below use)
         n1a += __popcll(__ballot(g1 != 0u));
         n1b += __popcll(__ballot(g2 != 0u));
         const uint32_t word = k2 ? (GL ? (k2 >> 2) : P16 ? (k2 >> 1) : k2) : trash;
@@ -1989,7 +1987,7 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
       if (64 * j < (int)nsnp) pair(cur.u[j], cur.u[j + 1], j, true);
     if (nsnp > 8 * WAVE) {
       if (CNT) {   // buffer loads (range-checked), rows masked in pair()
-        const __amdgpu_buffer_rsrc_t rr = count_rows(bins, cur.b, P.nm1);
+        const __amdgpu_buffer_rsrc_t rr = window_rows(bins, cur.b, cur.e, P.nm1);
         int vo = lane * 4 + 256 * 8;
         uint32_t x0 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo, 0, 0), x1 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo + 256, 0, 0);
         for (int j = 8; 64 * j < (int)nsnp; j += 2) {
@@ -2739,7 +2737,9 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     srn.y = __builtin_amdgcn_readfirstlane(srn.y);
     Win nxt;
     nxt.has = false;
+#ifndef SFS2D_LATE_PF
     if (more && fill) bounds(sn, srn, nxt);
+#endif
     MARK(24);
     // 1D spectra: one lane per folded inner bin reads (and clears) its R1 replicas; with <= 32 inner
     // bins per population, lanes 0-31 take population 1 and lanes 32-63 population 2 (acca)
@@ -2811,6 +2811,9 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       MARK(26);
       put(s, cur.b, nsnp, n2, n1a, n1b, nvar, nlast, s2, sa, sb, fq);
     }
+#ifdef SFS2D_LATE_PF
+    if (more && fill) bounds(sn, srn, nxt);
+#endif
     ++jb;
     group_sync<WAVE>();
     if (it == 0) STAMP(14);

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Config 3 (5e7 SNPs, 32 chromosomes, 20 kb, Fst) passes: one plan back to back vs S plans on S HIP
 streams (independent passes overlapping: one pass's bandwidth-bound k_prep beside the previous
-pass's compute-bound k_scan_w).  usage: python tools/exp_streams_cfg3.py [runs] [fst]"""
+pass's compute-bound k_scan_w).  usage: python tools/exp_streams_cfg3.py [runs] [fst|nofst] [scan workgroups per CU]"""
 import os
 import sys
 import time
@@ -17,12 +17,13 @@ from sfs2d.synth import synth_genome  # noqa: E402
 
 runs = int(sys.argv[1]) if len(sys.argv) > 1 else 24
 fst = len(sys.argv) > 2 and sys.argv[2] == "fst"
+cap = int(sys.argv[3]) if len(sys.argv) > 3 else 0
 p = synth_genome(32, 1_562_500, 25, 25, seed=777)
 eng = Engine.get(0)
 s0 = torch.cuda.Stream()
 eng.set_stream(s0.cuda_stream)
 dev = eng.upload(p)
-cfg = ScanConfig(n1p=25, n2p=25, window=20000, fst=fst)
+cfg = ScanConfig(n1p=25, n2p=25, window=20000, fst=fst, scan_wgs_per_cu=cap)
 plans = [eng.plan(dev, cfg) for _ in range(4)]
 streams = [s0.cuda_stream] + [torch.cuda.Stream().cuda_stream for _ in range(3)]
 nrec = plans[0].nrec
