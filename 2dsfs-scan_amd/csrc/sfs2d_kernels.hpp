@@ -1733,6 +1733,8 @@ __device__ __forceinline__ void fused_table(int nb2, int nh, int nt, int n1p, in
       leaves, nleaves, nodes, nnodes, nlevels, write_chrom, fsum, fst_out, ctr, cpar, leafsum, bg1d, sliced,  \
       gscr, nscr
 
+__device__ __forceinline__ void wave_sum3(double a, double b, double c, double& sa, double& sb, double& sc);
+
 template <bool P16, bool FUSED, bool FST, bool GL, bool CNT>
 __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
   static_assert(!(GL && FUSED), "k_scan_gw reads finished tables");
@@ -1775,8 +1777,12 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
     if (w.has) {   // the bins buffer has SCAN_PAD readable words past n (counts: buffer loads, 0 past n); masked in the last step
       if (CNT) {
         const __amdgpu_buffer_rsrc_t rr = window_rows(bins, w.b, w.e, P.nm1);
+        // (the lane's byte offset made opaque here: hoisted out of the window loop, the eight row offsets
+        // were kept live as eight VGPRs -- spilled elsewhere -- instead of one base + immediate offsets)
+        uint32_t lo = (uint32_t)lane * 4u;
+        asm volatile("" : "+v"(lo));
 #pragma unroll
-        for (int j = 0; j < 8; ++j) w.u[j] = __builtin_amdgcn_raw_buffer_load_b32(rr, lane * 4 + 256 * j, 0, 0);
+        for (int j = 0; j < 8; ++j) w.u[j] = __builtin_amdgcn_raw_buffer_load_b32(rr, (int)lo + 256 * j, 0, 0);
       } else {
         const uint32_t* q = bins + w.b + lane;
 #pragma unroll
@@ -1924,7 +1930,13 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
     uint32_t n2 = 0, nlast = 0, n1a = 0, n1b = 0, nvar = 0;
     bool ovf = false;   // GL: some u8 bin of this lane wrapped
     uint32_t kw[8];   // the 2D words of the first 8 steps, cleared after the window
-    auto pair = [&](uint32_t w0, uint32_t w1, int j, bool keep) {
+    // A pair of rows in two halves, software-pipelined as in k_scan_w: issue() classifies, issues the
+    // LDS atomics and (GL) the lp loads from the global table; finish() turns the returned ranks and lp
+    // into D(r) - lp_k.  The loops issue pair j before they finish pair j - 2: a pair's atomics and its
+    // L2 round trip for lp return under the next pair's work.
+    struct PairSt { uint32_t ov[2], xs[2], kk[2]; double lp[2]; };
+    auto issue = [&](uint32_t w0, uint32_t w1, int j, bool keep) {
+      PairSt st;
       // SNPs past e are excluded (unconditional: cheaper than a guard; CNT: the window-ranged loads
       // returned 0 there)
       if (!CNT) {
@@ -1932,7 +1944,6 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
         w1 = 64 * (j + 1) < lim ? w1 : 0u;
       }
       const uint32_t ww[2] = {w0, w1};   // (CNT: counts; 0 past e, in no spectrum)
-      uint32_t rk[2], kk[2], ov[2], xs[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const uint32_t w = ww[q];
@@ -1942,6 +1953,7 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
         n2 += 64u - (uint32_t)__popcll(__ballot(k2 == 0u));   // (the compare the selects below use)
         n1a += __popcll(__ballot(g1 != 0u));
         n1b += __popcll(__ballot(g2 != 0u));
+        if (GL) st.lp[q] = LPl[k2];   // (the global table; bin 0 is not zeroed there: finish selects 0)
         const uint32_t word = k2 ? (GL ? (k2 >> 2) : P16 ? (k2 >> 1) : k2) : trash;
         // the byte / half's shift: the hardware reads shift operands' low five bits, so k2 << 3 (GL)
         // or k2 << 4 serves without a mask (the bins word's low bits are k2's)
@@ -1949,22 +1961,26 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
         const uint32_t sh = GL ? (wk << 3) : P16 ? (wk << 4) : 0u;
         uint32_t one2 = 1u;
         if (GL || P16) asm("v_lshlrev_b32 %0, %1, 1" : "=v"(one2) : "v"(sh));
-        ov[q] = atomicAdd(&W[word], k2 ? one2 : 0u);
-        xs[q] = sh;
-        kk[q] = k2;
+        st.ov[q] = atomicAdd(&W[word], k2 ? one2 : 0u);
+        st.xs[q] = sh;
+        st.kk[q] = k2;
         if (keep) kw[(j + q) & 7] = word;
         const uint32_t u1 = g1 ? a1b + g1 * (4u * RG) : atr, u2 = g2 ? a2b + g2 * (4u * RG) : atr;
         __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u1, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u2, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
+      return st;
+    };
+    auto finish = [&](const PairSt& st) {
+      uint32_t rk[2];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {   // ranks after both SNPs' atomics are issued
+      for (int q = 0; q < 2; ++q) {
         if (GL) {   // (the trash word's low byte counts 1D increments: excluded SNPs take rank 0)
-          const uint32_t r = __builtin_amdgcn_ubfe(ov[q], xs[q], 8);
-          rk[q] = kk[q] ? r : 0u;
-          ovf |= (kk[q] != 0u) & (r == 255u);
+          const uint32_t r = __builtin_amdgcn_ubfe(st.ov[q], st.xs[q], 8);
+          rk[q] = st.kk[q] ? r : 0u;
+          ovf |= (st.kk[q] != 0u) & (r == 255u);
         } else {
-          rk[q] = P16 ? __builtin_amdgcn_ubfe(ov[q], xs[q], 16) : (kk[q] ? ov[q] : 0u);
+          rk[q] = P16 ? __builtin_amdgcn_ubfe(st.ov[q], st.xs[q], 16) : (st.kk[q] ? st.ov[q] : 0u);
         }
       }
       double d[2], lp[2];
@@ -1973,18 +1989,23 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
         if (GL) {   // D(r) for r < 64 from the lanes' registers, the global table beyond
           d[q] = __shfl(Dreg, (int)(rk[q] & 63u));
           if (rk[q] >= 64u) d[q] = Dt[min(rk[q], (uint32_t)LNT - 1u)];
+          lp[q] = st.kk[q] ? st.lp[q] : 0.0;
         } else {
           d[q] = Dt[min(rk[q], (uint32_t)LNT - 1u)];   // D[LNT-1] = 0: ranks past the table add 0
+          lp[q] = LPl[st.kk[q]];
         }
-        lp[q] = LPl[kk[q]];
-        if (GL && !kk[q]) lp[q] = 0.0;   // (the global table's bin 0 is not zeroed)
       }
 #pragma unroll
       for (int q = 0; q < 2; ++q) acc2 += d[q] - lp[q];
     };
+    PairSt pend;   // the issued pair not yet finished (every window has >= 1 SNP: pair 0 runs)
 #pragma unroll
     for (int j = 0; j < 8; j += 2)
-      if (64 * j < (int)nsnp) pair(cur.u[j], cur.u[j + 1], j, true);
+      if (64 * j < (int)nsnp) {
+        const PairSt st = issue(cur.u[j], cur.u[j + 1], j, true);
+        if (j > 0) finish(pend);
+        pend = st;
+      }
     if (nsnp > 8 * WAVE) {
       if (CNT) {   // buffer loads (range-checked), rows masked in pair()
         const __amdgpu_buffer_rsrc_t rr = window_rows(bins, cur.b, cur.e, P.nm1);
@@ -1995,7 +2016,9 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
           vo += 512;
           x0 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo, 0, 0);   // one pair ahead
           x1 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo + 256, 0, 0);
-          pair(w0, w1, j, false);
+          const PairSt st = issue(w0, w1, j, false);
+          finish(pend);
+          pend = st;
         }
       } else {
         const uint32_t* qb = bins + cur.b + lane;
@@ -2004,10 +2027,13 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
           const uint32_t w0 = x0, w1 = x1;
           x0 = 64 * (j + 2) < lim ? qb[64 * (j + 2)] : 0u;   // one pair ahead
           x1 = 64 * (j + 3) < lim ? qb[64 * (j + 3)] : 0u;
-          pair(w0, w1, j, false);
+          const PairSt st = issue(w0, w1, j, false);
+          finish(pend);
+          pend = st;
         }
       }
     }
+    finish(pend);
     if (!P.fold || filt) {   // rare settings: unfolded (SNPs in the excluded last 2D bin), variant_type filter
       for (uint32_t i0 = cur.b; i0 < cur.e; i0 += WAVE) {   // wave-uniform trip count
         const uint32_t w = i0 + lane < cur.e ? snp_word<CNT>(P, bins, i0 + lane) : 0u;
@@ -2077,7 +2103,7 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
     if (half1d) {
       wave_sum_dpp_halves(acc2, acca, s2, sa, sb);
     } else {
-      s2 = wave_sum_dpp(acc2); sa = wave_sum_dpp(acca); sb = wave_sum_dpp(accb);
+      wave_sum3(acc2, acca, accb, s2, sa, sb);
     }
     WinOut w;
     w.snp_count = nvar; w.n2_all = n2 + nlast; w.n2 = n2; w.n1a = n1a; w.n1b = n1b;
@@ -2243,6 +2269,27 @@ __device__ __forceinline__ double wave_sum5(double a, double h, double f1, doubl
   return z;
 }
 
+// three fp64 wave sums (k_scan_gw's 2D and two whole-wave 1D sums), reduce-scatter as wave_sum5: a, b
+// exchanged in one lane swap (lanes 0-31 then hold a's partials, 32-63 b's), c folded in both halves,
+// one 16-lane swap (rows: a, c, b, c), DPP row steps, three readlanes -- ~27 VALU instructions instead of
+// ~69 for three wave_sum_dpp
+__device__ __forceinline__ void wave_sum3(double a, double b, double c, double& sa, double& sb, double& sc) {
+  double x, y;
+  swap32_pair(a, b, x, y);
+  const double r1 = x + y;
+  swap32_pair(c, c, x, y);
+  const double r2 = x + y;
+  swap16_pair(r1, r2, x, y);
+  double q = x + y;
+  q += mdpp_d<0xB1>(q);    // quad_perm [1,0,3,2]
+  q += mdpp_d<0x4E>(q);    // quad_perm [2,3,0,1]
+  q += mdpp_d<0x124>(q);   // row_ror:4
+  q += mdpp_d<0x128>(q);   // row_ror:8
+  sa = readlane_d(q, 0);
+  sc = readlane_d(q, 16);
+  sb = readlane_d(q, 32);
+}
+
 // v_writelane_b32 (the LLVM intrinsic: this clang has no builtin for it): lane l (uniform) of `old`
 // takes the uniform value v; the compiler puts the lane select in M0
 extern "C" __device__ int sfs2d_llvm_writelane(int v, int l, int old) __asm("llvm.amdgcn.writelane.i32");
@@ -2328,8 +2375,12 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       const uint32_t* q = bins + w.b;
       if (CNT) {   // counts, no padding past n: range-checked buffer loads (0 past n; masked later)
         const __amdgpu_buffer_rsrc_t rr = window_rows(bins, w.b, w.e, P.nm1);
+        // (the lane's byte offset made opaque here: hoisted out of the window loop, the eight row offsets
+        // were kept live as eight VGPRs -- spilled elsewhere -- instead of one base + immediate offsets)
+        uint32_t lo = (uint32_t)lane * 4u;
+        asm volatile("" : "+v"(lo));
 #pragma unroll
-        for (int j = 0; j < 8; ++j) w.u[j] = __builtin_amdgcn_raw_buffer_load_b32(rr, lane * 4 + 256 * j, 0, 0);
+        for (int j = 0; j < 8; ++j) w.u[j] = __builtin_amdgcn_raw_buffer_load_b32(rr, (int)lo + 256 * j, 0, 0);
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) w.u[j] = q[(uint32_t)lane + 64u * j];
@@ -2352,12 +2403,27 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
 
   // table copies with every load of a thread in flight at once (a load-wait-store loop paid one
   // L2/MALL round trip per element: ~4 us of config 2's ~10)
-  lds_copy_d(Dt, dfg, 2 * LNT);
+  // the prologue's global loads in flight together (each dependent round trip to L2 / MALL cost ~1 us
+  // of config 2's ~4 us prologue): the D / F tables (two doubles per thread), and for sliced plans the
+  // leaf sums, the tree nodes and the head's inputs, then the lp table
+  static_assert(2 * LNT == 2 * SBLOCK, "two D / F doubles per thread");
+  const double dfv0 = dfg[tid], dfv1 = dfg[tid + SBLOCK];
   BgHead hb;
   const size_t rs = (size_t)P.nchrom * P.nh;     // replica stride
   const uint32_t* Rc = repl + (size_t)par * REPL * rs + (size_t)ch.chrom * P.nh;
   if (!FUSED) {
+    double lsv = 0.0;
+    int4 my_node = make_int4(0, 0, -1, 0);
+    uint32_t bc = 0u;
+    Bg1D o{};
+    if (sliced) {
+      if (tid < nleaves) lsv = leafsum[(size_t)bg * nleaves + tid];
+      if (tid < nnodes) my_node = nodes[tid];
+      if (tid == 0) { bc = bcount[(size_t)par * P.nchrom + bg]; o = bg1d[bg]; }
+    }
     lds_copy_d(LPl, LPg + (size_t)bg * P.nt, P.nt);
+    Dt[tid] = dfv0;
+    Dt[tid + SBLOCK] = dfv1;
     if (sliced) {
       // this run's per-chromosome table from k_bg_slice (proportions, logs, 1D part final) and its
       // leaf sums: numpy's tree over the leaves, then scipy's p[-1] rule on the 2D table -- the
@@ -2365,16 +2431,14 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       // completion step between the kernels).  Scratch: the histogram area (zeroed below).
       const bool writer = ch.first == 0 && (int)ch.chrom == write_chrom;
       double* lsum = reinterpret_cast<double*>(HB);
-      if (tid < nleaves) lsum[tid] = leafsum[(size_t)bg * nleaves + tid];
-      const int4 my_node = tid < nnodes ? nodes[tid] : make_int4(0, 0, -1, 0);
+      if (tid < nleaves) lsum[tid] = lsv;
       __syncthreads();
       for (int l = 0; l < nlevels; ++l) {
         if (my_node.z == l) lsum[nleaves + tid] = lsum[my_node.x] + lsum[my_node.y];
         __syncthreads();
       }
       if (tid == 0) {
-        const double B2 = (double)bcount[(size_t)par * P.nchrom + bg];
-        const Bg1D o = bg1d[bg];
+        const double B2 = (double)bc;
         uint32_t flags = o.flags;
         if (B2 == 0.0) flags |= BGF_B2_ZERO;
         const int M2 = P.nb2 - 2;
@@ -2402,6 +2466,8 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       hb = head[bg];
     }
   } else {
+    Dt[tid] = dfv0;
+    Dt[tid + SBLOCK] = dfv1;
     fused_table(P.nb2, P.nh, P.nt, P.n1p, P.n2p, P.n1, P.n2, P.t1a, P.t1b, P.nchrom, ch.chrom,
                 ch.first == 0 && (int)ch.chrom == write_chrom, bg,
                 Rc, rs, repl, bcount, par, tab, LPg, head, LPl, HB, leaves, nleaves, nodes, nnodes, nlevels, lnx,
