@@ -782,7 +782,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
       // k_scan_w: lp table (even-rounded) + D + F tables, then 8 per-wave histogram blocks (also the
       // fused prologue's scratch: u1 words, 1D proportions, leaf accumulators and sums)
       const int h2w = pl->p16 ? (((K.nb2 + 1) / 2 + 3) & ~3) : ((K.nb2 + 3) & ~3);
-      const int per = h2w + R1 * (K.n1p + 1) + R1 * (K.n2p + 1) + TRASH;
+      const int per = h2w + R1 * (K.n1p + 1) + R1 * (K.n2p + 1);   // (no trash words: scan_w_small)
       const size_t hist_words = std::max<size_t>((size_t)(SBLOCK / WAVE) * per, (size_t)FUSED_VCNT + K.nt + 16);
       pl->scan_lds = sizeof(double) * (size_t)(((K.nt + 1) & ~1) + 2 * LNT) + hist_words * 4;
       // with the static LDS of the variant that uses most (the batched finish's per-wave arrays, Fst);

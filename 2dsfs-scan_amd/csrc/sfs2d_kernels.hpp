@@ -2330,7 +2330,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   constexpr bool FSTIN = FST == 2;
   static_assert(!FSTIN || CNT, "Fst in the scan reads the counts");
   constexpr int NWV = SBLOCK / WAVE;
-  constexpr int SB = 4;    // windows per batch (see flush; LDS-limited)
+  constexpr int SB = 8;    // windows per batch (see flush; LDS-limited: the 2 KB of the retired trash words)
   __shared__ BgHead sh_hb;
   __shared__ double sh_bd[NWV][3][SB];      // batch: the three sums of window j
   __shared__ uint32_t sh_bu[NWV][5][SB];    // batch: slot, begin, n2 | n2_all, n1a | n1b, nsnp | nvar
@@ -2353,7 +2353,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   uint32_t* HB = reinterpret_cast<uint32_t*>(Ft + LNT);
   const int h2w = P16 ? ((P.nb2 + 1) / 2 + 3) & ~3 : (P.nb2 + 3) & ~3;
   const int h1w = R1 * (P.n1p + 1), h1wb = R1 * (P.n2p + 1);
-  const int per = h2w + h1w + h1wb + TRASH;
+  const int per = h2w + h1w + h1wb;   // (no trash words: SNPs outside the 2D SFS skip the atomic)
   uint32_t* W = HB + wv * per;
   uint32_t* H1a = W + h2w;
   uint32_t* H1b = H1a + h1w;
@@ -2494,13 +2494,14 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   const bool nan2 = hb.flags & BGF_NAN2, nan1a = hb.flags & BGF_NAN1A, nan1b = hb.flags & BGF_NAN1B;
   uint32_t* const H1a_l = H1a + rep;   // this lane's replica column of the 1D histograms
   uint32_t* const H1b_l = H1b + rep;
-  const uint32_t trash = (uint32_t)(h2w + h1w + h1wb + lane);   // the lane's trash word (index from W)
   const uint32_t one1 = P16 ? 0x10000u : 1u;   // 1D increment (P16: upper halves, see the window loop)
   // the 1D atomics' LDS byte addresses: per-lane bases kept opaque, so that a bin's address is one
   // v_lshl_add (the compiler otherwise re-splits base + replica + bin into three operations)
   typedef __attribute__((address_space(3))) uint32_t lds_u32;
   uint32_t a1b = (uint32_t)(uintptr_t)((lds_u32*)H1a_l), a2b = (uint32_t)(uintptr_t)((lds_u32*)H1b_l);
   asm volatile("" : "+v"(a1b), "+v"(a2b));
+  uint32_t awb = (uint32_t)(uintptr_t)((lds_u32*)W);   // the wave's 2D words (LDS byte address, uniform)
+  asm volatile("" : "+s"(awb));
   // ---- batched finish.  Lane j of the B* registers holds the j-th window this wavefront has
   // scanned since the last flush (slot, SNP range, counts, the three sums); per window only the
   // sums' wave reductions run, and the T values, the zero / NaN rules, the Fst value and the 64-B
@@ -2649,9 +2650,8 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     // SNP adds D(r) - lp_k (telescoping: sum_k x_k ln x_k = sum_i D(r_i)); the folded 1D bins are
     // counted in lane & 3 replicas, every SNP slot in one bin of each (the excluded bins 0 and n_p too:
     // dropped at the window's end, which derives n1a / n1b from them).  An SNP outside the 2D spectrum
-    // adds 0 to the lane's own trash word (a shared word instead -- bin (0,0) -- cost 60% more LDS
-    // bank-conflict cycles), whose low half stays 0 and gives rank 0, D(0) = 0, LPl[0] = 0.  n2 is a
-    // wave-uniform ballot count.
+    // skips the 2D atomic and takes rank 0: D(0) = 0, LPl[0] = 0 (it used to add 0 to a lane-private
+    // trash word: 2 KB of LDS per workgroup, now the batch's).  n2 is a wave-uniform ballot count.
     const uint32_t nsnp = cur.e - cur.b;
     const int lim = (int)nsnp - lane;
     const bool clampd = nsnp > (uint32_t)(LNT - 1);   // some rank may pass the D table
@@ -2676,19 +2676,27 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     auto pair = [&](uint32_t w0, uint32_t w1, int j, bool keep, const double2 (&fq)[4]) {
       const uint32_t ww[2] = {w0, w1};   // (CNT: counts)
       uint32_t rk[2], kk[2], ov[2], xs[2];
+      bool in2[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const uint32_t w = ww[q];
         uint32_t k2, gp;   // gp: the folded 1D bins of both populations (u16 pair; excluded ones included)
         if (CNT) cls_k2g<4 * R1>(P, w, k2, gp);
         else { k2 = bin_k2(w); gp = (bin_g1(w) | (bin_g2(w) << 16)) * (4u * R1); }
-        n2 += 64u - (uint32_t)__popcll(__ballot(k2 == 0u));   // (the compare the selects below use)
+        in2[q] = k2 != 0u;   // (one compare: the ballot, the atomic's exec mask, the rank's select)
+        n2 += __popcll(__ballot(in2[q]));
         const uint32_t x = (CNT ? k2 : w) << 4;   // low five bits: (k2 & 1) << 4, the u16 half's shift
-        const uint32_t word = k2 ? (P16 ? (k2 >> 1) : k2) : trash;
+        const uint32_t word = P16 ? (k2 >> 1) : k2;   // (k2 = 0: word 0, cleared after the window anyway)
         // (v_lshlrev_b32 / v_bfe_u32 read the shift's low five bits: no mask; C's << would need one)
         uint32_t one2 = 1u;
         if (P16) asm("v_lshlrev_b32 %0, %1, 1" : "=v"(one2) : "v"(x));
-        ov[q] = atomicAdd(&W[word], k2 ? one2 : 0u);
+        // an SNP outside the 2D SFS skips the atomic (exec mask; its rank is 0 below): no trash word,
+        // fewer lanes in the LDS atomic.  (The address before the branch: one v_lshl_add.)
+        const uint32_t wa = awb + word * 4u;
+        uint32_t o = one2;   // (any value: lanes outside take rank 0; one2's register, dead after the atomic)
+        if (in2[q])
+          o = __hip_atomic_fetch_add((lds_u32*)(uintptr_t)wa, one2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        ov[q] = o;
         xs[q] = x;
         kk[q] = k2;
         if (keep) kw[(j + q) & 7] = word;
@@ -2712,7 +2720,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       // the ranks once both SNPs' atomics are issued (extracted right after its own atomic, each rank's
       // wait held the other SNP's work back: two LDS round trips per pair instead of one)
 #pragma unroll
-      for (int q = 0; q < 2; ++q) rk[q] = P16 ? __builtin_amdgcn_ubfe(ov[q], xs[q], 16) : (kk[q] ? ov[q] : 0u);
+      for (int q = 0; q < 2; ++q) rk[q] = in2[q] ? (P16 ? __builtin_amdgcn_ubfe(ov[q], xs[q], 16) : ov[q]) : 0u;
       double d[2], lp[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
