@@ -119,6 +119,11 @@ struct sfs2d_data {
   std::vector<uint32_t> host_pos;   // upload path only: exact window-length bound for u16 bins
   bool ann_owned = false;
   bool strict = true;   // positions strictly increasing within each chromosome
+  // the largest called allele counts r + a of population 1 / 2 over the data set: counts plans with a
+  // supplied background run no pass that validates the counts (k_prep reads none), so they need
+  // max_nc1 <= n1 and max_nc2 <= n2 -- then no SNP can raise KeyError (a > 2 pop_size) or leave the
+  // grid after the fold; otherwise the plan takes the bins pipeline, whose k_prep raises the error
+  uint32_t max_nc1 = 0xffffffffu, max_nc2 = 0xffffffffu;
 };
 
 struct sfs2d_plan {
@@ -533,6 +538,16 @@ int sfs2d_data_upload(sfs2d_ctx* ctx, const uint32_t* counts, const uint32_t* po
   }
   d->last_pos.assign(nchrom, 0);
   d->host_pos.assign(pos, pos + n);
+  {
+    uint32_t m1 = 0, m2 = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      const uint32_t c = counts[i];
+      m1 = std::max(m1, (c & 0xffu) + ((c >> 8) & 0xffu));
+      m2 = std::max(m2, ((c >> 16) & 0xffu) + (c >> 24));
+    }
+    d->max_nc1 = m1;
+    d->max_nc2 = m2;
+  }
   for (int c = 0; c < nchrom; ++c) {
     int64_t s = d->chrom_off[c], t = d->chrom_off[c + 1];
     if (t > s) d->last_pos[c] = pos[t - 1];
@@ -572,6 +587,29 @@ int sfs2d_data_wrap_device(sfs2d_ctx* ctx, const uint32_t* d_counts, const uint3
   }
   d->last_pos.assign(chrom_last_pos, chrom_last_pos + nchrom);
   d->strict = true;   // contract: positions strictly increasing within each chromosome
+  if (n > 0) {   // the largest called counts (see max_nc1), one pass over the caller's counts
+    uint32_t* d_m = nullptr;
+    uint32_t hm[2] = {0, 0};
+    hipError_t e = hipMalloc((void**)&d_m, 2 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemsetAsync(d_m, 0, 2 * sizeof(uint32_t), CTX_STREAM(ctx));
+    if (e == hipSuccess) {
+      const unsigned grid = (unsigned)std::min<int64_t>(4096, (n + 1023) / 1024);
+      hipLaunchKernelGGL(k_max_called, dim3(grid), dim3(256), 0, CTX_STREAM(ctx), d->counts, (unsigned long long)n, d_m);
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(hm, d_m, sizeof(hm), hipMemcpyDeviceToHost, CTX_STREAM(ctx));
+    if (e == hipSuccess) e = hipStreamSynchronize(CTX_STREAM(ctx));
+    hipFree(d_m);
+    if (e != hipSuccess) {
+      if (d->ann_owned) hipFree(d->ann);
+      hipFree(d->d_chrom_off); delete d;
+      return set_err(ctx, SFS2D_E_HIP, std::string("wrap_device: ") + hipGetErrorString(e));
+    }
+    d->max_nc1 = hm[0];
+    d->max_nc2 = hm[1];
+  } else {
+    d->max_nc1 = d->max_nc2 = 0;
+  }
   *out = d;
   return 0;
 }
@@ -633,6 +671,8 @@ int sfs2d_data_synth_sims(sfs2d_ctx* ctx, const sfs2d_synth_params* sp, const ui
   }
   d->last_pos.assign(sp->n_replicates, sp->n_windows * sp->window_bp);   // upper bound: trailing slots stay empty
   d->strict = true;
+  d->max_nc1 = 2u * (uint32_t)sp->n1p;   // k_synth_sims: ref + alt + missing = 2 pop_size
+  d->max_nc2 = 2u * (uint32_t)sp->n2p;
   *out = d;
   return 0;
 }
@@ -727,6 +767,12 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   // SFS2D_CNT=0 forces the bins pipeline (comparison)
   pl->cnt = prm->ann_want < 0 && !prm->has_start && !prm->has_end;
   if (const char* ev = std::getenv("SFS2D_CNT")) pl->cnt = pl->cnt && ev[0] != '0';
+  // a supplied background: no k_prep pass reads (and validates) the counts of a counts plan, so one is
+  // taken only when no SNP can raise an error (max_nc1 / max_nc2); else the bins pipeline's k_prep
+  // classifies every SNP and reports KeyError / out-of-grid keys as the reference raises them
+  if (pl->cnt && prm->bg_mode != SFS2D_BG_PER_CHROM &&
+      !(data->max_nc1 <= (uint32_t)K.n1 && data->max_nc2 <= (uint32_t)K.n2))
+    pl->cnt = false;
   pl->K.nm1 = data->n > 0 ? (uint32_t)(data->n - 1) : 0u;
   pl->K.kmul = (uint32_t)(pl->K.n2 + 1) | (1u << 16);
   pl->K.n12 = (uint32_t)pl->K.n1 | ((uint32_t)pl->K.n2 << 16);
@@ -1318,6 +1364,44 @@ int sfs2d_plan_bg_exchange(sfs2d_plan* pl, uint32_t* host_repl, uint32_t* host_s
   return 0;
 }
 
+int sfs2d_plan_bg_rows_dev(sfs2d_plan* pl, int64_t* d_rows, int64_t row_stride) {
+  if (!pl) return SFS2D_E_ARG;
+  sfs2d_ctx* ctx = pl->ctx;
+  if (!pl->do_bg) return set_err(ctx, SFS2D_E_ARG, "plan has no per-chromosome backgrounds");
+  if (pl->base) return set_err(ctx, SFS2D_E_ARG, "exchange the base plan's backgrounds");
+  const int W = pl->K.h1b + pl->K.n2 + 2;
+  if (!d_rows || row_stride < W) return set_err(ctx, SFS2D_E_ARG, "rows: null or stride < SFS2D_BG_ROW_WORDS");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const int nc = pl->data->nchrom;
+  if (nc == 0) return 0;
+  const size_t rs = (size_t)nc * pl->K.nh;
+  hipLaunchKernelGGL(k_bg_rows_get, dim3((unsigned)((W + 255) / 256), (unsigned)nc), dim3(256), 0, CTX_STREAM(ctx), pl->K,
+                     pl->d_repl + (size_t)repl_par(pl) * REPL * rs, (unsigned long long)rs,
+                     pl->d_bcount + (size_t)plan_par(pl) * pl->K.nchrom, (long long*)d_rows, (long long)row_stride);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
+int sfs2d_plan_bg_rows_set_dev(sfs2d_plan* pl, const int64_t* d_rows, int64_t row_stride) {
+  if (!pl) return SFS2D_E_ARG;
+  sfs2d_ctx* ctx = pl->ctx;
+  if (!pl->do_bg) return set_err(ctx, SFS2D_E_ARG, "plan has no per-chromosome backgrounds");
+  if (pl->base) return set_err(ctx, SFS2D_E_ARG, "exchange the base plan's backgrounds");
+  const int W = pl->K.h1b + pl->K.n2 + 2;
+  if (!d_rows || row_stride < W) return set_err(ctx, SFS2D_E_ARG, "rows: null or stride < SFS2D_BG_ROW_WORDS");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const int nc = pl->data->nchrom;
+  if (nc == 0) return 0;
+  const size_t rs = (size_t)nc * pl->K.nh;
+  const int nk = std::max(W, pl->K.nh);
+  hipLaunchKernelGGL(k_bg_rows_set, dim3((unsigned)((nk + 255) / 256), (unsigned)nc), dim3(256), 0, CTX_STREAM(ctx), pl->K,
+                     pl->d_repl + (size_t)repl_par(pl) * REPL * rs, (unsigned long long)rs,
+                     pl->d_bcount + (size_t)plan_par(pl) * pl->K.nchrom, (const long long*)d_rows, (long long)row_stride,
+                     pl->d_err);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
 int sfs2d_plan_fst_buffer(sfs2d_plan* pl, void** dev_ptr, int64_t* nslots) {
   if (!pl || !dev_ptr || !nslots) return SFS2D_E_ARG;
   if (!pl->fst) return set_err(pl->ctx, SFS2D_E_ARG, "plan was created without SFS2D_F_FST");
@@ -1347,6 +1431,7 @@ int sfs2d_plan_check(sfs2d_plan* pl) {
   if (e) {
     HIPCHK(ctx, hipMemsetAsync(pl->d_err, 0, 4, CTX_STREAM(ctx)));
     HIPCHK(ctx, hipStreamSynchronize(CTX_STREAM(ctx)));
+    if (e & ERR_OVF) return set_err(ctx, SFS2D_E_ARG, "summed background histograms overflow uint32");
     if (e & ERR_KEY) return set_err(ctx, SFS2D_E_KEY, "allele count above 2*pop_size (reference: KeyError in calculate_1d_sfs)");
     return set_err(ctx, SFS2D_E_GRID, "folded 2D bin outside the (2n1+1)x(2n2+1) grid");
   }
@@ -1513,9 +1598,23 @@ int sfs2d_plan_attach(sfs2d_plan* base, const sfs2d_params* prm, sfs2d_plan** ou
   return 0;
 }
 
+static int bg_hist_impl(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* prm, int32_t chrom, int64_t* h2d,
+                        int64_t* h1a, int64_t* h1b, int64_t* d_row);
+
 int sfs2d_bg_hist(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* prm, int32_t chrom, int64_t* h2d,
                   int64_t* h1a, int64_t* h1b) {
   if (!ctx || !data || !prm || !h2d || !h1a || !h1b) return set_err(ctx, SFS2D_E_ARG, "null argument");
+  return bg_hist_impl(ctx, data, prm, chrom, h2d, h1a, h1b, nullptr);
+}
+
+int sfs2d_bg_hist_dev(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* prm, int32_t chrom, int64_t* d_row) {
+  if (!ctx || !data || !prm || !d_row) return set_err(ctx, SFS2D_E_ARG, "null argument");
+  return bg_hist_impl(ctx, data, prm, chrom, nullptr, nullptr, nullptr, d_row);
+}
+
+// d_row: the histograms as one device row (k_bg_rows_get's layout) instead of host arrays
+static int bg_hist_impl(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* prm, int32_t chrom, int64_t* h2d,
+                        int64_t* h1a, int64_t* h1b, int64_t* d_row) {
   if (chrom < -1 || chrom >= data->nchrom) return set_err(ctx, SFS2D_E_ARG, "chrom out of range");
   HIPCHK(ctx, hipSetDevice(ctx->device));
   KParams K;
@@ -1555,7 +1654,14 @@ int sfs2d_bg_hist(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* pr
       hipFuncSetAttribute((const void*)k_prep<true, false, true, false, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.bg_lds),
       hipFuncSetAttribute((const void*)k_prep<true, false, true, false, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.bg_lds);
     if (e == hipSuccess) e = launch_prep(&pl, false);
-    if (e == hipSuccess) e = hipMemcpyAsync(hist.data(), pl.d_repl, sizeof(uint32_t) * REPL * K.nh, hipMemcpyDeviceToHost, CTX_STREAM(ctx));
+    if (e == hipSuccess && d_row) {
+      const int W = K.h1b + K.n2 + 2;
+      hipLaunchKernelGGL(k_bg_rows_get, dim3((unsigned)((W + 255) / 256), 1u), dim3(256), 0, CTX_STREAM(ctx), pl.K,
+                         pl.d_repl, (unsigned long long)K.nh, pl.d_bcount, (long long*)d_row, (long long)W);
+      e = hipGetLastError();
+    } else if (e == hipSuccess) {
+      e = hipMemcpyAsync(hist.data(), pl.d_repl, sizeof(uint32_t) * REPL * K.nh, hipMemcpyDeviceToHost, CTX_STREAM(ctx));
+    }
     uint32_t err = 0;
     if (e == hipSuccess) e = hipMemcpyAsync(&err, pl.d_err, 4, hipMemcpyDeviceToHost, CTX_STREAM(ctx));
     if (e == hipSuccess) e = hipStreamSynchronize(CTX_STREAM(ctx));
@@ -1565,7 +1671,7 @@ int sfs2d_bg_hist(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* pr
   hipFree(pl.d_tiles); hipFree(pl.d_repl); hipFree(pl.d_err); hipFree(pl.d_bcount);
   pl.d_tiles = nullptr; pl.d_repl = nullptr; pl.d_err = nullptr; pl.d_bcount = nullptr;
   if (e != hipSuccess) return set_err(ctx, SFS2D_E_HIP, std::string("bg_hist: ") + hipGetErrorString(e));
-  if (rc) return rc;
+  if (rc || d_row) return rc;
   for (int k = 0; k < K.h1b + K.n2 + 1; ++k) {
     int64_t s = 0;
     for (int r = 0; r < REPL; ++r) s += hist[(size_t)r * K.nh + k];

@@ -92,7 +92,7 @@ __device__ __forceinline__ uint32_t take_replicas(uint32_t* p, uint32_t shift) {
 }
 constexpr int FUSED_VCNT = 2 * (1536 + 256) + 16;   // k_scan_w fused prologue: word offset of the counts
 
-enum : uint32_t { ERR_KEY = 1u, ERR_GRID = 2u };
+enum : uint32_t { ERR_KEY = 1u, ERR_GRID = 2u, ERR_OVF = 4u };   // OVF: summed background rows >= 2^32
 enum : uint32_t {
   BGF_B2_ZERO = 1u, BGF_B1A_ZERO = 2u, BGF_B1B_ZERO = 4u, BGF_NAN2 = 8u, BGF_NAN1A = 16u, BGF_NAN1B = 32u,
   BGF_FLOATV = 64u
@@ -518,6 +518,70 @@ __global__ void k_init_lnx(double* lnx, double* dtab, double* ftab, double* rtab
     dtab[i] = i < LNT - 1 ? b - a : 0.0;
     ftab[i] = a;
   }
+}
+
+// the largest called allele counts r1 + a1 / r2 + a2 over a data set (sfs2d_data_wrap_device: whether a
+// counts plan may skip validating the counts); m[2] zeroed by the caller
+__global__ __launch_bounds__(256) void k_max_called(const uint32_t* __restrict__ counts, unsigned long long n,
+                                                    uint32_t* __restrict__ m) {
+  uint32_t m1 = 0, m2 = 0;
+  for (unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (unsigned long long)gridDim.x * 256) {
+    const uint32_t c = counts[i];
+    m1 = max(m1, __builtin_amdgcn_udot4(c, 0x00000101u, 0u, false));
+    m2 = max(m2, __builtin_amdgcn_udot4(c, 0x01010000u, 0u, false));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    m1 = max(m1, (uint32_t)__shfl_xor((int)m1, o, WAVE));
+    m2 = max(m2, (uint32_t)__shfl_xor((int)m2, o, WAVE));
+  }
+  if ((threadIdx.x & (WAVE - 1)) == 0) {
+    atomicMax(&m[0], m1);
+    atomicMax(&m[1], m2);
+  }
+}
+
+// ------------------------------------------------------------------------------------------ background rows
+// A plan's per-chromosome background histograms as int64 rows (the multi-GPU exchange, sfs2d/dist.py):
+// row c = [nb2 2D bins | n1+1 unfolded pop-1 | n2+1 unfolded pop-2 | inner 2D sum] = SFS2D_BG_ROW_WORDS.
+// get: the REPL replicas of this run's k_prep pass summed (read only); set: the summed rows of every
+// rank back into replica 0 (the others and the padding zeroed) and the inner sums, before the scan.
+// Grid (ceil(W / 256), nchrom).
+__global__ __launch_bounds__(256) void k_bg_rows_get(KParams P, const uint32_t* __restrict__ repl, unsigned long long rs,
+                                                     const uint32_t* __restrict__ bsum, long long* __restrict__ rows,
+                                                     long long stride) {
+  const int c = blockIdx.y, k = blockIdx.x * 256 + threadIdx.x;
+  const int W = P.h1b + P.n2 + 2;
+  if (k >= W) return;
+  long long v;
+  if (k == W - 1) {
+    v = (long long)bsum[c];
+  } else {
+    const uint32_t* q = repl + (size_t)c * P.nh + k;
+    v = 0;
+#pragma unroll
+    for (int r = 0; r < REPL; ++r) v += (long long)q[(size_t)r * rs];
+  }
+  rows[(size_t)c * stride + k] = v;
+}
+
+__global__ __launch_bounds__(256) void k_bg_rows_set(KParams P, uint32_t* __restrict__ repl, unsigned long long rs,
+                                                     uint32_t* __restrict__ bsum, const long long* __restrict__ rows,
+                                                     long long stride, uint32_t* __restrict__ err_word) {
+  const int c = blockIdx.y, k = blockIdx.x * 256 + threadIdx.x;
+  const int W = P.h1b + P.n2 + 2;
+  if (k >= P.nh && k != W - 1) return;
+  const long long v = k < W ? rows[(size_t)c * stride + k] : 0;
+  if (v < 0 || v > 0xffffffffll) atomicOr(err_word, ERR_OVF);
+  if (k == W - 1) {
+    bsum[c] = (uint32_t)v;
+    if (k >= P.nh) return;
+  }
+  uint32_t* q = repl + (size_t)c * P.nh + k;
+  q[0] = k < W - 1 ? (uint32_t)v : 0u;
+#pragma unroll
+  for (int r = 1; r < REPL; ++r) q[(size_t)r * rs] = 0u;
 }
 
 // ------------------------------------------------------------------------------------------ K1

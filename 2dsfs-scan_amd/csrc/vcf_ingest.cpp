@@ -564,15 +564,24 @@ int sfs2d_vcf_read(const char* vcf_path, const char* popmap_path, int nthreads, 
     if (const char* ev = std::getenv("SFS2D_VCF_MERGE_CHUNK")) chunk = std::max<int64_t>(1, std::atoll(ev));
     {
       const int S = std::max(1, std::min<int>(T, (int)std::max<int64_t>(1, total / chunk)));
+      // SFS2D_VCF_MERGE_SKEW=1 (tests): every key in shard 0, the most uneven spread the hash can give
+      const char* skew_ev = std::getenv("SFS2D_VCF_MERGE_SKEW");
+      const bool skew = skew_ev && skew_ev[0] == '1';
+      auto shard_of = [&](uint64_t h) { return skew ? 0 : (int)((h >> 40) % (uint64_t)S); };
       auto shard = [&](int t) {
+        // the table is sized from this shard's own record count (>= its distinct keys), so its load
+        // factor stays <= 1/2 however unevenly the hash spreads the keys over the shards
+        size_t mine = 0;
+        for (const Part& p : parts)
+          for (const uint64_t h : p.hash) mine += shard_of(h) == t;
         size_t cap = 16;
-        while (cap < (size_t)(total / S + 1) * 2) cap <<= 1;
+        while (cap < (mine + 1) * 2) cap <<= 1;
         std::vector<int64_t> table(cap, -1);   // bucket -> (part, record) of the key's first record
         for (size_t pi = 0; pi < parts.size(); ++pi) {
           const Part& p = parts[pi];
           for (size_t r = 0; r < p.hash.size(); ++r) {
             const uint64_t h = p.hash[r];
-            if ((int)((h >> 40) % (uint64_t)S) != t) continue;
+            if (shard_of(h) != t) continue;
             const char* k = p.keys.data() + p.key_off[r];
             const size_t kl = (size_t)(p.key_off[r + 1] - p.key_off[r]);
             size_t bk = h & (cap - 1);

@@ -24,6 +24,12 @@ W_EMPTY = 0x80000000
 W_BG2_ZERO, W_BG1A_ZERO, W_BG1B_ZERO = 0x1, 0x2, 0x4
 W_EXTRA = 0x40000000
 
+
+def bg_row_words(n1p: int, n2p: int) -> int:
+    """SFS2D_BG_ROW_WORDS: one background as an int64 row [2D bins | unfolded pop-1 | unfolded pop-2 |
+    inner 2D sum] (sfs2d_bg_hist_dev, sfs2d_plan_bg_rows_dev)."""
+    return (2 * n1p + 1) * (2 * n2p + 1) + 2 * n1p + 2 * n2p + 3
+
 # the exported symbols of include/sfs2d.h (checked by tests/test_lib_abi.py)
 EXPORTS = [
     "sfs2d_abi_version", "sfs2d_ctx_create", "sfs2d_ctx_destroy", "sfs2d_last_error", "sfs2d_ctx_set_stream",
@@ -36,7 +42,7 @@ EXPORTS = [
     "sfs2d_plan_stats", "sfs2d_plan_grids", "sfs2d_plan_attach", "sfs2d_data_synth_sims",
     "sfs2d_data_read", "sfs2d_dist_unique_id", "sfs2d_dist_create", "sfs2d_dist_scan_gather",
     "sfs2d_dist_destroy", "sfs2d_dist_set_gather", "sfs2d_plan_run_streams",
-    "sfs2d_dist_scan_gather_streams",
+    "sfs2d_dist_scan_gather_streams", "sfs2d_bg_hist_dev", "sfs2d_plan_bg_rows_dev", "sfs2d_plan_bg_rows_set_dev",
 ]
 
 
@@ -113,6 +119,9 @@ def lib():
     L.sfs2d_plan_bg_buffer.argtypes = [vp, C.POINTER(vp), C.POINTER(i64)]
     L.sfs2d_plan_bg_words.argtypes = [vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)]
     L.sfs2d_plan_bg_exchange.argtypes = [vp, vp, vp, C.c_int]
+    L.sfs2d_bg_hist_dev.argtypes = [vp, vp, C.POINTER(Params), i32, vp]
+    L.sfs2d_plan_bg_rows_dev.argtypes = [vp, vp, i64]
+    L.sfs2d_plan_bg_rows_set_dev.argtypes = [vp, vp, i64]
     L.sfs2d_plan_check.argtypes = [vp]
     L.sfs2d_plan_time.argtypes = [vp, C.c_int] + [C.POINTER(C.c_double)] * 4
     L.sfs2d_plan_destroy.argtypes = [vp]

@@ -209,12 +209,109 @@ def _allreduce_sum(v: np.ndarray, comm_device):
     return t.cpu().numpy()
 
 
+def hist_width(cfg) -> int:
+    """Words of one chromosome's background row in the split exchange (L.bg_row_words: 2D bins,
+    both unfolded 1D spectra, the inner 2D sum); 0 for a supplied background (nothing to exchange)."""
+    return L.bg_row_words(cfg.n1p, cfg.n2p) if cfg.bg_mode == L.BG_PER_CHROM else 0
+
+
 def whole_scan(split_scan):
     """The one-rank scan of a split-scan job factory: its own histograms are the totals."""
     def scan(sub, cfg, bg):
         job = split_scan(sub, cfg, bg)
+        if hasattr(job, "whole"):
+            return job.whole()
         return job.finish(job.partial())
     return scan
+
+
+def _all_reduce_dev(buf):
+    """Sum ``buf`` over the group where it lives: RCCL on the device (nccl); gloo reduces a host copy
+    (the GPU tests' gloo groups: gloo's CUDA support is not relied on)."""
+    import torch.distributed as dist
+    if buf.is_cuda and dist.get_backend() != "nccl":
+        h = buf.cpu()
+        dist.all_reduce(h)
+        buf.copy_(h)
+    else:
+        dist.all_reduce(buf)
+
+
+def _all_gather_dev(out, world):
+    """All-gather equal-size uint8 tables; the result on the host (the post-pass reads it there)."""
+    import torch
+    import torch.distributed as dist
+    if out.is_cuda and dist.get_backend() != "nccl":
+        out = out.cpu()
+    g = torch.empty((world * out.shape[0], out.shape[1]), dtype=out.dtype, device=out.device)
+    dist.all_gather_into_tensor(g, out)
+    return g.cpu().numpy()
+
+
+def _split_device(p, cfg, bg, split_scan, device, cuts, c0s, sub, c0, rank, world, last):
+    """scan_records_split for jobs that exchange in HBM (engine.SplitJob).  Two collectives per scan,
+    both on device buffers: ONE all-reduce of [every chromosome's background rows | per rank: failed,
+    records] (each rank's part written by k_bg_rows_get; RCCL over xGMI), then ONE all-gather of the
+    fixed-stride record tables, each followed by its rank's status row.  The host reads the small tail
+    (to size the gather and to see failures) and the gathered table (the post-pass is sequential).
+    Returns the merged table, or None when any rank failed (the caller falls back)."""
+    import dataclasses
+
+    import torch
+    from .engine import Engine
+    dev = torch.device(f"cuda:{device}")
+    eng = Engine.get(device)
+    W = hist_width(cfg)
+    H = p.nchrom * W
+    lo, hi = cuts[rank], cuts[rank + 1]
+    eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)   # kernels ordered with torch's / RCCL's ops
+    job = None
+    try:
+        buf = torch.zeros(H + 2 * world, dtype=torch.int64, device=dev)
+        err, nrec = None, 0
+        if hi > lo:
+            try:
+                job = split_scan(sub, dataclasses.replace(cfg, prev_extra=bool(cfg.prev_extra) and rank == last), bg)
+                nrec = job.rows()
+                if W:
+                    job.partial_dev(buf.data_ptr() + 8 * c0 * W, W)
+            except Exception as e:  # noqa: BLE001  (every rank takes the fallback)
+                err = e
+        buf[H + 2 * rank] = 1 if err is not None else 0
+        buf[H + 2 * rank + 1] = nrec
+        _all_reduce_dev(buf)
+        STATS["allreduce"] += 1 if W else 0
+        tail = buf[H:].cpu().numpy().reshape(world, 2)
+        if tail[:, 0].any():
+            return None
+        rows = int(tail[:, 1].max())
+        out = torch.zeros((rows + 1, 64), dtype=torch.uint8, device=dev)   # + this rank's status row
+        if job is not None:
+            try:
+                job.finish_dev(buf.data_ptr() + 8 * c0 * W if W else None, W, out.data_ptr())
+            except Exception:  # noqa: BLE001
+                out[rows, 0] = 1
+        g = _all_gather_dev(out, world).reshape(world, rows + 1, 64)
+        if g[:, rows, 0].any():
+            return None
+        tables = [np.ascontiguousarray(g[r, : int(tail[r, 1])]).view(L.WINDOW_DTYPE).reshape(-1) for r in range(world)]
+        return _merge_split(tables, cuts, c0s, bool(cfg.prev_extra),
+                            int(cfg.window) if cfg.window_mode == L.WINDOW_SNPS else 0, p.chrom_off)
+    finally:
+        if job is not None:
+            job.close()
+        torch.cuda.current_stream(dev).synchronize()
+        eng.set_stream(None)
+
+
+def _rows_on_device(split_scan) -> bool:
+    if not getattr(split_scan, "device_rows", False):
+        return False
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except ImportError:
+        return False
 
 
 def scan_records_split(p, cfg, bg, split_scan, device: int = 0, comm_device="auto") -> np.ndarray:
@@ -222,16 +319,17 @@ def scan_records_split(p, cfg, bg, split_scan, device: int = 0, comm_device="aut
     rank r scans SNPs [c_r, c_r+1) -- chromosomes cut wherever that balances the SNPs, so one
     chromosome spreads over all ranks.  With per-chromosome backgrounds every chromosome's histograms
     are the sum of its parts': between k_prep and the scan each rank's partial histograms are summed
-    over the ranks (one all-reduce of int64 words, SURVEY 8(e) collective (1)).
+    over the ranks (one all-reduce of int64 rows, SURVEY 8(e) collective (1)).
 
     ``split_scan(sub, cfg, bg)`` makes a rank's job over its part ``sub`` (chromosomes numbered from
-    the part's first): ``job.partial()`` runs k_prep and returns the part's histograms as an int64
-    array (one row per chromosome of ``sub``; None without per-chromosome backgrounds), and
-    ``job.finish(total)`` writes the summed rows back, scans and returns the records.  Every rank
-    returns the global record table (sfs2d.post reads it like one plan's).  When any rank fails, the
-    whole scan is redone sharded by whole chromosomes (scan_records), which raises the error the
-    reference raises on every rank (a chromosome's first bad SNP decides it, and it may sit in another
-    rank's part)."""
+    the part's first).  HIP jobs (``split_scan.device_rows``: engine.SplitJob) exchange in HBM
+    (_split_device: the rows written and read back by kernels, RCCL on the device buffers).  Other jobs
+    (the tests' oracle jobs) exchange on the host: ``job.partial()`` runs the histogram pass and returns
+    the part's rows (int64 [nchrom, hist_width]; None without per-chromosome backgrounds), and
+    ``job.finish(total)`` takes the summed rows, scans and returns the records.  Every rank returns the
+    global record table (sfs2d.post reads it like one plan's).  When any rank fails, the whole scan is
+    redone sharded by whole chromosomes (scan_records), which raises the error the reference raises on
+    every rank (a chromosome's first bad SNP decides it, and it may sit in another rank's part)."""
     import dataclasses
 
     import torch.distributed as dist
@@ -243,6 +341,13 @@ def scan_records_split(p, cfg, bg, split_scan, device: int = 0, comm_device="aut
     last = max((r for r in range(world) if cuts[r + 1] > cuts[r]), default=-1)
     sub, c0 = p.slice_snps(lo, hi)
     c0s = [p.slice_snps(cuts[r], cuts[r + 1])[1] for r in range(world)]
+    if _rows_on_device(split_scan):
+        out = _split_device(p, cfg, bg, split_scan, device, cuts, c0s, sub, c0, rank, world, last)
+        if out is not None:
+            STATS["split"] += 1
+            return out
+        STATS["fallback"] += 1
+        return scan_records(p, cfg, bg, whole_scan(split_scan), device, comm_device)
     job, part, err = None, None, None
     if hi > lo:
         try:
@@ -267,12 +372,64 @@ def scan_records_split(p, cfg, bg, split_scan, device: int = 0, comm_device="aut
                 err = e
         failed, _ = _agree(err, 0, world)
     if failed:
+        # this rank's job (its uploaded part and plan) is released before the fallback re-uploads
+        if job is not None and hasattr(job, "close"):
+            job.close()
         STATS["fallback"] += 1
         return scan_records(p, cfg, bg, whole_scan(split_scan), device, comm_device)
     STATS["split"] += 1
     tables = gather_tables(local, world, comm_device)
     return _merge_split(tables, cuts, c0s, bool(cfg.prev_extra),
                         int(cfg.window) if cfg.window_mode == L.WINDOW_SNPS else 0, p.chrom_off)
+
+
+def sharded_bg_hist(p, cfg, device: int = 0, chrom: int = -1):
+    """calculate_2d_sfs / calculate_1d_sfs (twoDSFS_class.py:140-232, 398-444) over SNPs held by every
+    rank of the default process group: rank r histograms the r-th of ``world`` contiguous SNP slices of
+    chromosome ``chrom`` (-1: the whole data set) on its GPU into one int64 row (sfs2d_bg_hist_dev), and
+    ONE all-reduce of [row | per rank: error bits] sums them (RCCL on the device buffer).  Every rank
+    returns (h2d (n1+1, n2+1), unfolded h1a, unfolded h1b) as numpy int64, or raises what the
+    single-GPU call raises: the error bits of all ranks are OR-ed, as one GPU's error word is (KeyError
+    for counts above 2 * pop_size before the out-of-grid ValueError)."""
+    import torch
+    import torch.distributed as dist
+    from .engine import Engine
+    rank, world = dist.get_rank(), dist.get_world_size()
+    lo_c, hi_c = (0, p.n) if chrom < 0 else (int(p.chrom_off[chrom]), int(p.chrom_off[chrom + 1]))
+    span = hi_c - lo_c
+    a, b = lo_c + span * rank // world, lo_c + span * (rank + 1) // world
+    W = L.bg_row_words(cfg.n1p, cfg.n2p)
+    on_dev = torch.cuda.is_available()
+    dev = torch.device(f"cuda:{device}") if on_dev else torch.device("cpu")
+    buf = torch.zeros(W + world, dtype=torch.int64, device=dev)
+    code = 0
+    if b > a:
+        sub, _ = p.slice_snps(a, b)
+        eng = Engine.get(device)
+        eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        d = eng.upload(sub)
+        try:
+            eng.bg_hist_dev(d, cfg, -1, buf.data_ptr())
+        except KeyError:
+            code = 1
+        except L.Sfs2dError as e:
+            if e.code != L.E_GRID:
+                raise
+            code = 2
+        finally:
+            d.close()
+            eng.set_stream(None)
+    buf[W + rank] = code
+    _all_reduce_dev(buf)
+    h = buf.cpu().numpy()
+    bits = int(np.bitwise_or.reduce(h[W:].astype(np.int64))) if world else 0
+    if bits & 1:
+        raise KeyError("allele count above 2*pop_size (reference: KeyError in calculate_1d_sfs)")
+    if bits & 2:
+        raise L.Sfs2dError(L.E_GRID, "folded 2D bin outside the (2n1+1)x(2n2+1) grid")
+    n1, n2 = 2 * cfg.n1p, 2 * cfg.n2p
+    nb = (n1 + 1) * (n2 + 1)
+    return h[:nb].reshape(n1 + 1, n2 + 1), h[nb:nb + n1 + 1], h[nb + n1 + 1:nb + n1 + n2 + 2]
 
 
 def scan_records(p, cfg, bg, scan_local, device: int = 0, comm_device="auto") -> np.ndarray:

@@ -116,6 +116,12 @@ class Engine:
                                           L.ptr(h1b)))
         return h2.reshape(n1 + 1, n2 + 1), h1a, h1b
 
+    def bg_hist_dev(self, data: "DeviceData", cfg: ScanConfig, chrom: int, row_ptr: int):
+        """sfs2d_bg_hist_dev: the histograms as one int64 row (L.bg_row_words) at device address
+        ``row_ptr``, enqueued on the engine's stream (synchronises to report count errors)."""
+        prm = cfg.params()
+        self.check(self.lib.sfs2d_bg_hist_dev(self.h, data.h, C.byref(prm), int(chrom), C.c_void_p(row_ptr)))
+
     def plan(self, data: "DeviceData", cfg: ScanConfig) -> "Plan":
         return Plan(self, data, cfg)
 
@@ -290,8 +296,15 @@ class Plan:
 
 class SplitJob:
     """A rank's part of a scan split over ranks at window boundaries (sfs2d.dist.scan_records_split):
-    its SNPs uploaded, one plan, k_prep run alone (``partial``: this part's per-chromosome background
-    histograms), the summed histograms written back and the scan run (``finish``)."""
+    its SNPs uploaded and one plan.  The exchange stays in HBM: ``partial_dev`` runs k_prep alone
+    (phase 1) and writes this part's per-chromosome background histograms as int64 rows into a device
+    buffer (sfs2d_plan_bg_rows_dev); after the ranks' all-reduce of that buffer (RCCL), ``finish_dev``
+    writes the summed rows back (sfs2d_plan_bg_rows_set_dev), runs tables + scan (phase 2) into a device
+    record buffer and checks the run.  ``whole`` is the one-rank scan (its own histograms are the totals).
+    Everything is enqueued on the engine's stream: the caller sets it to the stream its collectives are
+    ordered on (torch's current stream)."""
+
+    device_rows = True
 
     def __init__(self, eng: Engine, sub: PackedSNPs, cfg: ScanConfig, bg=None):
         self.eng, self.cfg, self.nchrom = eng, cfg, sub.nchrom
@@ -304,44 +317,35 @@ class SplitJob:
         except Exception:
             self.close()
             raise
-        self.shape = None
 
-    def _words(self):
-        r, c, b = C.c_int64(), C.c_int64(), C.c_int64()
-        self.eng.check(self.eng.lib.sfs2d_plan_bg_words(self.pl.h, C.byref(r), C.byref(c), C.byref(b)))
-        return r.value, c.value, b.value
+    def rows(self) -> int:
+        """Records the scan writes (window slots, + the Q9 helper)."""
+        return self.pl.nrec
 
-    def partial(self) -> Optional[np.ndarray]:
-        """int64 [nchrom, bins + 1]: the part's histograms (replicas summed) and inner 2D sums; None for a
-        supplied background (nothing to exchange)."""
+    def partial_dev(self, rows_ptr: int, stride: int):
+        """k_prep alone; this part's background histograms into ``rows_ptr`` (int64, row c at
+        rows_ptr + 8 * c * stride).  Nothing to do for a supplied background."""
         if self.cfg.bg_mode != L.BG_PER_CHROM:
-            return None
+            return
         self.pl.run(phase=1)
-        r, c, b = self._words()
-        self.shape = (r, c, b)
-        repl = np.zeros(r * c * b, np.uint32)
-        sums = np.zeros(c, np.uint32)
-        self.eng.check(self.eng.lib.sfs2d_plan_bg_exchange(self.pl.h, L.ptr(repl), L.ptr(sums), 0))
-        h = repl.reshape(r, c, b).sum(axis=0, dtype=np.int64)
-        return np.concatenate([h, sums.astype(np.int64)[:, None]], axis=1)
+        self.eng.check(self.eng.lib.sfs2d_plan_bg_rows_dev(self.pl.h, C.c_void_p(rows_ptr), int(stride)))
 
-    def finish(self, total: Optional[np.ndarray]) -> np.ndarray:
-        """Scan with the summed histograms ``total`` (partial()'s layout) and return the records."""
+    def finish_dev(self, rows_ptr: Optional[int], stride: int, out_ptr: int):
+        """The summed rows back, the scan into ``out_ptr`` (device, rows() records), errors raised."""
         try:
-            if total is None or self.shape is None:
-                self.pl.run()
+            if self.cfg.bg_mode == L.BG_PER_CHROM:
+                self.eng.check(self.eng.lib.sfs2d_plan_bg_rows_set_dev(self.pl.h, C.c_void_p(rows_ptr), int(stride)))
+                self.pl.run(out_ptr, phase=2)
             else:
-                r, c, b = self.shape
-                t = np.asarray(total, np.int64)
-                if t.shape != (c, b + 1):
-                    raise ValueError(f"summed histograms have shape {t.shape}, the plan's are {(c, b + 1)}")
-                if t.size and (t.min() < 0 or t.max() >= 1 << 32):
-                    raise L.Sfs2dError(L.E_ARG, "summed background histograms overflow uint32")
-                repl = np.zeros((r, c, b), np.uint32)
-                repl[0] = t[:, :b]
-                sums = np.ascontiguousarray(t[:, b], np.uint32)
-                self.eng.check(self.eng.lib.sfs2d_plan_bg_exchange(self.pl.h, L.ptr(repl), L.ptr(sums), 1))
-                self.pl.run(phase=2)
+                self.pl.run(out_ptr)
+            self.pl.check()
+        finally:
+            self.close()
+
+    def whole(self) -> np.ndarray:
+        """The part scanned on its own (one rank: its histograms are the totals); host records."""
+        try:
+            self.pl.run()
             self.pl.check()
             return self.pl.read()
         finally:

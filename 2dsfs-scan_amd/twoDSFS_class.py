@@ -132,6 +132,21 @@ class LikelihoodInference_jointSFS:
     def _split_scan(self, p: PackedSNPs, cfg: ScanConfig, bg=None):
         from sfs2d.engine import SplitJob
         return SplitJob(self._engine(), p, cfg, bg)
+    _split_scan.device_rows = True   # its jobs exchange background rows in HBM (sfs2d.dist._split_device)
+
+    def _hist(self, p: PackedSNPs, cfg: ScanConfig, chrom: int):
+        """Background histograms (h2d, unfolded h1a, unfolded h1b) of chromosome ``chrom`` (-1: all
+        SNPs) on the GPU; distributed: every rank histograms a slice, one all-reduce on the device
+        (sfs2d.dist.sharded_bg_hist)."""
+        if self.distributed:
+            from sfs2d import dist as D
+            return D.sharded_bg_hist(p, cfg, self.device, chrom)
+        eng = self._engine()
+        dev = eng.upload(p if chrom < 0 else p.subset_chroms([chrom]))
+        try:
+            return eng.bg_hist(dev, cfg, -1)
+        finally:
+            dev.close()
 
     def _scan_local(self, p: PackedSNPs, cfg: ScanConfig, bg=None):
         eng = self._engine()
@@ -143,14 +158,9 @@ class LikelihoodInference_jointSFS:
         return recs
 
     def _bg_arrays(self, p: PackedSNPs, chrom: int):
-        """Unnormalised background of one chromosome (2D grid + folded 1D), computed on the GPU (every
-        rank computes it itself when distributed: integer counts, no collective)."""
-        eng = self._engine()
-        dev = eng.upload(p.subset_chroms([chrom]))
-        try:
-            h2, u1, u2 = eng.bg_hist(dev, self._cfg(p), 0)
-        finally:
-            dev.close()
+        """Unnormalised background of one chromosome (2D grid + folded 1D), computed on the GPU
+        (distributed: sharded over the ranks, one all-reduce)."""
+        h2, u1, u2 = self._hist(p, self._cfg(p), chrom)
         return h2, _fold_counts(u1), _fold_counts(u2)
 
     # ------------------------------------------------------------------ window scans
@@ -345,18 +355,15 @@ class LikelihoodInference_jointSFS:
 
     # ------------------------------------------------------------------ SFS primitives
     def calculate_2d_sfs(self, data_dict):
-        """2D SFS dict over the grid (140-232), accumulated on the GPU."""
+        """2D SFS dict over the grid (140-232), accumulated on the GPU (distributed: every rank a slice
+        of the SNPs, one device all-reduce -- the genome-wide background of the reference script,
+        1970-1983, from sharded data)."""
         self.data_dict = data_dict
         p = self._pack(data_dict)
         n1, n2 = 2 * self.pop1_size, 2 * self.pop2_size
         if p.n == 0:
             return {(i, j): 0 for i in range(n1 + 1) for j in range(n2 + 1)}
-        eng = self._engine()
-        dev = eng.upload(p)
-        try:
-            h2, _, _ = eng.bg_hist(dev, self._cfg(p), -1)
-        finally:
-            dev.close()
+        h2, _, _ = self._hist(p, self._cfg(p), -1)
         return {(i, j): int(h2[i, j]) for i in range(n1 + 1) for j in range(n2 + 1)}
 
     def calculate_1d_sfs(self, data_dict, pop, pop_size, start_position, end_position, variant_type):
@@ -370,18 +377,13 @@ class LikelihoodInference_jointSFS:
         p = self._pack(data_dict, pop1=pop, pop2=pop).single_pop(pop)
         if p.n == 0:
             return {i: 0 for i in range(2 * pop_size + 1)}
-        eng = self._engine()
-        dev = eng.upload(p)
         ann = -1
         if variant_type is not None:
             ann = p.ann_names.index(variant_type) if variant_type in p.ann_names else _NO_ANN
         cfg = ScanConfig(n1p=pop_size, n2p=pop_size, fold=False, ann_want=ann,
                          start_position=None if start_position is None else int(start_position),
                          end_position=None if end_position is None else int(end_position))
-        try:
-            _, u1, _ = eng.bg_hist(dev, cfg, -1)
-        finally:
-            dev.close()
+        _, u1, _ = self._hist(p, cfg, -1)
         return {i: int(u1[i]) for i in range(2 * pop_size + 1)}
 
     def fold_1d_sfs(self, sfs_dict):

@@ -140,8 +140,17 @@ int sfs2d_data_read(const sfs2d_data* data, uint32_t* counts, uint32_t* pos, int
 int sfs2d_bg_hist(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* params, int32_t chrom,
                   int64_t* h2d, int64_t* h1a, int64_t* h1b);
 
-/* Plans: everything that depends only on (data, params) is built once; plan_run replays the
- * launches (captured in a hipGraph) with inputs and outputs resident in HBM. */
+/* The same histograms as ONE int64 row on the device (d_row: SFS2D_BG_ROW_WORDS int64), laid out
+ * [2D bins | unfolded pop-1 spectrum | unfolded pop-2 spectrum | inner 2D sum (bins[1:-1])]: the
+ * multi-GPU calculate_2d_sfs / calculate_1d_sfs (sfs2d/dist.py sharded_bg_hist) all-reduce these
+ * rows over the ranks without a host copy.  Enqueued on the ctx stream; synchronises to report
+ * SFS2D_E_KEY / SFS2D_E_GRID (the row is then undefined). */
+#define SFS2D_BG_ROW_WORDS(n1p, n2p) ((2 * (n1p) + 1) * (2 * (n2p) + 1) + 2 * (n1p) + 2 * (n2p) + 3)
+int sfs2d_bg_hist_dev(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* params, int32_t chrom,
+                      int64_t* d_row);
+
+/* Plans: everything that depends only on (data, params) is built once; plan_run enqueues the pass's
+ * kernels (k_prep, k_bg_slice, the scan) with inputs and outputs resident in HBM. */
 int sfs2d_plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* params, sfs2d_plan** out);
 /* number of output records the plan writes (window slots, +1 when SFS2D_F_PREV_EXTRA) */
 int64_t sfs2d_plan_num_records(const sfs2d_plan* plan);
@@ -178,6 +187,14 @@ int sfs2d_plan_bg_buffer(sfs2d_plan* plan, void** dev_ptr, int64_t* nbytes);
  * chromosome's SNPs are held by several ranks.  Plans without per-chromosome backgrounds: all 0. */
 int sfs2d_plan_bg_words(const sfs2d_plan* plan, int64_t* replicas, int64_t* nchrom, int64_t* bins);
 int sfs2d_plan_bg_exchange(sfs2d_plan* plan, uint32_t* host_repl, uint32_t* host_sums, int to_device);
+/* The device-resident form of that exchange (no host copy; the SURVEY 8(e) all-reduce runs on the
+ * rows in HBM, RCCL over xGMI): after sfs2d_plan_run_phase(plan, 1), _bg_rows_dev writes the plan's
+ * per-chromosome partial histograms as int64 rows (row c at d_rows + c * row_stride, row_stride >=
+ * SFS2D_BG_ROW_WORDS; layout of sfs2d_bg_hist_dev); after the all-reduce, _bg_rows_set_dev writes the
+ * summed rows back (sums >= 2^32: SFS2D_E_ARG from sfs2d_plan_check), then sfs2d_plan_run_phase(plan, 2).
+ * Both are enqueued on the ctx stream (order the collective against it). */
+int sfs2d_plan_bg_rows_dev(sfs2d_plan* plan, int64_t* d_rows, int64_t row_stride);
+int sfs2d_plan_bg_rows_set_dev(sfs2d_plan* plan, const int64_t* d_rows, int64_t row_stride);
 /* Fst of the last run per window slot (NaN: no qualifying SNP / empty slot); plans with SFS2D_F_FST */
 int sfs2d_plan_fst_read(sfs2d_plan* plan, double* out_host, int64_t cap);
 int sfs2d_plan_fst_buffer(sfs2d_plan* plan, void** dev_ptr, int64_t* nslots);
@@ -198,7 +215,8 @@ int sfs2d_plan_attach(sfs2d_plan* base, const sfs2d_params* params, sfs2d_plan**
 int sfs2d_plan_grids(const sfs2d_plan* plan, int64_t* prep_threads, int64_t* scan_threads);
 /* cumulative number of windows re-evaluated on the exact path (|T| ~ 0: proportionality test) */
 int sfs2d_plan_stats(sfs2d_plan* plan, uint32_t* exact_windows);
-/* last run's error word (0 = ok, else SFS2D_E_KEY / SFS2D_E_GRID); synchronises */
+/* last run's error word (0 = ok, else SFS2D_E_KEY / SFS2D_E_GRID, or SFS2D_E_ARG for summed background
+ * rows that overflow); synchronises */
 int sfs2d_plan_check(sfs2d_plan* plan);
 /* live timing: every `every`-th of the following runs (up to `max_samples` of them) launches k_prep
  * and the scan kernel with start/stop events in their own dispatch packets (hipExtLaunchKernelGGL):
@@ -217,7 +235,8 @@ int sfs2d_plan_timing_read(sfs2d_plan* plan, int* nruns, double* ms_k1, double* 
 int sfs2d_plan_time(sfs2d_plan* plan, int iters, double* ms_per_run, double* ms_k1, double* ms_k2, double* ms_k3);
 int sfs2d_plan_destroy(sfs2d_plan* plan);
 
-/* ---- multi-GPU: one process per GPU, windows sharded by chromosome (sfs2d/dist.py), one RCCL
+/* ---- multi-GPU, native step loop: one process per GPU, each rank scanning its own data set (the
+ * drivers' split at window boundaries lives in sfs2d/dist.py), one RCCL
  * all-gather of the fixed-stride window tables per scan (replaces the reference's
  * single-process loop over every window, twoDSFS_class.py:787-991).  RCCL is loaded at the first
  * call (dlopen librccl.so.1: the copy torch already loaded, else the ROCm one).

@@ -81,10 +81,11 @@ class FakeSplitJob:
         if self.cfg.bg_mode != L.BG_PER_CHROM:
             return None
         rows = []
-        for c in range(self.sub.nchrom):
+        for c in range(self.sub.nchrom):   # the exchange's row layout (sfs2d.dist.hist_width)
             idx = np.arange(self.sub.chrom_off[c], self.sub.chrom_off[c + 1])
-            rows.append(np.concatenate([O.sfs2d(self.sub, idx, self.ocfg).ravel(), O.sfs1d(self.sub, idx, 1, self.ocfg),
-                                        O.sfs1d(self.sub, idx, 2, self.ocfg)]))
+            h2 = O.sfs2d(self.sub, idx, self.ocfg).ravel()
+            rows.append(np.concatenate([h2, O.sfs1d(self.sub, idx, 1, self.ocfg), O.sfs1d(self.sub, idx, 2, self.ocfg),
+                                        [h2[1:-1].sum()]]))
         return np.array(rows, dtype=np.int64).reshape(self.sub.nchrom, -1)
 
     def finish(self, total):
@@ -93,9 +94,12 @@ class FakeSplitJob:
             return _fake_records(self.sub, self.cfg, self.ocfg, lambda c: b)
         n1, n2 = 2 * self.cfg.n1p, 2 * self.cfg.n2p
         nb = (n1 + 1) * (n2 + 1)
-        bgs = [(t[:nb].reshape(n1 + 1, n2 + 1), O.fold1d(t[nb:nb + n1 + 1]), O.fold1d(t[nb + n1 + 1:]))
+        bgs = [(t[:nb].reshape(n1 + 1, n2 + 1), O.fold1d(t[nb:nb + n1 + 1]), O.fold1d(t[nb + n1 + 1:nb + n1 + n2 + 2]))
                for t in np.asarray(total, np.int64)]
         return _fake_records(self.sub, self.cfg, self.ocfg, lambda c: bgs[c])
+
+    def close(self):
+        pass
 
 
 def _class_obj(cfgd, mode):
@@ -211,6 +215,7 @@ def run_single(mode, out_path):
     p = synth_genome(1, [60000], 25, 25, seed=17)
     if mode == "gpu":
         factory = lambda sub, cfg, bg: SplitJob(Engine.get(dev), sub, cfg, bg)
+        factory.device_rows = True   # background rows exchanged in HBM (sfs2d.dist._split_device)
     else:
         factory = FakeSplitJob
     bg = (np.arange(51 * 51, dtype=np.float64).reshape(51, 51) % 7 + 1, np.arange(26.0) + 1, np.arange(26.0) % 5 + 1)
@@ -236,16 +241,88 @@ def run_single(mode, out_path):
     dist.barrier()
 
 
+def _strip(t):
+    """A table as one plan over all SNPs leaves it for the post-pass: empty bp slots dropped, the Q9
+    helper's wid (its first SNP's index in the scanned data, unused) zeroed."""
+    from sfs2d import _lib as L
+    t = t[((t["flags"] & L.W_EMPTY) == 0) | ((t["flags"] & L.W_EXTRA) != 0)].copy()
+    t["wid"][(t["flags"] & L.W_EXTRA) != 0] = 0
+    return t
+
+
+def run_config3(mode, out_path, data_path):
+    """BASELINE config 3 at full size (5e7 SNPs, 32 chromosomes; the parent generated it into
+    ``data_path``) split over the ranks at window boundaries -- with 3 ranks the cuts fall inside
+    chromosomes, so their background rows are all-reduced -- at 20 kb and 500 kb with per-chromosome
+    backgrounds, and at 20 kb against the genome-wide background (the reference script's
+    calculate_2d_sfs(all) -> normalize -> scan_precomputed_BG, twoDSFS_class.py:1970-1983, 1161),
+    histogrammed sharded (sfs2d.dist.sharded_bg_hist).  Rank 0 compares every merged table with the
+    table one GPU's plan over the whole genome writes, byte for byte."""
+    import torch.distributed as dist
+    from sfs2d import _lib as L
+    from sfs2d import dist as D
+    from sfs2d.engine import Engine, ScanConfig, SplitJob
+    from sfs2d.pack import PackedSNPs
+    dev = int(os.environ.get("SFS2D_DEVICE", "0"))
+    z = np.load(data_path)
+    p = PackedSNPs(z["counts"], z["pos"], z["chrom_off"], [f"chr{c:02d}" for c in range(len(z["chrom_off"]) - 1)],
+                   None, [], "p1", "p2")
+    factory = lambda sub, cfg, bg: SplitJob(Engine.get(dev), sub, cfg, bg)
+    factory.device_rows = True
+    rank = dist.get_rank()
+    out = {}
+    cfgs = {"bp20k_perchrom": (ScanConfig(n1p=25, n2p=25, window=20000, prev_extra=True), None),
+            "bp500k_perchrom": (ScanConfig(n1p=25, n2p=25, window=500000, prev_extra=True), None)}
+    # the genome-wide background, sharded, against one GPU's histogram of all SNPs
+    hcfg = ScanConfig(n1p=25, n2p=25)
+    h2, u1, u2 = D.sharded_bg_hist(p, hcfg, dev)
+    if rank == 0:
+        eng = Engine.get(dev)
+        d = eng.upload(p)
+        r2, r1, r1b = eng.bg_hist(d, hcfg, -1)
+        d.close()
+        out["genome_hist_equal"] = bool(np.array_equal(h2, r2) and np.array_equal(u1, r1) and np.array_equal(u2, r1b))
+    # normalised as normalize_2d_sfs / normalize_1d_sfs do (sum of values[1:-1] in insertion order)
+    fold = lambda u: np.bincount(np.minimum(np.arange(len(u)), len(u) - 1 - np.arange(len(u))), weights=u)
+    def norm(v):
+        t = sum(v[1:-1].tolist())
+        return np.array([x / t for x in v.tolist()])
+    bg = (norm(h2.ravel().astype(np.float64)).reshape(h2.shape), norm(fold(u1.astype(np.float64))),
+          norm(fold(u2.astype(np.float64))))
+    cfgs["bp20k_genome_bg"] = (ScanConfig(n1p=25, n2p=25, window=20000, bg_mode=L.BG_SUPPLIED), bg)
+    for name, (cfg, b) in cfgs.items():
+        before = dict(D.STATS)
+        got = D.scan_records_split(p, cfg, b, factory, dev)
+        split = D.STATS["split"] - before["split"]
+        if rank == 0:
+            full = _strip(D.whole_scan(factory)(p, cfg, b))
+            got = _strip(got)
+            out[name] = {"equal": got.tobytes() == full.tobytes(), "n": int(len(full)), "split": split,
+                         "windows": int(((full["flags"] & L.W_EMPTY) == 0).sum())}
+    out["_stats"] = dict(D.STATS)
+    out["cuts"] = D.split_points(p, cfgs["bp20k_perchrom"][0], dist.get_world_size())
+    if rank == 0:
+        with open(out_path, "w") as fh:
+            json.dump(out, fh)
+    dist.barrier()
+
+
 def main():
     import torch.distributed as dist
     mode, out_path = sys.argv[1], sys.argv[2]
-    dist.init_process_group("gloo", rank=int(os.environ["RANK"]), world_size=int(os.environ["WORLD_SIZE"]))
+    backend = os.environ.get("SFS2D_TEST_BACKEND", "gloo")
+    if backend == "nccl":   # RCCL: the device-resident collectives of the split path (one GPU: world 1)
+        import torch
+        torch.cuda.set_device(int(os.environ.get("SFS2D_DEVICE", "0")))
+    dist.init_process_group(backend, rank=int(os.environ["RANK"]), world_size=int(os.environ["WORLD_SIZE"]))
     try:
         what = sys.argv[3] if len(sys.argv) > 3 else ""
         if what == "errors":
             run_errors(mode, out_path)
         elif what == "single":
             run_single(mode, out_path)
+        elif what == "config3":
+            run_config3(mode, out_path, sys.argv[4])
         else:
             run_all(mode, out_path, skip=() if what == "all" else ("chr1",))
     finally:

@@ -101,3 +101,46 @@ def test_config3_full_size_20kb_500kb_one_pass():
         log(f"{ws} bp windows checked")
     base.close()
     dev.close()
+
+
+@pytest.mark.timeout(600)
+def test_config3_genome_wide_background_precomputed():
+    """BASELINE config 3's genome-wide-background variant at full size, through the drop-in class as the
+    reference script runs it (twoDSFS_class.py:1970-1983 then scan_precomputed_BG, 1161): the whole
+    genome's 2D / folded 1D SFS (GPU histograms), normalised in dict order, every 20 kb window scored
+    against it.  Window labels and SNP counts for every window from the positions; a 200-window oracle
+    sample of the statistics (1e-10 relative) against the oracle's own genome background."""
+    import time
+    import twoDSFS_class as T
+    from sfs2d.synth import synth_genome
+    t0 = time.perf_counter()
+    log = lambda m: print(f"[config3-genome {time.perf_counter() - t0:6.1f}s] {m}", flush=True)
+    p = synth_genome(NCHROM, PER, POP, POP, seed=777)
+    log("generated")
+    obj = T.LikelihoodInference_jointSFS(None, None, pop1="p1", pop2="p2", pop1_size=POP, pop2_size=POP)
+    bg2 = obj.normalize_2d_sfs(obj.calculate_2d_sfs(p))
+    bg1 = obj.normalize_1d_sfs(obj.fold_1d_sfs(obj.calculate_1d_sfs(p, "p1", POP, None, None, None)))
+    bg1b = obj.normalize_1d_sfs(obj.fold_1d_sfs(obj.calculate_1d_sfs(p, "p2", POP, None, None, None)))
+    log("background")
+    res = obj.scan_precomputed_BG(p, 20000, bg2, bg1, bg1b)
+    log("scanned")
+    exp = _expected_windows(p, 20000)
+    labels = [f"{p.chrom_names[c]} {1 + w * 20000}-{(w + 1) * 20000}" for c, w in exp[:, :2].tolist()]
+    assert list(res) == labels
+    assert [r["snp_count"] for r in res.values()] == (exp[:, 3] - exp[:, 2]).tolist()
+    ocfg = O.Cfg(POP, POP)
+    g = O.genome_backgrounds_normalized(p, ocfg)
+    # the oracle's normalised background equals the class's (the same sums in the same order)
+    assert np.array_equal(g[0].ravel(), np.array(list(bg2.values()))), "2D background"
+    assert np.array_equal(g[1], np.array(list(bg1.values()))) and np.array_equal(g[2], np.array(list(bg1b.values())))
+    rng = np.random.default_rng(5)
+    sample = np.sort(rng.choice(len(exp), 200, replace=False))
+    vals = list(res.values())
+    for i in sample:
+        q = _win(p, int(exp[i, 2]), int(exp[i, 3]))
+        o = O.window_records(q, [(0, 0, q.n)], ocfg, lambda _c: g)[0]
+        r = vals[i]
+        for f, k in (("T2D", "T2D"), ("T1D_pop1", "T1D_p1"), ("T1D_pop2", "T1D_p2")):
+            assert gu.close(r[f], o[k]), (i, f, r[f], o[k])
+        assert gu.close(r["new_term_pop1"], None if o["T2D"] is None or o["T1D_p1"] is None else o["T2D"] - o["T1D_p1"])
+    log("oracle sample checked")

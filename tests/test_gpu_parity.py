@@ -253,6 +253,43 @@ def test_key_error_on_counts_above_sample_size():
         obj.combined_scan(d, 100)
 
 
+def _bad_count_dict():
+    """Two chromosomes; chromosome "b" holds one SNP whose pop-1 alt count (3) exceeds 2 * pop_size (2)."""
+    d = {}
+    for c in ("a", "b"):
+        for i in range(1, 40):
+            d[f"{c}-{i * 3}"] = {"calls": {"uv": (i % 2, (i + 1) % 2), "bv": ((i // 2) % 2, 1 - (i // 2) % 2)},
+                                 "annotation": "x"}
+    d["b-50"] = {"calls": {"uv": (0, 3), "bv": (1, 1)}, "annotation": "x"}
+    return d
+
+
+@pytest.mark.parametrize("driver", ["precomputed", "chooseChr", "chooseChr_bySNPs", "perChr_bySNPs"])
+def test_key_error_with_supplied_background(driver):
+    """Counts above 2 * pop_size raise KeyError (calculate_1d_sfs, twoDSFS_class.py:433) also when the
+    background is supplied: those plans run no k_prep pass over the counts, so a data set whose called
+    counts exceed the grid takes the bins pipeline, whose k_prep reports the SNP."""
+    import twoDSFS_class as T
+    d = _bad_count_dict()
+    obj = T.LikelihoodInference_jointSFS(None, None, pop1_size=1, pop2_size=1)
+    good = {k: v for k, v in d.items() if k.startswith("a-")}
+    bg2 = obj.calculate_2d_sfs(good)
+    bg1 = obj.fold_1d_sfs(obj.calculate_1d_sfs(good, "uv", 1, None, None, None))
+    bg1b = obj.fold_1d_sfs(obj.calculate_1d_sfs(good, "bv", 1, None, None, None))
+    with pytest.raises(KeyError):
+        if driver == "precomputed":
+            obj.scan_precomputed_BG(d, 100, bg2, bg1, bg1b)
+        elif driver == "chooseChr":
+            obj.scan_chooseChr(d, 100, "a")
+        elif driver == "chooseChr_bySNPs":
+            obj.scan_chooseChr_bySNPs(d, 5, "a")
+        else:
+            obj.scan_perChr_bySNPs(d, 5)
+    # the same calls on the clean chromosome run (the counts plan: max called counts within the grid)
+    obj.scan_precomputed_BG(good, 100, bg2, bg1, bg1b)
+    obj.scan_chooseChr_bySNPs(good, 5, "a")
+
+
 def test_dense_primitives_vs_oracle(golden):
     p = golden.packed("synth_n50")
     import twoDSFS_class as T

@@ -146,6 +146,21 @@ def test_threads_and_oracle(tmp_path, monkeypatch, late, merge_chunk):
         same_dict(V.read_vcf(path, pm, nthreads=nt).to_data_dict(), ref)
 
 
+def test_merge_skewed_shards(tmp_path, monkeypatch):
+    """Every key hashed into one shard of a many-shard merge: that shard's table is sized from its own
+    record count (a table sized from total / shards filled up and its probe never ended)."""
+    monkeypatch.setenv("SFS2D_VCF_MERGE_CHUNK", "61")
+    monkeypatch.setenv("SFS2D_VCF_MERGE_SKEW", "1")
+    raw = synth_vcf(8000, SAMPLES, seed=11)
+    path = str(tmp_path / "k.vcf")
+    open(path, "wb").write(raw)
+    pm = str(tmp_path / "pm.txt")
+    write_popmap(pm, [(s, ["uv", "bv"][i % 2]) for i, s in enumerate(SAMPLES)])
+    ref = vcf_oracle.make_data_dict_vcf(path, pm)
+    for nt in (4, 16):
+        same_dict(V.read_vcf(path, pm, nthreads=nt).to_data_dict(), ref)
+
+
 def test_bgzf_multi_block(tmp_path):
     sys.path.insert(0, GOLD)
     from gen_golden_vcf import bgzf_bytes   # BGZF writer (data only; no reference code)
