@@ -1,27 +1,32 @@
 #!/usr/bin/env python3
 """Benchmark: genomic windows/s of the 2D-SFS composite-likelihood scan (BASELINE.json metric).
 
-Workload (BASELINE configs[1]): one synthetic chromosome of 1e6 SNPs per GPU (SURVEY 8d
-generator, seed 12345 + rank), n1 = n2 = 50 haploid (pop_size 25/25), 20 kb fixed-bp windows,
-each chromosome its own background (combined_scan semantics).  A step = one full scan pass over
-the HBM-resident packed SNPs: background histograms + window segmentation (K1), background
-tables (K2), window scan (K3) -> device-resident 64-B window records.  Consecutive passes are
-independent: they go round-robin over --streams plans (default 3), each on its own HIP stream, so
-one pass's latency-bound kernels overlap the next one's (sfs2d_plan_run_streams).  The timed loop
-is the same at every N (weak scaling: each rank its own chromosome, no data-path collective); with
-N > 1 ranks the timed region ends with one RCCL all-gather of every rank's final window table.
+Headline (``value``): BASELINE configs[2] -- the synthetic whole genome, 32 chromosomes x 1.5625e6 =
+5e7 SNPs (SURVEY 8d generator, seed 777), n1 = n2 = 50 haploid (pop_size 25/25), 20 kb fixed-bp
+windows, every chromosome its own background (combined_scan semantics), T2D + T1D_p1 + T1D_p2 +
+Hudson Fst -- SHARDED BY WINDOW over the N GPUs (strong scaling: the same genome at every N).  Rank
+r holds the SNPs [c_r, c_r+1) of sfs2d.dist.split_points (cuts at window starts nearest k n / N; at
+N | 32 they are chromosome ends, so no chromosome's background spans two ranks).  A step = one full
+scan pass over the genome: on every rank, background histograms + window segmentation (k_prep),
+then the window scan (k_scan_w, its table prologue fused) -> HBM-resident 64-B window records + Fst.
+Consecutive passes are independent: they go round-robin over 2 plans on 2 HIP streams (the scan
+capped at one workgroup per CU so the next pass's bandwidth-bound k_prep finds CUs beside it).  The
+timed region ends with ONE RCCL all-gather of every rank's final window table over xGMI (N > 1).
+At N = 1 the 5e7-SNP stream (~609 MB per pass) is far past the 256 MB Infinity Cache: the HBM
+roofline is measured on it.
+
+Second key ``config2_weak``: BASELINE configs[1] (one 1e6-SNP chromosome per GPU, weak scaling, 3 plans
+on 3 streams), the round-1..3 headline, with its own roofline and the single-stream pass latency.
 
 `--gpus N` with no launcher: this script starts the N rank processes itself (before touching the
 GPU) and exits with their status; under torchrun, WORLD_SIZE must equal N, and a box with fewer
 than N GPUs fails instead of reporting fewer.
 
-Prints ONE JSON line on rank 0.  `roofline` is for the dominant kernel (K3) from HIP events in its
-dispatch packets, on the stream it runs on (with overlapped passes: in a single-stream pass right
-after the timed steps, whose durations agree with rocprofv3's kernel trace; the contended interval
-of the timed steps is `ms_timed_region`); `roofline_hbm` repeats the measurement
-on a >= 400 MB stream (BASELINE config 3 at 1 GPU: 32 x 1.5625e6 SNPs) that does not fit the
-256 MB Infinity Cache.  `cpu_baseline` times the CPU oracle (a numpy/scipy restatement of the
-reference's dense per-window algorithm, 1 core) on a bounded sample of the same stream.
+Prints ONE JSON line on rank 0.  ``roofline``: the dominant kernel (k_scan_w) of the headline workload,
+algorithmic bytes per launch over its duration from HIP events in its dispatch packets in a
+single-stream pass after the timed loop (on the stream it runs on).  ``cpu_baseline``: the C oracle
+(the reference's dense per-window algorithm, OpenMP) on the box's host cores over a bounded sample of
+the same genome (its first chromosome).
 """
 from __future__ import annotations
 
@@ -38,9 +43,11 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
-N_SNP = 1_000_000
 POP = 25
 WS = 20000
+C3_NCHROM, C3_PER, C3_SEED = 32, 1_562_500, 777
+C2_SNP, C2_SEED = 1_000_000, 12345
+METRIC = "genomic windows/s (T2D+T1D+Fst) at 20 kb, n1=n2=50; HBM GB/s fraction"
 
 
 def algorithmic_bytes(n_snp, n_slots, n_win, which):
@@ -79,9 +86,9 @@ def pmc_traffic(kernel, grid):
 def cpu_baseline(p):
     """The CPU baseline on this box's host cores: the C restatement of the oracle (oracle/sfs_oracle_c.c,
     the reference's dense per-window algorithm, OpenMP over windows; test infrastructure, pinned to
-    the numpy oracle) over the whole rank-0 config-2 stream, repeated for >= 3 s; beside it the numpy
-    oracle itself (dense grids + scipy multinomial.logpmf, as the reference computes them) on one core
-    over the same stream."""
+    the numpy oracle) over a bounded sample of the headline genome (its first chromosome), repeated
+    for >= 3 s; beside it the numpy oracle itself (dense grids + scipy multinomial.logpmf, as the
+    reference computes them) on one core over the same sample."""
     from oracle import sfs_oracle as O
     from oracle import sfs_oracle_c as OC
     threads = min(16, os.cpu_count() or 1)   # the box's CPU share (OMP_NUM_THREADS is 16 there)
@@ -96,16 +103,20 @@ def cpu_baseline(p):
         if dt >= 3.0:
             break
     nwin = len(r["b"])
+    q = p.subset_chroms([0])
+    q = type(q)(q.counts[:200_000], q.pos[:200_000], np.array([0, 200_000]), q.chrom_names, q.ann_id[:200_000],
+                q.ann_names, q.pop1, q.pop2)
     cfg = O.Cfg(POP, POP)
     t1 = time.perf_counter()
-    res = O.combined_scan(p, WS, cfg)
+    res = O.combined_scan(q, WS, cfg)
     dt1 = time.perf_counter() - t1
     return {"value": nwin * reps / dt, "unit": "windows/s", "cores": threads, "kind": "port",
-            "sample": f"the full rank-0 config-2 stream ({p.n} SNPs, {nwin} windows) x {reps} in {dt:.1f} s: "
+            "sample": f"chromosome 0 of the headline genome ({p.n} SNPs, {nwin} windows) x {reps} in {dt:.1f} s: "
                       "oracle/sfs_oracle_c.c (the reference's dense per-window grids and scipy's logpmf "
-                      f"closed form, numpy's pairwise p-sums), OpenMP over windows on {threads} host threads",
+                      f"closed form, numpy's pairwise p-sums; T2D + T1D, no Fst), OpenMP over windows on "
+                      f"{threads} host threads",
             "numpy_oracle_1core": {"value": len(res) / dt1, "unit": "windows/s", "cores": 1,
-                                   "sample": f"oracle/sfs_oracle.combined_scan on the same stream ({dt1:.1f} s)"}}
+                                   "sample": f"oracle/sfs_oracle.combined_scan on its first {q.n} SNPs ({dt1:.1f} s)"}}
 
 
 def end_to_end(n_rec=1_000_000, nchrom=8, seed=3):
@@ -169,84 +180,6 @@ def end_to_end(n_rec=1_000_000, nchrom=8, seed=3):
                         "script's three scans) from the file on disk to the three CSVs written, second run"}
 
 
-def hbm_stream_roofline(eng, steps=5):
-    """BASELINE config 3 on one GPU (5e7 SNPs, 32 chromosomes, ~600 MB read): past the MALL."""
-    from sfs2d.engine import ScanConfig
-    from sfs2d.synth import synth_genome
-    p = synth_genome(32, 1_562_500, POP, POP, seed=777)
-    dev = eng.upload(p)
-    pl = eng.plan(dev, ScanConfig(n1p=POP, n2p=POP, window=WS, fst=True))
-    pl.run()
-    pl.check()
-    pl.set_timing(steps, every=2)
-    pl.run_many(2 * steps)
-    nr, (k1, k2, k3) = pl.timing_read()
-    pl.set_timing(0)
-    pl.check()
-    t0 = time.perf_counter()
-    pl.run_many(4 * steps)
-    pl.check()
-    wall = (time.perf_counter() - t0) / (4 * steps)   # per run, back to back (gaps included)
-    recs = pl.read()
-    nwin = int(((recs["flags"] & 0x80000000) == 0).sum())
-    b3 = algorithmic_bytes(p.n, pl.nrec, nwin, "k3")
-    b1 = algorithmic_bytes(p.n, pl.nrec, nwin, "k1")
-    bp = algorithmic_bytes(p.n, pl.nrec, nwin, "pipeline")
-    out = {"bound": "hbm", "achieved": b3 / (k3 * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": b3 / (k3 * 1e-3) / 1e9 / HBM_PEAK_GBS, "kernel": "k_scan_w", "ms": k3,
-           "k1_GBs": b1 / (k1 * 1e-3) / 1e9, "k1_frac": b1 / (k1 * 1e-3) / 1e9 / HBM_PEAK_GBS, "k1_ms": k1,
-           "k2_ms": k2,
-           "serial": {"pipeline_GBs": bp / wall / 1e9, "pipeline_frac": bp / wall / 1e9 / HBM_PEAK_GBS,
-                      "pipeline_ms": wall * 1e3, "windows_per_s": nwin / wall,
-                      "note": "T2D + T1D + Fst, back-to-back runs of one plan on one stream"},
-           "pipeline_bytes_note": "SURVEY 8(d): 12 B/SNP + 64 B/window per pass over the time per pass; "
-                                  "pipeline_*: independent passes overlapped on 2 HIP streams as in the bench's "
-                                  "own loop (the 'overlapped' entry, T2D + T1D + Fst)",
-           "windows": nwin,
-           "workload": "config 3 stream on 1 GPU: 32 chrom x 1.5625e6 SNPs, 20 kb, per-chromosome bg, T2D + T1D + Fst"}
-    pl.close()
-    # independent passes overlapped on 2 HIP streams (the bench's own mode), the scan kernel capped at one
-    # workgroup per CU so that the next pass's bandwidth-bound k_prep runs beside the previous pass's
-    # compute-bound scan (profiles/r03h_streams_wgs.txt): with Fst (the metric's statistics) and without
-    # (T2D + T1D, the reference's statistics)
-    import torch
-    from sfs2d.engine import Plan
-    streams = [torch.cuda.current_stream().cuda_stream, torch.cuda.Stream().cuda_stream]
-    for key, fst in (("overlapped", True), ("t2d_t1d_overlapped", False)):
-        cfg2 = ScanConfig(n1p=POP, n2p=POP, window=WS, fst=fst, scan_wgs_per_cu=1)
-        plans = [eng.plan(dev, cfg2) for _ in range(2)]
-        outs = [torch.zeros((plans[0].nrec, 64), dtype=torch.uint8, device="cuda") for _ in range(2)]
-        ptrs = [o.data_ptr() for o in outs]
-        Plan.run_streams(plans, streams, 8, ptrs)
-        torch.cuda.synchronize()
-        reps = []   # three repetitions, the median reported (the box's host and neighbours make single runs noisy)
-        for _ in range(3):
-            t0 = time.perf_counter()
-            Plan.run_streams(plans, streams, 8 * steps, ptrs)
-            torch.cuda.synchronize()
-            reps.append((time.perf_counter() - t0) / (8 * steps))
-        wo = sorted(reps)[1]
-        for q in plans:
-            q.check()
-        if not torch.equal(outs[0], outs[1]):
-            raise RuntimeError("config-3 overlapped passes disagree")
-        if fst and not np.array_equal(plans[0].read_fst(), plans[1].read_fst(), equal_nan=True):
-            raise RuntimeError("config-3 overlapped passes disagree (Fst)")
-        out[key] = {
-            "pipeline_GBs": bp / wo / 1e9, "pipeline_frac": bp / wo / 1e9 / HBM_PEAK_GBS, "pipeline_ms": wo * 1e3,
-            "pipeline_ms_reps": [r * 1e3 for r in reps], "windows_per_s": nwin / wo,
-            "note": ("T2D + T1D + Fst" if fst else "T2D + T1D only (the reference's statistics; Hudson Fst not computed)")
-                    + ": 2 plans on 2 HIP streams, passes overlapped, scan kernel capped at 1 workgroup per CU; "
-                      "SURVEY 8(d) bytes over the time per pass"}
-        for q in plans:
-            q.close()
-    dev.close()
-    o = out["overlapped"]
-    out.update({"pipeline_GBs": o["pipeline_GBs"], "pipeline_frac": o["pipeline_frac"], "pipeline_ms": o["pipeline_ms"],
-                "windows_per_s": o["windows_per_s"]})
-    return out
-
-
 def launch_ranks(n):
     """``--gpus N`` with no launcher around this process: start N rank processes of this script
     (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rendezvous on 127.0.0.1) before this process
@@ -278,25 +211,238 @@ def launch_ranks(n):
     return rc
 
 
+class Ctx:
+    """What both workloads share on a rank: the process group, the engine and the library's stream."""
+
+    def __init__(self, world, rank, local):
+        import torch
+        import torch.distributed as dist
+        from sfs2d.engine import Engine
+        self.torch, self.dist = torch, dist
+        self.world, self.rank, self.local = world, rank, local
+        self.cdev = f"cuda:{local}"
+        self.eng = Engine.get(local)
+        self.scan_s = torch.cuda.Stream(device=local)   # the HIP library's stream (and the final gather's)
+        torch.cuda.set_stream(self.scan_s)
+        self.eng.set_stream(self.scan_s.cuda_stream)
+
+    def max_over_ranks(self, x, dtype=None):
+        if self.world == 1:
+            return x
+        torch = self.torch
+        t = torch.tensor([x], dtype=dtype or (torch.float64 if isinstance(x, float) else torch.int64), device=self.cdev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return t.item()
+
+
+def run_loop(cx, plans, steps, warmup, label):
+    """The timed loop shared by both workloads: `warmup` untimed rounds, then exactly `steps` passes
+    round-robin over the plans (plan i % S on stream i % S), then (N > 1) ONE all-gather of every
+    rank's final window table; barrier + synchronize on both sides, the max over ranks.  Returns the
+    wall time, the device time of the passes and of the gather (HIP events on the gather's stream),
+    the host enqueue time, the gathered table (host) and this rank's final table."""
+    torch, dist = cx.torch, cx.dist
+    from sfs2d.engine import Plan
+    ns = len(plans)
+    nrec = plans[0].nrec
+    rows = int(cx.max_over_ranks(nrec))   # tables padded to the largest shard (rows flagged empty)
+    sstreams = [cx.scan_s.cuda_stream] + [torch.cuda.Stream(device=cx.local).cuda_stream for _ in range(ns - 1)]
+    outs = [torch.zeros((rows, 64), dtype=torch.uint8, device=cx.cdev) for _ in range(ns)]
+    for o in outs:
+        o[nrec:, 39] = 0x80   # padding rows: flags = SFS2D_W_EMPTY
+    optrs = [o.data_ptr() for o in outs]
+    gathered = torch.empty((cx.world * rows, 64), dtype=torch.uint8, device=cx.cdev) if cx.world > 1 else None
+    ev_done = [torch.cuda.Event() for _ in range(ns)]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    last = (steps - 1) % ns   # the table the last timed step writes
+
+    def gather_final(k, timed):
+        # the single collective: every rank's final window table to every rank (RCCL over xGMI),
+        # ordered after the passes of all the plans' streams
+        for j, e in enumerate(ev_done):
+            e.record(torch.cuda.ExternalStream(sstreams[j]))
+            cx.scan_s.wait_event(e)
+        if timed:
+            ev[1].record(cx.scan_s)
+        if cx.world > 1:
+            dist.all_gather_into_tensor(gathered, outs[k])
+        if timed:
+            ev[2].record(cx.scan_s)
+
+    plans[0].run(optrs[0])
+    plans[0].check()
+    Plan.run_streams(plans, sstreams, warmup * ns, optrs)
+    gather_final(last, False)
+    torch.cuda.synchronize()
+    if cx.world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev[0].record(cx.scan_s)
+    Plan.run_streams(plans, sstreams, steps, optrs)
+    gather_final(last, True)
+    t_enq = time.perf_counter() - t0   # host time to enqueue the timed steps (diagnostic)
+    torch.cuda.synchronize()
+    if cx.world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    dt = float(cx.max_over_ranks(dt))
+    dev_ms = float(cx.max_over_ranks(float(ev[0].elapsed_time(ev[1]))))
+    gat_ms = float(cx.max_over_ranks(float(ev[1].elapsed_time(ev[2]))))
+    for k, q in enumerate(plans):   # every plan's last pass wrote the same records (independent state)
+        q.check()
+        if not torch.equal(outs[k][:nrec], outs[0][:nrec]):
+            raise RuntimeError(f"{label}: plan {k} on stream {k} disagrees with plan 0")
+    mine = outs[last][:nrec].cpu().numpy()
+    if cx.world > 1:
+        g = gathered.view(cx.world, rows, 64)
+        if not torch.equal(g[cx.rank][:nrec], outs[last][:nrec]):
+            raise RuntimeError(f"{label}: the gathered table disagrees with this rank's own")
+        allr = g.cpu().numpy().reshape(-1, 64)
+    else:
+        allr = mine
+    return {"dt": dt, "device_ms": dev_ms, "gather_ms": gat_ms, "t_enq": t_enq, "rows": rows,
+            "gathered": allr, "mine": mine, "streams": ns}
+
+
+def kernel_times(plan, runs=16):
+    """k_prep / k_bg_slice / scan kernel durations (events in their dispatch packets), one stream, untimed."""
+    plan.set_timing(runs, every=1)
+    plan.run_many(runs)
+    _, (k1, k2, k3) = plan.timing_read()
+    plan.set_timing(0)
+    plan.check()
+    return k1, k2, k3
+
+
+def single_pass_ms(cx, plan, runs=10):
+    """One plan back to back on one stream: the latency of a single pass (no overlap)."""
+    torch = cx.torch
+    plan.run_many(2)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    plan.run_many(runs)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / runs * 1e3
+
+
+def n_windows(table):
+    from sfs2d import _lib as L
+    r = np.frombuffer(np.ascontiguousarray(table).tobytes(), dtype=L.WINDOW_DTYPE)
+    return int(((r["flags"] & L.W_EMPTY) == 0).sum())
+
+
+def config3_cuts(p, cfg, world):
+    """Rank r scans SNPs [cuts[r], cuts[r+1]): sfs2d.dist.split_points (window starts nearest k n / N);
+    when one of them falls inside a chromosome (N not dividing 32), whole-chromosome shards instead
+    (sfs2d.dist.shard_chromosomes), so that no background spans two ranks inside the timed loop."""
+    from sfs2d import dist as D
+    cuts = D.split_points(p, cfg, world)
+    ends = set(p.chrom_off.tolist())
+    if not all(c in ends for c in cuts):
+        sh = D.shard_chromosomes(p.chrom_off, world)
+        cuts = [int(p.chrom_off[a]) for a, _ in sh] + [p.n]
+    return cuts
+
+
+def config3_strong(cx, args):
+    """The headline: config 3, sharded by window over the ranks, strong scaling."""
+    from sfs2d import dist as D
+    from sfs2d.engine import ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(C3_NCHROM, C3_PER, POP, POP, seed=C3_SEED)
+    cfg = ScanConfig(n1p=POP, n2p=POP, window=WS, fst=True, scan_wgs_per_cu=1)
+    cuts = config3_cuts(p, cfg, cx.world)
+    sub, c0 = p.slice_snps(cuts[cx.rank], cuts[cx.rank + 1])
+    dev = cx.eng.upload(sub)
+    ns = 2
+    plans = [cx.eng.plan(dev, cfg) for _ in range(ns)]
+    r = run_loop(cx, plans, args.steps, args.warmup, "config 3")
+    total_windows = n_windows(r["gathered"])
+    win_rank = n_windows(r["mine"])
+    k1, _, k3 = kernel_times(plans[0])
+    one = single_pass_ms(cx, plans[0]) if cx.rank == 0 else None
+    extra = {}
+    if cx.world == 1 and not args.no_variants:
+        # the same loop without Fst (the reference's statistics): what Hudson's Fst costs the pass
+        cfg2 = ScanConfig(n1p=POP, n2p=POP, window=WS, fst=False, scan_wgs_per_cu=1)
+        q = [cx.eng.plan(dev, cfg2) for _ in range(ns)]
+        rr = run_loop(cx, q, args.steps, args.warmup, "config 3 without Fst")
+        extra["t2d_t1d_only"] = {"ms_per_step": rr["dt"] / args.steps * 1e3,
+                                 "windows_per_s": n_windows(rr["gathered"]) * args.steps / rr["dt"],
+                                 "note": "the same loop, T2D + T1D only (Hudson Fst not computed)"}
+        for x in q:
+            x.close()
+    nrec, grids = plans[0].nrec, plans[0].grids()
+    for x in plans:
+        x.close()
+    dev.close()
+    step_s = r["dt"] / args.steps
+    out = {"value": total_windows * args.steps / r["dt"], "ms_per_step": step_s * 1e3,
+           "host_enqueue_ms_per_step": r["t_enq"] / args.steps * 1e3,
+           "device_ms_per_step": r["device_ms"] / args.steps, "gather_ms": r["gather_ms"],
+           "windows": total_windows, "snps": p.n, "cuts": cuts,
+           "rank0": {"snps": sub.n, "windows": win_rank, "slots": nrec, "k_prep_ms": k1, "k_scan_w_ms": k3,
+                     "single_stream_pass_ms": one, "scan_grid_threads": grids[1]}}
+    out.update(extra)
+    return out, p
+
+
+def config2_weak(cx, args):
+    """BASELINE configs[1]: one 1e6-SNP chromosome per rank (seed 12345 + rank), 3 plans on 3 streams."""
+    from sfs2d.engine import ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(1, C2_SNP, POP, POP, seed=C2_SEED + cx.rank)
+    dev = cx.eng.upload(p)
+    cfg = ScanConfig(n1p=POP, n2p=POP, window=WS, fst=True)
+    ns = max(1, args.streams)
+    plans = [cx.eng.plan(dev, cfg) for _ in range(ns)]
+    steps = max(args.steps, args.config2_steps)
+    r = run_loop(cx, plans, steps, max(args.warmup, 20), "config 2")
+    k1, k2, k3 = kernel_times(plans[0])
+    one = single_pass_ms(cx, plans[0], 40) if cx.rank == 0 else None
+    nrec, grids = plans[0].nrec, plans[0].grids()
+    for x in plans[::-1]:
+        x.close()
+    dev.close()
+    total = n_windows(r["gathered"])
+    nwin = n_windows(r["mine"])
+    b3 = algorithmic_bytes(p.n, nrec, nwin, "k3")
+    ach = b3 / (k3 * 1e-3) / 1e9
+    traffic, tsrc = pmc_traffic("k_scan_w", grids[1])
+    return {"value": total * steps / r["dt"], "unit": "windows/s", "scaling": "weak", "steps": steps,
+            "ms_per_step": r["dt"] / steps * 1e3, "host_enqueue_ms_per_step": r["t_enq"] / steps * 1e3,
+            "single_stream_pass_ms": one,
+            "workload": "configs[1]: synthetic 1 chromosome x 1e6 SNPs per GPU (seed 12345 + rank), 20 kb, "
+                        "per-chromosome background, T2D + T1D + Fst",
+            "windows_per_gpu": nwin, "windows_all_gpus": total,
+            "parallelism": f"one chromosome per GPU, {ns} plans on {ns} HIP streams (passes overlap)"
+                           + ("; one RCCL all-gather of the final tables" if cx.world > 1 else ""),
+            "kernels_ms": {"k_prep": k1, "k_bg_slice": k2, "k_scan_w": k3},
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                         "traffic": traffic, "kernel": "k_scan_w", "ms": k3, "algorithmic_bytes": b3,
+                         "note": "the 8 MB stream is MALL-resident: not an HBM measurement; traffic: "
+                                 + (tsrc or "no PMC pass committed")}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=400)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-hbm-stream", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the VCF -> CSV end-to-end timing")
-    ap.add_argument("--streams", type=int, default=3,
-                    help="consecutive steps round-robin over this many plans, each on its own HIP stream "
-                         "(independent passes overlap; sfs2d_plan_run_streams)")
+    ap.add_argument("--no-config2", action="store_true", help="skip the config-2 (weak scaling) key")
+    ap.add_argument("--no-variants", action="store_true", help="skip the config-3 run without Fst")
+    ap.add_argument("--streams", type=int, default=3, help="config 2: plans / HIP streams (passes overlap)")
+    ap.add_argument("--config2-steps", type=int, default=400, help="config 2: at least this many passes")
     args = ap.parse_args()
-    if args.gpus < 1:
-        raise SystemExit("--gpus must be >= 1")
-    # hardware queues per process: HIP maps streams onto GPU_MAX_HW_QUEUES queues (4 on the box); S
+    if args.gpus < 1 or args.steps < 1:
+        raise SystemExit("--gpus and --steps must be >= 1")
+    # hardware queues per process: HIP maps streams onto GPU_MAX_HW_QUEUES queues (4 on the box); the
     # pass streams + the library's and torch's own need more than 4 or two passes share a queue and
-    # serialise (3 streams: 1.35e8 windows/s with 4 queues, 1.92-1.94e8 with 6-8; profiles/r02h_*).
-    # Set before the HIP runtime starts (torch imported below; rank processes inherit it).
-    need = max(1, args.streams) + 4
+    # serialise (profiles/r02h_*).  Set before the HIP runtime starts (rank processes inherit it).
+    need = max(2, args.streams) + 4
     if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < need:
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(8, need)))
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -319,158 +465,56 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29517")
         dist.init_process_group("nccl", rank=rank, world_size=world)
         world = dist.get_world_size()   # n_gpus from the communicator
+    cx = Ctx(world, rank, local)
 
-    from sfs2d import _lib as L
-    from sfs2d.engine import Engine, Plan, ScanConfig
-    from sfs2d.synth import synth_genome
-
-    # weak scaling: every rank scans its own chromosome (seed 12345 + rank) -- whole chromosomes are
-    # the shard unit of per-chromosome-background scans
-    p = synth_genome(1, N_SNP, POP, POP, seed=12345 + rank)
-    eng = Engine.get(local)
-    scan_s = torch.cuda.Stream(device=local)    # the HIP library's stream (and the final gather's)
-    torch.cuda.set_stream(scan_s)
-    eng.set_stream(scan_s.cuda_stream)
-    dev = eng.upload(p)
-    cfg = ScanConfig(n1p=POP, n2p=POP, window=WS, fst=True)
-    ns = max(1, args.streams)
-    plans = [eng.plan(dev, cfg) for _ in range(ns)]
-    pl = plans[0]
-    nrec = pl.nrec
-    cdev = f"cuda:{local}"
-    rows = nrec
-    if world > 1:   # shards differ in window count: tables are padded to the largest (rows flagged empty)
-        c = torch.tensor([nrec], dtype=torch.int64, device=cdev)
-        dist.all_reduce(c, op=dist.ReduceOp.MAX)
-        rows = int(c.item())
-    sstreams = [scan_s.cuda_stream] + [torch.cuda.Stream(device=local).cuda_stream for _ in range(ns - 1)]
-    ev_done = [torch.cuda.Event() for _ in range(ns)]
-    outs = [torch.zeros((rows, 64), dtype=torch.uint8, device=cdev) for _ in range(ns)]
-    for o in outs:
-        o[nrec:, 39] = 0x80   # padding rows: flags = SFS2D_W_EMPTY
-    optrs = [o.data_ptr() for o in outs]
-    gathered = torch.empty((world * rows, 64), dtype=torch.uint8, device=cdev) if world > 1 else None
-    last = (args.steps - 1) % ns   # the table the last timed step writes
-
-    def gather_final(k):
-        # the single collective: every rank's final window table to every rank (RCCL over xGMI),
-        # ordered after the scans of all the plans' streams
-        for j, e in enumerate(ev_done):
-            e.record(torch.cuda.ExternalStream(sstreams[j]))
-            scan_s.wait_event(e)
-        dist.all_gather_into_tensor(gathered, outs[k])
-
-    pl.run(optrs[0])
-    pl.check()
-    # warmup: the same loop, and (N > 1) the collective once (RCCL communicators are made lazily)
-    Plan.run_streams(plans, sstreams, args.warmup * ns, optrs)
-    if world > 1:
-        gather_final(last)
-    torch.cuda.synchronize()
-    # HIP events around the scan kernel (the roofline's) and k_bg_slice of sampled timed runs of plan 0,
-    # carried in their dispatch packets on the stream the kernels run on (events around all three
-    # kernels of every 8th run cost ~2 us per step, around these two ~1 us: tools/timing_overhead.py);
-    # k_prep is timed in an untimed pass after the timed loop.  Short runs (the driver's 20 steps)
-    # sample every 2nd run of plan 0 so that the average is over >= 5 launches.
-    every = 8 if args.steps >= 160 else 2
-    pl.set_timing(args.steps, every=every, kernels=6)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    # the timed loop, the same at every N: step i = one scan pass of plan i % ns on stream i % ns;
-    # with N > 1 ranks, then one gather of the final window tables
-    Plan.run_streams(plans, sstreams, args.steps, optrs)
-    if world > 1:
-        gather_final(last)
-    t_enq = time.perf_counter() - t0   # host time to enqueue the timed steps (diagnostic)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=cdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    nr, (_, k2, k3) = pl.timing_read()
-    pl.set_timing(16, every=1)   # k_prep (and the other two again), one stream, outside the timed region
-    pl.run_many(16, optrs[0])
-    _, (k1, _, k3_untimed) = pl.timing_read()
-    pl.set_timing(0)
-    for k, q in enumerate(plans):   # every plan's last pass wrote the same records (independent state)
-        q.check()
-        if not torch.equal(outs[k][:nrec], outs[0][:nrec]):
-            raise RuntimeError(f"plan {k} on stream {k} disagrees with plan 0")
-    recs = np.frombuffer(outs[0][:nrec].cpu().numpy().tobytes(), dtype=L.WINDOW_DTYPE)
-    nwin_rank = int(((recs["flags"] & L.W_EMPTY) == 0).sum())
-    total_windows = nwin_rank
-    if world > 1:
-        g = gathered.view(world, rows, 64)
-        if not torch.equal(g[rank][:nrec], outs[0][:nrec]):
-            raise RuntimeError("the gathered table disagrees with this rank's own")
-        allr = np.frombuffer(g.cpu().numpy().tobytes(), dtype=L.WINDOW_DTYPE)
-        total_windows = int(((allr["flags"] & L.W_EMPTY) == 0).sum())
-    value = total_windows * args.steps / dt
+    c3, genome = config3_strong(cx, args)
+    c2 = None if args.no_config2 else config2_weak(cx, args)
 
     if rank == 0:
-        b3 = algorithmic_bytes(p.n, nrec, nwin_rank, "k3")
-        # the roofline's duration: with overlapped passes (ns > 1) a kernel's event interval in the
-        # timed region also holds the time its workgroups wait for CUs that the other passes' kernels
-        # occupy (k_scan_w 14-16 us there vs 9.5-9.8 us in rocprofv3's kernel trace of the same
-        # command), so the kernel's own duration comes from the single-stream pass of 16 runs after
-        # the timed loop (the same kernel, data and dispatch-packet events)
-        k3_roof = k3_untimed if ns > 1 else k3
-        achieved = b3 / (k3_roof * 1e-3) / 1e9
-        bp = algorithmic_bytes(p.n, nrec, nwin_rank, "pipeline") * world
-        step_s = dt / args.steps
-        traffic, tsrc = pmc_traffic("k_scan_w", pl.grids()[1])
+        r0 = c3["rank0"]
+        b3 = algorithmic_bytes(r0["snps"], r0["slots"], r0["windows"], "k3")
+        ach = b3 / (r0["k_scan_w_ms"] * 1e-3) / 1e9
+        bp = algorithmic_bytes(c3["snps"], 0, c3["windows"], "pipeline")
+        step_s = c3["ms_per_step"] * 1e-3
+        traffic, tsrc = pmc_traffic("k_scan_w", r0["scan_grid_threads"])
         line = {
-            "metric": "genomic windows/s (T2D+T1D+Fst) at 20 kb, n1=n2=50; HBM GB/s fraction",
-            "value": value, "unit": "windows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": dt / args.steps * 1e3, "host_enqueue_ms_per_step": t_enq / args.steps * 1e3,
-            "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f64", "data": "synthetic (SURVEY 8d generator, seed 12345+rank)",
-            "config": {"workload": "configs[1]: synthetic 1 chromosome x 1e6 SNPs per GPU, 20 kb windows, "
-                                   "n1=n2=50 haploid (pop_size 25/25), per-chromosome background",
-                       "snps_per_gpu": p.n, "windows_per_gpu": nwin_rank, "windows_all_gpus": total_windows,
-                       "window_bp": WS,
+            "metric": METRIC, "value": c3["value"], "unit": "windows/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": c3["ms_per_step"], "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic (SURVEY 8d generator, seed 777)",
+            "config": {"workload": "configs[2]: synthetic whole genome, 32 chromosomes x 1.5625e6 = 5e7 SNPs, 20 kb "
+                                   "windows, n1=n2=50 haploid (pop_size 25/25), per-chromosome background, "
+                                   "sharded by window over the GPUs",
+                       "snps": c3["snps"], "windows": c3["windows"], "window_bp": WS,
                        "stats": "T2D, T1D_p1, T1D_p2 (reference semantics) + Hudson Fst (DESIGN.md; not in the "
                                 "reference, parity vs its own oracle restatement)",
-                       "parallelism": f"one chromosome per GPU ({world} GPU(s)), no data-path collective; "
-                                      f"{ns} plans on {ns} HIP streams, steps round-robin (passes overlap)"
-                                      + ("; one RCCL all-gather of the final window tables in the timed region"
-                                         if world > 1 else "")},
-            "kernels_ms": {"k_prep": k1, "k_bg_slice": k2, "k_scan_w": k3, "k_scan_w_untimed_pass": k3_untimed,
-                           "timed_runs_sampled": nr, "exact_path_windows": pl.stats(),
-                           "note": f"k_bg_slice / k_scan_w: events in every {every}th timed run of plan 0; k_prep: 16 "
-                                   "runs after the timed loop (one stream, untimed)"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_scan_w", "ms": k3_roof, "ms_timed_region": k3, "algorithmic_bytes": b3,
-                         "note": "k_scan_w: algorithmic bytes 4 B/SNP + 96 B/slot per launch over its average "
-                                 + (f"duration in the single-stream pass of 16 runs after the timed loop (kernel "
-                                    "start/end events in the dispatch packets; in the timed region, every "
-                                    f"{every}th run of plan 0, the interval also holds the wait for CUs held by "
-                                    "the other streams' passes: ms_timed_region); " if ns > 1 else
-                                    f"duration (kernel start/end events in the dispatch packets of every {every}th "
-                                    "timed run); ")
-                                 + "the 8 MB config-2 stream is MALL-resident (see roofline_hbm for the HBM-sized "
-                                 "stream); traffic: " + (tsrc or "no PMC pass committed")},
+                       "parallelism": f"{world} GPU(s), SNP ranges cut at window starts ({c3['cuts']}: chromosome "
+                                      "ends, no background exchange); 2 plans on 2 HIP streams per GPU, passes "
+                                      "overlapped" + ("; one RCCL all-gather of the final window tables in the "
+                                                      "timed region" if world > 1 else "")},
+            "host_enqueue_ms_per_step": c3["host_enqueue_ms_per_step"],
+            "device_ms_per_step": c3["device_ms_per_step"], "gather_ms": c3["gather_ms"],
+            "rank0": r0,
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_scan_w",
+                         "ms": r0["k_scan_w_ms"], "algorithmic_bytes": b3,
+                         "note": "k_scan_w on rank 0's shard: 4 B/SNP + 96 B/slot per launch over its average duration "
+                                 "(kernel start/end events in the dispatch packets, 16 runs on one stream after the "
+                                 "timed loop); traffic: " + (tsrc or "no PMC pass committed")},
             "roofline_pipeline": {"bound": "hbm", "achieved": bp / step_s / 1e9, "peak": HBM_PEAK_GBS * world,
                                   "unit": "GB/s", "frac": bp / step_s / 1e9 / (HBM_PEAK_GBS * world),
                                   "note": "whole step over all GPUs (SURVEY 8(d): 12 B/SNP + 64 B/window) over "
                                           "ms_per_step"},
         }
-        if not args.no_hbm_stream and world == 1:
-            line["roofline_hbm"] = hbm_stream_roofline(eng)
+        if "t2d_t1d_only" in c3:
+            line["t2d_t1d_only"] = c3["t2d_t1d_only"]
+            line["fst_cost"] = c3["ms_per_step"] / c3["t2d_t1d_only"]["ms_per_step"] - 1.0
+        if c2 is not None:
+            line["config2_weak"] = c2
         if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(p)
+            line["cpu_baseline"] = cpu_baseline(genome.subset_chroms([0]))
         if not args.no_e2e and world == 1:
             line["end_to_end_vcf_csv"] = end_to_end()
         print(json.dumps(line), flush=True)
-    for q in plans[::-1]:
-        q.close()
-    dev.close()
     if world > 1:
         dist.destroy_process_group()
 
