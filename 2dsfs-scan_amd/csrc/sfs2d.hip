@@ -196,6 +196,7 @@ struct sfs2d_plan {
   uint32_t fst_m = 0;             // attached Fst: base windows per window (their sums add)
   bool fst_win = false;           // Fst by window kernels (fst_windows) instead of k_prep's sums
   bool fst_scan = false;          // Fst summed by k_scan_w itself (counts plans, small grids): k_prep has no Fst work
+  bool lite = false;              // k_scan_wl instead of k_scan_w (counts plans, small grids: six waves per SIMD)
   int nfst = 0;                   // k_bg_slice's extra Fst workgroups
 };
 
@@ -281,10 +282,30 @@ void launch_scan_gw(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
                      pl->d_ctr, (int)(pl->runs & 1), pl->d_leafsum, pl->d_bg1d, 0, pl->d_gscr, pl->nscr);
 }
 
+template <bool FUSED, int FST>
+void launch_scan_wl(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
+  hipExtLaunchKernelGGL((k_scan_wl<FUSED, FST>), dim3((unsigned)pl->chunks.size()), dim3(SBLOCK), pl->scan_lds,
+                     CTX_STREAM(pl->ctx), pl->kev[4], pl->kev[5], 0, pl->K, scan_src(pl), pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
+                     per_chrom, pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, bp, pl->d_repl, pl->d_bcount,
+                     plan_par(pl), pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels,
+                     pl->extra_rec >= 0 ? (int)pl->last_chrom : -1, pl->d_fsum, pl->d_fst, pl->d_ctr,
+                     (int)(pl->runs & 1), pl->d_leafsum, pl->d_bg1d, pl->sliced ? 1 : 0, pl->d_gscr, pl->nscr);
+}
+
 template <bool P16, bool CNT>
 hipError_t launch_scan_c(sfs2d_plan* pl, sfs2d_window* out) {
   const int per_chrom = pl->prm.bg_mode == SFS2D_BG_PER_CHROM ? 1 : 0;
   const int bp = pl->prm.window_mode == SFS2D_WINDOW_BP ? 1 : 0;
+  if (CNT && pl->lite) {
+    if (pl->fused) {
+      if (pl->fst) launch_scan_wl<true, 2>(pl, out, per_chrom, bp);
+      else launch_scan_wl<true, 0>(pl, out, per_chrom, bp);
+    } else {
+      if (pl->fst) launch_scan_wl<false, 2>(pl, out, per_chrom, bp);
+      else launch_scan_wl<false, 0>(pl, out, per_chrom, bp);
+    }
+    return hipGetLastError();
+  }
   if (pl->gw) {
     if (pl->fst) launch_scan_gw<P16, true, CNT>(pl, out, per_chrom, bp);
     else launch_scan_gw<P16, false, CNT>(pl, out, per_chrom, bp);
@@ -904,6 +925,35 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
       if (hipFuncGetAttributes(&fa, f) != hipSuccess || pl->scan_lds + fa.sharedSizeBytes > 160 * 1024) pl->fst_scan = false;
     }
   }
+  // k_scan_wl (six waves per SIMD: u8 2D bins, 2 1D replicas, three workgroups per CU) for counts plans on
+  // the small-grid path whose Fst, if any, is summed in the scan, when more of its workgroups fit a CU
+  // than k_scan_w's.  SFS2D_LITE=0/1 forces the choice (where the kernel can run the plan).
+  const PwTree pw = pw_plan(K.nb2 - 3);
+  {
+    const bool can = pl->cnt && pl->G == WAVE && !pl->gw;
+    int occ_l = 0, occ_w = 0;
+    if (can) {
+      const size_t lds_l = wl_lds_bytes(K.nb2, K.n1p, K.n2p, K.nt, (int)pw.leaves.size(), (int)pw.nodes.size(),
+                                        pl->fused ? 1 : 0, pl->sliced ? 1 : 0);
+      const void* fl = pl->fused ? (pl->fst ? (const void*)k_scan_wl<true, 2> : (const void*)k_scan_wl<true, 0>)
+                                 : (pl->fst ? (const void*)k_scan_wl<false, 2> : (const void*)k_scan_wl<false, 0>);
+      if (lds_l > 64 * 1024) hipFuncSetAttribute(fl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::min<size_t>(lds_l, 160 * 1024));
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_l, fl, SBLOCK, lds_l) != hipSuccess) occ_l = 0;
+      (void)hipGetLastError();
+      const void* fw = pl->fst_scan ? (pl->fused ? (const void*)k_scan_w<true, true, 2, true> : (const void*)k_scan_w<true, false, 2, true>)
+                                    : (pl->fused ? (const void*)k_scan_w<true, true, false, true> : (const void*)k_scan_w<true, false, false, true>);
+      if (pl->scan_lds > 64 * 1024)
+        hipFuncSetAttribute(fw, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::min<size_t>(pl->scan_lds, 160 * 1024));
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_w, fw, SBLOCK, pl->scan_lds) != hipSuccess) occ_w = 0;
+      (void)hipGetLastError();
+      pl->lite = occ_l > occ_w;
+      if (const char* ev = std::getenv("SFS2D_LITE")) pl->lite = occ_l >= 1 && ev[0] == '1';
+      if (pl->lite) {
+        pl->scan_lds = lds_l;
+        pl->fst_scan = pl->fst;   // Fst summed in the scan
+      }
+    }
+  }
   pl->fst_win = pl->sliced && bp && pl->fst && !pl->fst_scan;
   pl->nfst = pl->fst_win ? (int)std::min<int64_t>(1024, std::max<int64_t>(1, (pl->nslots + 7) / 8)) : 0;   // ~1 window per wave
   if (pl->scan_lds > 64 * 1024) {
@@ -940,7 +990,10 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
     int occ = 0;
     // (the grid is one dispatch wave of resident workgroups: occupancy of the variant that runs)
     hipError_t oe;
-    if (pl->gw)
+    if (pl->lite)
+      oe = pl->fused ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_wl<true, 2>, SBLOCK, pl->scan_lds)
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_wl<false, 2>, SBLOCK, pl->scan_lds);
+    else if (pl->gw)
       oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<true, true, true>, WAVE, pl->scan_lds)
                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<false, true, true>, WAVE, pl->scan_lds);
     else if (pl->fst_scan && pl->fused)
@@ -959,6 +1012,8 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
     if (prm->scan_wgs_per_cu > 0 && (int)prm->scan_wgs_per_cu < occ) occ = (int)prm->scan_wgs_per_cu;
     int64_t cap = (int64_t)occ * ctx->ncu;
     if (pl->gw) pl->nscr = (int)cap;   // one exact-path histogram per resident wavefront
+    // k_scan_wl: exact evaluations are rare (|T| ~ 0, a wrapped u8 bin): a few shared slots, taken by CAS
+    if (pl->lite) pl->nscr = (int)std::min<int64_t>(256, cap * (SBLOCK / WAVE));
     if (const char* ev = std::getenv("SFS2D_WGS")) cap = std::max<int64_t>(1, std::atoll(ev));   // tuning
     const double S = (double)std::max<unsigned long long>(1, slot_base[nc] - slot_base[0]);
     const uint32_t NW = pl->gw ? 1u : (uint32_t)(SBLOCK / WAVE);   // wavefronts per workgroup
@@ -1077,7 +1132,6 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
 
   // numpy pairwise plan over the 2D inner bins except the last (p[:-1] of bins[1:-1]) and the
   // k_bg_slice bin ranges: LEAVES_PER_SLICE leaves each, the first from bin 0, the last to nb2
-  const PwTree pw = pw_plan(K.nb2 - 3);
   pl->nleaves = (int)pw.leaves.size();
   pl->nnodes = (int)pw.nodes.size();
   pl->nlevels = pw.nlevels;
@@ -1103,8 +1157,8 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   rc = rc ? rc : dalloc(ctx, &pl->d_done, (size_t)pl->nbg);
   const size_t nctr = (size_t)2 * std::max(1, nc) * CTR_POOLS * CTR_STRIDE;
   rc = rc ? rc : dalloc(ctx, &pl->d_ctr, nctr);
-  const size_t ngscr = pl->gw ? (size_t)pl->nscr * (K.nb2 + 1) : 0;
-  if (pl->gw) rc = rc ? rc : dalloc(ctx, &pl->d_gscr, ngscr);
+  const size_t ngscr = (pl->gw || pl->lite) ? (size_t)pl->nscr * (K.nb2 + 1) : 0;
+  if (pl->gw || pl->lite) rc = rc ? rc : dalloc(ctx, &pl->d_gscr, ngscr);
   rc = rc ? rc : dalloc(ctx, &pl->d_bgval, (size_t)pl->nbg * K.nt);
   rc = rc ? rc : dalloc(ctx, &pl->d_tab, (size_t)pl->nbg * K.nt);
   rc = rc ? rc : dalloc(ctx, &pl->d_lp, (size_t)pl->nbg * K.nt);
@@ -1134,7 +1188,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_bcount, 0, sizeof(uint32_t) * 2 * std::max(1, nc), st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_done, 0, sizeof(uint32_t) * pl->nbg, st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_ctr, 0, sizeof(uint32_t) * nctr, st);
-  if (e == hipSuccess && pl->gw) e = hipMemsetAsync(pl->d_gscr, 0, sizeof(uint32_t) * ngscr, st);
+  if (e == hipSuccess && (pl->gw || pl->lite)) e = hipMemsetAsync(pl->d_gscr, 0, sizeof(uint32_t) * ngscr, st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_err, 0, 4 * sizeof(uint32_t), st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_bins, 0, sizeof(uint32_t) * nbins, st);
   if (e == hipSuccess && pl->fst) e = hipMemsetAsync(pl->d_fsum, 0, sizeof(unsigned long long) * 2 * ((size_t)pl->nslots + 1), st);
@@ -1543,7 +1597,8 @@ int sfs2d_plan_attach(sfs2d_plan* base, const sfs2d_params* prm, sfs2d_plan** ou
   sfs2d_plan* a = nullptr;
   int rc = plan_create(ctx, base->data, prm, base->sliced ? 1 : 0, &a);
   if (rc) return rc;
-  if (a->fused != base->fused || a->sliced != base->sliced || a->G != base->G || a->cnt != base->cnt) {
+  if (a->fused != base->fused || a->sliced != base->sliced || a->G != base->G || a->cnt != base->cnt ||
+      a->lite != base->lite) {
     plan_free(a); delete a;
     return set_err(ctx, SFS2D_E_ARG, "attached plan would take a different kernel path than its base");
   }

@@ -1581,7 +1581,8 @@ __device__ __forceinline__ void fused_table(int nb2, int nh, int nt, int n1p, in
                                                       BgHead* __restrict__ head, double* LPl, uint32_t* HB,
                                                       const int2* __restrict__ leaves, int nleaves,
                                                       const int4* __restrict__ nodes, int nnodes, int nlevels,
-                                                      const double* __restrict__ lnx, BgHead* hb_out) {
+                                                      const double* __restrict__ lnx, BgHead* hb_out,
+                                                      double* lsum, uint32_t* vcnt) {
   __shared__ double sh_misc[8];
   __shared__ double sh_lnb[3];
   __shared__ uint32_t sh_flags;
@@ -1597,8 +1598,8 @@ __device__ __forceinline__ void fused_table(int nb2, int nh, int nt, int n1p, in
   double* p1a = scr + 264;           // 128
   double* p1b = scr + 392;           // 128
   double* acc8 = scr + 512;          // 8 per leaf (<= 128 leaves)
-  double* lsum = scr + 1536;         // <= 128 leaves + 127 nodes
-  uint32_t* vcnt = HB + FUSED_VCNT;  // the table's counts (2D, then folded 1D), nt words
+  // lsum: leaf sums and tree nodes (nleaves + nnodes); vcnt: the table's counts (2D, then folded 1D),
+  // nt words -- both in HB past acc8 (k_scan_w: fixed offsets; k_scan_wl: packed after this grid's leaves)
   const double B2 = (double)bcount[(size_t)par * nchrom + chrom];
   const int4 my_node = tid < nnodes ? nodes[tid] : make_int4(0, 0, -1, 0);
   const int2 my_leaf = tid < nleaves ? leaves[tid] : make_int2(0, 0);   // this thread's leaf to combine
@@ -1925,7 +1926,7 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
     fused_table(P.nb2, P.nh, P.nt, P.n1p, P.n2p, P.n1, P.n2, P.t1a, P.t1b, P.nchrom, ch.chrom,
                 ch.first == 0 && (int)ch.chrom == write_chrom, bg,
                 Rc, rs, repl, bcount, par, tab, LPg, head, LPl, HB, leaves, nleaves, nodes, nnodes, nlevels, lnx,
-                &sh_hb);
+                &sh_hb, reinterpret_cast<double*>(HB) + 1536, HB + FUSED_VCNT);
     hb = sh_hb;
   }
   for (int k = lane; k < per / 4; k += WAVE) reinterpret_cast<uint4*>(W)[k] = make_uint4(0, 0, 0, 0);
@@ -2535,7 +2536,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     fused_table(P.nb2, P.nh, P.nt, P.n1p, P.n2p, P.n1, P.n2, P.t1a, P.t1b, P.nchrom, ch.chrom,
                 ch.first == 0 && (int)ch.chrom == write_chrom, bg,
                 Rc, rs, repl, bcount, par, tab, LPg, head, LPl, HB, leaves, nleaves, nodes, nnodes, nlevels, lnx,
-                &sh_hb);
+                &sh_hb, reinterpret_cast<double*>(HB) + 1536, HB + FUSED_VCNT);
     hb = sh_hb;
   }
   for (int k = lane; k < per / 4; k += WAVE) reinterpret_cast<uint4*>(W)[k] = make_uint4(0, 0, 0, 0);
@@ -2971,6 +2972,526 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   __builtin_amdgcn_s_barrier();   // diagnostic build only: the block's end is its last active wave's
 #endif
   BLK_STAMP(1, 1);
+}
+
+// ------------------------------------------------------------------------------------------ K3, lite
+// k_scan_wl: the window scan of counts plans on small grids (no filter: the scan classifies the
+// counts it streams; Fst summed in the scan or off), laid out for SIX wavefronts per SIMD -- three
+// 512-thread workgroups per CU and <= 80 VGPRs -- where k_scan_w (two workgroups, 128 VGPRs) runs
+// four: that kernel waits on memory / LDS for ~55% of its wave cycles on config 3
+// (profiles/r03x_pmc_config3_fst.csv).  Per workgroup: the background's lp table, D(r) for r < 256,
+// and per wavefront its 2D histogram with u8-packed bins (a quarter of u32 bins: 652 words at 51 x 51)
+// and two lane-&-1 replicas of each folded 1D spectrum.  A rank of 255 returned by a 2D atomic means
+// the byte wrapped (>= 256 SNPs of the window in one bin): the window is re-evaluated exactly, on a
+// u32 histogram in global memory (gscr, as k_scan_gw), like windows of >= 65535 SNPs and windows whose
+// |T| is ~0 (the exact-zero rule).  Window schedule three deep: at window i's start the rows of window
+// i+1 are issued (its slot record arrived during window i-1), the slot record of window i+2 is loaded
+// (its pool index arrived during window i-1) and the pool atomic for window i+3 issued, so a window's
+// rows have a whole window's time to arrive from HBM.  The window loop, the batched finish (8 windows
+// per flush, evaluated per lane) and the numerics are k_scan_w's.
+constexpr int LDT = 256;   // D(r) in LDS: u8 ranks (255 = the byte wrapped)
+constexpr int R1L = 2;     // folded 1D replicas per bin (lane & 1)
+
+__host__ __device__ inline int wl_h2w(int nb2) { return ((nb2 + 3) / 4 + 3) & ~3; }   // u8-packed 2D words, 16-B rows
+__host__ __device__ inline int wl_per(int nb2, int n1p, int n2p) {                     // words per wavefront
+  return (wl_h2w(nb2) + R1L * (n1p + 1) + R1L * (n2p + 1) + 3) & ~3;
+}
+// fused prologue scratch in the histogram area (fused_table): u1 words [0, 512) | p1a, p1b (doubles
+// 264.., 392..) | acc8 (double 512, 8 per leaf) | lsum (leaves + nodes) | vcnt (nt words)
+__host__ __device__ inline int wl_lsum_off(int nleaves) { return 512 + 8 * nleaves; }   // doubles
+__host__ __device__ inline int wl_vcnt_off(int nleaves, int nnodes) {                  // words (16-B aligned)
+  return (2 * (wl_lsum_off(nleaves) + nleaves + nnodes) + 3) & ~3;
+}
+// words of a workgroup's histogram area: the 8 wavefronts', or the prologue's scratch if larger
+__host__ __device__ inline int wl_hb_words(int nb2, int n1p, int n2p, int nt, int nleaves, int nnodes, int fused,
+                                           int sliced) {
+  int w = (SBLOCK / WAVE) * wl_per(nb2, n1p, n2p);
+  if (fused) w = w > wl_vcnt_off(nleaves, nnodes) + nt + 16 ? w : wl_vcnt_off(nleaves, nnodes) + nt + 16;
+  if (sliced) w = w > 2 * (nleaves + nnodes) ? w : 2 * (nleaves + nnodes);
+  return w;
+}
+// LDS bytes of a k_scan_wl workgroup besides its static arrays: lp | D | histogram area
+__host__ __device__ inline size_t wl_lds_bytes(int nb2, int n1p, int n2p, int nt, int nleaves, int nnodes, int fused,
+                                               int sliced) {
+  return sizeof(double) * (size_t)(((nt + 1) & ~1) + LDT) +
+         4 * (size_t)wl_hb_words(nb2, n1p, n2p, nt, nleaves, nnodes, fused, sliced);
+}
+
+// what only the batch finish and the exact path read, parked in LDS for the window loop's duration (read
+// back behind a compiler barrier): kept in scalar registers, these values and the kernel arguments they
+// come from spilled the loop's own to VGPR lanes (v_readlane / v_writelane inside the loop)
+struct WlCold {
+  KParams P;
+  sfs2d_window* out;
+  double* fst_out;
+  uint32_t* err_word;
+  uint32_t* gscr;
+  const PL* tab;          // this chromosome's background table (global)
+  const uint32_t* Rc;     // this chromosome's replicas (fused plans)
+  unsigned long long rs;  // replica stride
+  BgHead hb;
+  uint32_t chrom, wid_lo, slot_lo, nscr, zflags, nanf;
+};
+
+// k_scan_wl's exact re-evaluation of one window (rare), out of line: its register needs stay out of the
+// window loop's allocation (live values are saved around the call only when it runs).  A u32 histogram in
+// global memory (a gscr slot taken by CAS, as k_scan_gw), the folded 1D spectra in the wave's LDS replicas
+// (stride R1L, clean before and after); the record written by lane 0.
+template <bool FUSED>
+__device__ __noinline__ void wl_exact(const WlCold* Cp, const double* LPl, const uint32_t* __restrict__ bins,
+                                      uint32_t* H1a, uint32_t* H1b, const double* __restrict__ lnx, uint32_t xs,
+                                      uint32_t xb, uint32_t xe, uint32_t sl) {
+  const WlCold& C = *Cp;
+  const KParams PC = C.P;
+  const uint32_t nscr_ = C.nscr;
+  uint32_t* gs = C.gscr;
+  uint32_t* lock = gs + (size_t)nscr_ * PC.nb2;
+  const int lane = threadIdx.x & (WAVE - 1);
+  sl %= nscr_;
+  for (;;) {
+    uint32_t got = 1u;
+    if (lane == 0) got = atomicCAS(&lock[sl], 0u, 1u);
+    if (__builtin_amdgcn_readfirstlane(got) == 0u) break;
+    sl = sl + 1u == nscr_ ? 0u : sl + 1u;
+  }
+  const BgHead hbc = C.hb;
+  WinOut x;
+  if (FUSED)
+    x = eval_exact<WAVE, false, R1L, true>(PC, bins, xb, xe,
+                                           TabFused{LPl, C.Rc, (size_t)C.rs, PC.nb2, PC.n1, PC.n2, PC.n1p, PC.h1a, PC.h1b,
+                                                    PC.t1a, PC.t1b},
+                                           hbc, lnx, gs + (size_t)sl * PC.nb2, H1a, H1b, nullptr, nullptr);
+  else
+    x = eval_exact<WAVE, false, R1L, true>(PC, bins, xb, xe, TabLocal{C.tab, LPl}, hbc, lnx, gs + (size_t)sl * PC.nb2,
+                                           H1a, H1b, nullptr, nullptr);
+  __threadfence();   // the slot's words are clean again before it is released
+  if (lane == 0) {
+    atomicExch(&lock[sl], 0u);
+    write_rec(C.out + xs, C.chrom, C.wid_lo + (xs - C.slot_lo), xb, xe, x, C.zflags);
+    atomicAdd(C.err_word + 1, 1u);   // statistics: windows that took the exact path
+  }
+}
+
+template <bool FUSED, int FST>
+__device__ __forceinline__ void scan_wl(double* ldsd, SCAN_W_ARGS) {
+  constexpr bool FSTIN = FST == 2;
+  static_assert(FST == 0 || FST == 2, "k_scan_wl: Fst summed in the scan, or none");
+  constexpr int NWV = SBLOCK / WAVE;
+  constexpr int SB = 8;   // windows per batch
+  __shared__ BgHead sh_hb;
+  __shared__ double sh_bd[NWV][3][SB];      // batch: the three sums of window j
+  __shared__ uint32_t sh_bu[NWV][6][SB];    // batch: slot, begin, end, n2 | n2_all, n1a | n1b, nvar | exact << 31
+  __shared__ double sh_bf[NWV][FSTIN ? 2 : 1][SB];   // batch (FSTIN): the two Fst sums
+  __shared__ WlCold sh_c;
+  STAMP(10);
+  BLK_STAMP(1, 0);
+  const int tid = threadIdx.x;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & (WAVE - 1);
+  const Chunk ch = chunks[blockIdx.x];
+  const int bg = bg_per_chrom ? (int)ch.chrom : 0;
+  const double2* artg = reinterpret_cast<const double2*>(dfg + 2 * LNT + 2 * RCPN);   // Fst (p, A) by (alt, ref)
+  double* LPl = ldsd;
+  double* Dt = LPl + ((P.nt + 1) & ~1);
+  uint32_t* HB = reinterpret_cast<uint32_t*>(Dt + LDT);
+  const int h2w = wl_h2w(P.nb2);
+  const int h1w = R1L * (P.n1p + 1);
+  const int per = wl_per(P.nb2, P.n1p, P.n2p);
+  uint32_t* W = HB + wv * per;
+  uint32_t* H1a = W + h2w;
+  uint32_t* H1b = H1a + h1w;
+  const uint32_t rep = lane & (R1L - 1);
+
+  // ---- schedule: static first window, then the pool; two pool atomics in flight from the start
+  const uint32_t npool = ch.pool & 0xffffu, pool = ch.pool >> 16;
+  const bool dyn = ch.slot_lo + ch.nstatic < ch.slot_hi;
+  const uint32_t dbase = ch.slot_lo + ch.nstatic + pool;
+  uint32_t* myctr = ctr + (((size_t)cpar * P.nchrom + ch.chrom) * CTR_POOLS + pool) * CTR_STRIDE;
+  uint32_t s = ch.slot_lo + ch.first + wv;
+  const bool active = s < ch.slot_hi;
+  uint32_t gq1 = 0, gq2 = 0;
+  if (active && dyn && lane == 0) {
+    gq1 = atomicAdd(myctr, 1u);
+    gq2 = atomicAdd(myctr, 1u);
+  }
+  const uint2 sr0 = (active && mode_bp) ? slots[s] : make_uint2(0, 0);   // in flight during the table work
+  if (blockIdx.x == 0)   // the other parity's counters, for the next run
+    for (int k = tid; k < P.nchrom * CTR_POOLS; k += SBLOCK) ctr[((size_t)(1 - cpar) * P.nchrom * CTR_POOLS + k) * CTR_STRIDE] = 0u;
+
+  // ---- prologue: the chromosome's table in LDS (k_scan_w's three sources), D(r)
+  const double dv = tid < LDT ? dfg[tid] : 0.0;
+  BgHead hb;
+  const size_t rs = (size_t)P.nchrom * P.nh;
+  const uint32_t* Rc = repl + (size_t)par * REPL * rs + (size_t)ch.chrom * P.nh;
+  if (!FUSED) {
+    double lsv = 0.0;
+    int4 my_node = make_int4(0, 0, -1, 0);
+    uint32_t bc = 0u;
+    Bg1D o{};
+    if (sliced) {
+      if (tid < nleaves) lsv = leafsum[(size_t)bg * nleaves + tid];
+      if (tid < nnodes) my_node = nodes[tid];
+      if (tid == 0) { bc = bcount[(size_t)par * P.nchrom + bg]; o = bg1d[bg]; }
+    }
+    lds_copy_d(LPl, LPg + (size_t)bg * P.nt, P.nt);
+    if (tid < LDT) Dt[tid] = dv;
+    if (sliced) {
+      const bool writer = ch.first == 0 && (int)ch.chrom == write_chrom;
+      double* lsum = reinterpret_cast<double*>(HB);
+      if (tid < nleaves) lsum[tid] = lsv;
+      __syncthreads();
+      for (int l = 0; l < nlevels; ++l) {
+        if (my_node.z == l) lsum[nleaves + tid] = lsum[my_node.x] + lsum[my_node.y];
+        __syncthreads();
+      }
+      if (tid == 0) {
+        const double B2 = (double)bc;
+        uint32_t flags = o.flags;
+        if (B2 == 0.0) flags |= BGF_B2_ZERO;
+        const int M2 = P.nb2 - 2;
+        if (M2 >= 1 && B2 != 0.0) {
+          const double S = (nleaves + nnodes) ? lsum[nleaves + nnodes - 1] : 0.0;
+          const double padj = 1.0 - S;
+          if (padj < -1e-15) {
+            flags |= BGF_NAN2;
+          } else if (fabs(padj) > 1e-15) {
+            const double l2 = log(padj);
+            LPl[M2] = l2;
+            if (writer) { tab[(size_t)bg * P.nt + M2].lp = l2; LPg[(size_t)bg * P.nt + M2] = l2; }
+          }
+        }
+        BgHead h;
+        h.B2 = B2; h.B1a = o.B1a; h.B1b = o.B1b; h.flags = flags; h.pad = 0;
+        sh_hb = h;
+        if (writer) head[bg] = h;
+      }
+      if (blockIdx.x == 0)
+        for (int c = tid; c < P.nchrom; c += SBLOCK) bcount[(size_t)(1 - par) * P.nchrom + c] = 0u;
+      __syncthreads();
+      hb = sh_hb;
+    } else {
+      hb = head[bg];
+    }
+  } else {
+    if (tid < LDT) Dt[tid] = dv;
+    fused_table(P.nb2, P.nh, P.nt, P.n1p, P.n2p, P.n1, P.n2, P.t1a, P.t1b, P.nchrom, ch.chrom,
+                ch.first == 0 && (int)ch.chrom == write_chrom, bg,
+                Rc, rs, repl, bcount, par, tab, LPg, head, LPl, HB, leaves, nleaves, nodes, nnodes, nlevels, lnx,
+                &sh_hb, reinterpret_cast<double*>(HB) + wl_lsum_off(nleaves), HB + wl_vcnt_off(nleaves, nnodes));
+    hb = sh_hb;
+  }
+  for (int k = lane; k < per / 4; k += WAVE) reinterpret_cast<uint4*>(W)[k] = make_uint4(0, 0, 0, 0);
+  if (tid == 0) {
+    LPl[0] = 0.0;   // bin 0 ((0,0), never counted): SNPs outside the 2D SFS read it and add 0
+    WlCold c;
+    c.P = P; c.out = out; c.fst_out = fst_out; c.err_word = err_word; c.gscr = gscr; c.tab = tab + (size_t)bg * P.nt;
+    c.Rc = Rc; c.rs = rs; c.hb = hb; c.chrom = ch.chrom; c.wid_lo = ch.wid_lo; c.slot_lo = ch.slot_lo;
+    c.nscr = (uint32_t)nscr; c.zflags = bg_zero_flags(hb); c.nanf = hb.flags;
+    sh_c = c;
+  }
+  __syncthreads();
+  if (FUSED) {   // the other parity's replicas and inner sums, zeroed for the next run (a slice per workgroup)
+    uint32_t* Ro = repl + (size_t)(1 - par) * REPL * rs;
+    const size_t tot = (size_t)REPL * rs, share = (tot + gridDim.x - 1) / gridDim.x;
+    const size_t lo = (size_t)blockIdx.x * share, hi = lo + share < tot ? lo + share : tot;
+    for (size_t k = lo + tid; k < hi; k += SBLOCK) Ro[k] = 0u;
+    if (blockIdx.x == 0)
+      for (int c = tid; c < P.nchrom; c += SBLOCK) bcount[(size_t)(1 - par) * P.nchrom + c] = 0u;
+  }
+  if (!active) return;
+  const bool half1d = P.n1p <= 31 && P.n2p <= 31;
+  typedef __attribute__((address_space(3))) uint32_t lds_u32;
+  typedef __attribute__((address_space(3))) double lds_f64;
+  uint32_t a1b = (uint32_t)(uintptr_t)((lds_u32*)(H1a + rep)), a2b = (uint32_t)(uintptr_t)((lds_u32*)(H1b + rep));
+  asm volatile("" : "+v"(a1b), "+v"(a2b));
+  uint32_t awb = (uint32_t)(uintptr_t)((lds_u32*)W);
+  asm volatile("" : "+s"(awb));
+  const uint32_t dtb = (uint32_t)(uintptr_t)((lds_f64*)Dt), lpb = (uint32_t)(uintptr_t)((lds_f64*)LPl);
+
+  // ---- batched finish (k_scan_w's flush, with the window's end stored and an explicit exact flag)
+  uint32_t jb = 0;
+  auto flush = [&]() {
+    MARK(44);
+    asm volatile("" ::: "memory");   // (sh_c read back from LDS, not kept in registers across the loop)
+    const WlCold& C = sh_c;
+    uint32_t ln = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    asm volatile("" : "+v"(ln));
+    const bool mine = ln < jb;
+    const int jl = ln & (SB - 1);
+    const double B2 = sh_bd[wv][0][jl], Ba = sh_bd[wv][1][jl], Bb = sh_bd[wv][2][jl];
+    const uint32_t Bs = sh_bu[wv][0][jl], Bsb = sh_bu[wv][1][jl], Bse = sh_bu[wv][2][jl], Bn2 = sh_bu[wv][3][jl],
+                   Bn1 = sh_bu[wv][4][jl], Bnv = sh_bu[wv][5][jl];
+    const bool empty = Bse == Bsb;
+    const uint32_t wid = C.wid_lo + (Bs - C.slot_lo);
+    WinOut w;
+    w.snp_count = Bnv & 0x7fffffffu; w.n2 = Bn2 & 0xffffu; w.n2_all = Bn2 >> 16; w.n1a = Bn1 & 0xffffu; w.n1b = Bn1 >> 16;
+    w.t2d = 2.0 * (B2 - (double)w.n2 * lnx[w.n2]);
+    w.t1a = 2.0 * (Ba - (double)w.n1a * lnx[w.n1a]);
+    w.t1b = 2.0 * (Bb - (double)w.n1b * lnx[w.n1b]);
+    const bool exact = mine && !empty &&
+                       ((Bnv >> 31) != 0u || suspect_zero(w.t2d, w.n2) || suspect_zero(w.t1a, w.n1a) ||
+                        suspect_zero(w.t1b, w.n1b));
+    const uint32_t nanf = C.nanf, zflags = C.zflags;
+    if (nanf & BGF_NAN2) w.t2d = __builtin_nan("");
+    if (nanf & BGF_NAN1A) w.t1a = __builtin_nan("");
+    if (nanf & BGF_NAN1B) w.t1b = __builtin_nan("");
+    if (empty) { w.t2d = 0.0; w.t1a = 0.0; w.t1b = 0.0; }
+    if (mine && !exact)
+      write_rec(C.out + Bs, C.chrom, wid, empty ? 0u : Bsb, empty ? 0u : Bse, w, empty ? SFS2D_W_EMPTY : zflags);
+    if (mine) {
+      if (FSTIN) {
+        const double fx = sh_bf[wv][0][jl], fy = sh_bf[wv][FSTIN ? 1 : 0][jl];
+        C.fst_out[Bs] = fy != 0.0 ? fx / fy : __builtin_nan("");
+      }
+      if (mode_bp) {
+        uint32_t z = 0u;
+        asm volatile("" : "+v"(z));
+        slots[Bs] = make_uint2(z, z);
+      }
+    }
+    MARK(45);
+    // rare: exact re-evaluation on a u32 histogram in global memory (a scratch slot taken by CAS)
+    for (unsigned long long m = __ballot(exact); m; m &= m - 1) {
+      const int l = __builtin_ctzll(m);
+      const uint32_t xs = __builtin_amdgcn_readlane(Bs, l), xb = __builtin_amdgcn_readlane(Bsb, l),
+                     xe = __builtin_amdgcn_readlane(Bse, l);
+      wl_exact<FUSED>(&sh_c, LPl, bins, H1a, H1b, lnx, xs, xb, xe, blockIdx.x * NWV + wv);
+      group_sync<WAVE>();
+    }
+    jb = 0;
+  };
+  constexpr unsigned long long OWN5 = 1ull | (1ull << 33) | (1ull << 48) | (FSTIN ? (1ull << 16) | (1ull << 32) : 0ull);
+  uint32_t sdst;
+  {
+    double* d = lane == 0 ? &sh_bd[wv][0][0] : lane == 33 ? &sh_bd[wv][1][0] : lane == 48 ? &sh_bd[wv][2][0]
+              : lane == 16 ? &sh_bf[wv][0][0] : &sh_bf[wv][FSTIN ? 1 : 0][0];
+    sdst = (uint32_t)(uintptr_t)((lds_f64*)d);
+  }
+  asm volatile("" : "+v"(sdst));
+
+  // ---- the window loop.  Every VMEM load is waited for in issue order (vmcnt), and the Fst gathers of
+  // a window's rows are waited for inside its row loop: so the next window's rows, its slot record and the
+  // pool atomic are issued right after the row loop (the rest of the window -- 1D pass, sums, batch --
+  // is their cover, with the other five waves of the SIMD), never before a gather they would hold back.
+  auto window_of = [&](uint32_t sl, uint2 sr, uint32_t& b, uint32_t& e) {
+    if (mode_bp) {   // slot record: first + 1, last + 1 (0: no SNP in the slot -> b == e)
+      b = sr.x ? sr.x - 1u : 0u;
+      e = sr.x ? sr.y : 0u;
+    } else {
+      b = ch.cb + (ch.wid_lo + (sl - ch.slot_lo)) * P.ws;
+      e = b + P.ws;
+    }
+  };
+  uint32_t u[8];
+  auto issue_rows = [&](uint32_t b, uint32_t e) {
+    const __amdgpu_buffer_rsrc_t rr = window_rows(bins, b, e, P.nm1);
+    // (the lane's byte offset made opaque here: hoisted out of the loop, the eight row offsets were kept
+    // as eight VGPRs -- spilled -- instead of one base + the loads' immediate offsets)
+    uint32_t lo = (uint32_t)lane * 4u;
+    asm volatile("" : "+v"(lo));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) u[j] = __builtin_amdgcn_raw_buffer_load_b32(rr, (int)lo + 256 * j, 0, 0);
+  };
+  auto pool_slot = [&](uint32_t g) -> uint32_t {
+    const uint32_t j = __builtin_amdgcn_readfirstlane(g);
+    return dyn && dbase + npool * j < ch.slot_hi ? dbase + npool * j : ch.slot_hi;
+  };
+  uint32_t b = 0, e = 0;
+  window_of(s, make_uint2(__builtin_amdgcn_readfirstlane(sr0.x), __builtin_amdgcn_readfirstlane(sr0.y)), b, e);
+  issue_rows(b, e);
+  uint32_t s1 = pool_slot(gq1);
+  uint2 sr1 = (mode_bp && s1 < ch.slot_hi) ? slots[s1] : make_uint2(0, 0);
+  STAMP(11);
+  int it = 0;
+  while (true) {
+    MARK(40);
+    const uint32_t nsnp = e - b;
+    double acc2 = 0.0, fA = 0.0, fP = 0.0, fM = 0.0;
+    uint32_t n2 = 0;
+    bool wrap = false;
+    // one row of 64 SNPs: per SNP the 2D atomic (u8 bins) returns the SNP's rank r in its bin and the SNP
+    // adds D(r) - lp_k; both folded 1D bins counted (lane & 1 replicas; bins 0 and n_p dropped at the end);
+    // Fst's (p, A) of both populations gathered from the (alt, ref) table (gather(), issued first, so that
+    // a streamed row's load can follow it and stay in flight).  Rows past e load as 0.
+    auto gather = [&](uint32_t w, double2& fa, double2& fb) {
+      if (FSTIN) {
+        fa = artg[w & 0xffffu];
+        fb = artg[w >> 16];
+      }
+    };
+    auto row = [&](uint32_t w, const double2& fa, const double2& fb) {
+      uint32_t k2, gp;
+      cls_k2g<4 * R1L>(P, w, k2, gp);
+      const bool in2 = k2 != 0u;
+      n2 += __popcll(__ballot(in2));
+      const uint32_t x = k2 << 3;   // the byte's shift: the hardware reads the low five bits
+      uint32_t one2;
+      asm("v_lshlrev_b32 %0, %1, 1" : "=v"(one2) : "v"(x));
+      const uint32_t wa = awb + (k2 & ~3u);
+      uint32_t o = one2;
+      if (in2)
+        o = __hip_atomic_fetch_add((lds_u32*)(uintptr_t)wa, one2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_add((lds_u32*)(uintptr_t)(a1b + (gp & 0xffffu)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_add((lds_u32*)(uintptr_t)(a2b + (gp >> 16)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (FSTIN) {
+        fA += fa.y + fb.y;
+        fP += fa.x + fb.x;
+        fM = fma(fa.x, fb.x, fM);
+      }
+      const uint32_t r = in2 ? __builtin_amdgcn_ubfe(o, x, 8) : 0u;
+      wrap |= r == 255u;
+      const double d = ((lds_f64*)(uintptr_t)(dtb + 8u * r))[0];
+      const double lp = ((lds_f64*)(uintptr_t)(lpb + 8u * k2))[0];
+      acc2 += d - lp;
+    };
+    if (nsnp) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (64 * j < (int)nsnp) {
+          double2 fa, fb;
+          gather(u[j], fa, fb);
+          row(u[j], fa, fb);
+        }
+      if (nsnp > 8 * WAVE) {   // rows 8 on, streamed one row ahead (buffer loads: 0 past the window's end)
+        const __amdgpu_buffer_rsrc_t rr = window_rows(bins, b, e, P.nm1);
+        uint32_t ln = (uint32_t)lane * 4u;
+        asm volatile("" : "+v"(ln));
+        int vo = (int)ln + 256 * 8;
+        uint32_t x0 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo, 0, 0);
+        for (int j = 8; 64 * j < (int)nsnp; ++j) {
+          const uint32_t w0 = x0;
+          double2 fa, fb;
+          gather(w0, fa, fb);
+          vo += 256;
+          x0 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo, 0, 0);
+          row(w0, fa, fb);
+        }
+      }
+    }
+    MARK(41);
+    // the pipeline: window s1's rows (its slot record arrived during this window), window s2's slot record
+    // (its pool index arrived during this window), the pool atomic for the window after it
+    // (the batch's last window issues them after the flush instead: no row registers live across it)
+    const bool more = s1 < ch.slot_hi;
+    const bool fill = jb + 1u < (uint32_t)SB;
+    uint32_t b1 = 0, e1 = 0;
+    if (more) {
+      window_of(s1, make_uint2(__builtin_amdgcn_readfirstlane(sr1.x), __builtin_amdgcn_readfirstlane(sr1.y)), b1, e1);
+      if (fill) issue_rows(b1, e1);
+    }
+    const uint32_t s2 = more ? pool_slot(gq2) : ch.slot_hi;
+    const uint2 sr2 = (mode_bp && s2 < ch.slot_hi) ? slots[s2] : make_uint2(0, 0);
+    if (s2 < ch.slot_hi && lane == 0) gq2 = atomicAdd(myctr, 1u);
+    if (nsnp == 0u) {   // an empty slot
+      if (lane == 0) {
+        sh_bu[wv][0][jb] = s; sh_bu[wv][1][jb] = 0u; sh_bu[wv][2][jb] = 0u;
+        sh_bu[wv][3][jb] = 0u; sh_bu[wv][4][jb] = 0u; sh_bu[wv][5][jb] = 0u;
+        sh_bd[wv][0][jb] = 0.0; sh_bd[wv][1][jb] = 0.0; sh_bd[wv][2][jb] = 0.0;
+        if (FSTIN) { sh_bf[wv][0][jb] = 0.0; sh_bf[wv][FSTIN ? 1 : 0][jb] = 0.0; }
+      }
+    } else {
+      uint32_t nlast = 0;
+      if (!P.fold) {   // unfolded: SNPs in the excluded last 2D bin count in n2_all
+        for (uint32_t i0 = b; i0 < e; i0 += WAVE) {
+          const uint32_t w = i0 + lane < e ? cls_word(P, bins[i0 + lane]) : 0u;
+          nlast += __popcll(__ballot((w & B_LAST) != 0u));
+        }
+      }
+      group_sync<WAVE>();
+      // 1D spectra: one lane per folded bin reads and clears its R1L replicas (lanes 0-31 population 1,
+      // 32-63 population 2 when both have <= 31 bins); every SNP slot of the rows counted in one bin of
+      // each spectrum: n1a / n1b = slots - bin 0 - bin n_p
+      double acca = 0.0;
+      uint32_t n1a, n1b;
+      const uint32_t slots128 = 64u * ((nsnp + 63u) / 64u);
+      // (the lane id made opaque: hoisted out of the window loop, the lane predicates and LDS addresses
+      // below were kept in registers across it -- and spilled)
+      uint32_t ln1 = (uint32_t)lane, z1 = 0u;   // (z1: the replicas' clearing zeros, likewise)
+      asm volatile("" : "+v"(ln1), "+v"(z1));
+      if (half1d) {
+        const bool pa = ln1 < 32u;
+        const int k = (int)(ln1 & 31u), np = pa ? P.n1p : P.n2p;
+        uint32_t x = 0;
+        if (k <= np) {
+          uint2* q = reinterpret_cast<uint2*>((pa ? H1a : H1b) + k * R1L);
+          const uint2 v = *q;
+          *q = make_uint2(z1, z1);
+          x = v.x + v.y;
+          if (k >= 1 && k < np && x) acca = (double)x * lnx[x] - (double)x * LPl[(pa ? P.t1a : P.t1b) + k];
+        }
+        n1a = slots128 - (uint32_t)__builtin_amdgcn_readlane((int)x, 0) - (uint32_t)__builtin_amdgcn_readlane((int)x, P.n1p);
+        n1b = slots128 - (uint32_t)__builtin_amdgcn_readlane((int)x, 32) - (uint32_t)__builtin_amdgcn_readlane((int)x, 32 + P.n2p);
+      } else {
+        double accb = 0.0;
+        uint32_t xa[2] = {0u, 0u}, xb[2] = {0u, 0u};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int k = (int)ln1 + WAVE * j;
+          if (k <= P.n1p) {
+            uint2* q = reinterpret_cast<uint2*>(H1a + k * R1L);
+            const uint2 v = *q;
+            *q = make_uint2(z1, z1);
+            xa[j] = v.x + v.y;
+            if (k >= 1 && k < P.n1p && xa[j]) acca += (double)xa[j] * lnx[xa[j]] - (double)xa[j] * LPl[P.t1a + k];
+          }
+          if (k <= P.n2p) {
+            uint2* q = reinterpret_cast<uint2*>(H1b + k * R1L);
+            const uint2 v = *q;
+            *q = make_uint2(z1, z1);
+            xb[j] = v.x + v.y;
+            if (k >= 1 && k < P.n2p && xb[j]) accb += (double)xb[j] * lnx[xb[j]] - (double)xb[j] * LPl[P.t1b + k];
+          }
+        }
+        const uint32_t ea = P.n1p >= WAVE ? (uint32_t)__builtin_amdgcn_readlane((int)xa[1], P.n1p - WAVE)
+                                          : (uint32_t)__builtin_amdgcn_readlane((int)xa[0], P.n1p);
+        const uint32_t eb = P.n2p >= WAVE ? (uint32_t)__builtin_amdgcn_readlane((int)xb[1], P.n2p - WAVE)
+                                          : (uint32_t)__builtin_amdgcn_readlane((int)xb[0], P.n2p);
+        n1a = slots128 - (uint32_t)__builtin_amdgcn_readlane((int)xa[0], 0) - ea;
+        n1b = slots128 - (uint32_t)__builtin_amdgcn_readlane((int)xb[0], 0) - eb;
+        // (wave_sum5 sums its h operand over each lane half: population 1's total in lane 0, 2's in 32)
+        const double sa = wave_sum_all(acca), sb = wave_sum_all(accb);
+        acca = lane == 0 ? sa : (lane == 32 ? sb : 0.0);
+      }
+      MARK(42);
+      {   // clear the 2D histogram (u8 words: three 16-B stores per lane at 51 x 51)
+        uint4* q = reinterpret_cast<uint4*>(W);
+        for (int k = lane; k < h2w / 4; k += WAVE) q[k] = make_uint4(0, 0, 0, 0);
+      }
+      const double m2 = 2.0 * fM;
+      const double v = wave_sum5(acc2, acca, FSTIN ? fA - m2 : 0.0, FSTIN ? fP - m2 : 0.0, (uint32_t)lane);
+      if ((OWN5 >> lane) & 1ull) ((lds_f64*)(uintptr_t)(sdst + 8u * jb))[0] = v;
+      const bool ex = __ballot(wrap) != 0ull || nsnp >= 65535u;
+      if (lane == 0) {
+        sh_bu[wv][0][jb] = s;
+        sh_bu[wv][1][jb] = b;
+        sh_bu[wv][2][jb] = e;
+        sh_bu[wv][3][jb] = min(n2, 0xffffu) | (min(n2 + nlast, 0xffffu) << 16);
+        sh_bu[wv][4][jb] = min(n1a, 0xffffu) | (min(n1b, 0xffffu) << 16);
+        sh_bu[wv][5][jb] = nsnp | (ex ? 0x80000000u : 0u);
+      }
+    }
+    ++jb;
+    ++it;
+    group_sync<WAVE>();
+    MARK(43);
+    if (!fill) {
+      flush();
+      if (more) issue_rows(b1, e1);
+    }
+    if (!more) break;
+    s = s1; b = b1; e = e1;   // window s1 (its rows in u) becomes the current one
+    s1 = s2; sr1 = sr2;
+  }
+  if (jb) flush();
+  STAMP(15);
+  WV_STAMP(it);
+  BLK_STAMP(1, 1);
+}
+
+template <bool FUSED, int FST>
+__global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(6))) void k_scan_wl(SCAN_W_ARGS) {
+  extern __shared__ double ldsd[];
+  scan_wl<FUSED, FST>(ldsd, SCAN_W_PASS);
 }
 
 // CNT: `bins` is the counts array (counts plans): every scan classifies the counts it streams

@@ -254,13 +254,14 @@ def test_key_error_on_counts_above_sample_size():
 
 
 def _bad_count_dict():
-    """Two chromosomes; chromosome "b" holds one SNP whose pop-1 alt count (3) exceeds 2 * pop_size (2)."""
+    """Two chromosomes (pop_size 2: 4 alleles per population); chromosome "b" holds one SNP whose pop-1
+    alt count (5) exceeds 2 * pop_size."""
     d = {}
     for c in ("a", "b"):
-        for i in range(1, 40):
-            d[f"{c}-{i * 3}"] = {"calls": {"uv": (i % 2, (i + 1) % 2), "bv": ((i // 2) % 2, 1 - (i // 2) % 2)},
-                                 "annotation": "x"}
-    d["b-50"] = {"calls": {"uv": (0, 3), "bv": (1, 1)}, "annotation": "x"}
+        for i in range(1, 60):
+            a, b = i % 5, (i // 2) % 5
+            d[f"{c}-{i * 3}"] = {"calls": {"uv": (4 - a, a), "bv": (4 - b, b)}, "annotation": "x"}
+    d["b-50"] = {"calls": {"uv": (0, 5), "bv": (1, 1)}, "annotation": "x"}
     return d
 
 
@@ -271,11 +272,11 @@ def test_key_error_with_supplied_background(driver):
     counts exceed the grid takes the bins pipeline, whose k_prep reports the SNP."""
     import twoDSFS_class as T
     d = _bad_count_dict()
-    obj = T.LikelihoodInference_jointSFS(None, None, pop1_size=1, pop2_size=1)
+    obj = T.LikelihoodInference_jointSFS(None, None, pop1_size=2, pop2_size=2)
     good = {k: v for k, v in d.items() if k.startswith("a-")}
     bg2 = obj.calculate_2d_sfs(good)
-    bg1 = obj.fold_1d_sfs(obj.calculate_1d_sfs(good, "uv", 1, None, None, None))
-    bg1b = obj.fold_1d_sfs(obj.calculate_1d_sfs(good, "bv", 1, None, None, None))
+    bg1 = obj.fold_1d_sfs(obj.calculate_1d_sfs(good, "uv", 2, None, None, None))
+    bg1b = obj.fold_1d_sfs(obj.calculate_1d_sfs(good, "bv", 2, None, None, None))
     with pytest.raises(KeyError):
         if driver == "precomputed":
             obj.scan_precomputed_BG(d, 100, bg2, bg1, bg1b)
@@ -285,9 +286,10 @@ def test_key_error_with_supplied_background(driver):
             obj.scan_chooseChr_bySNPs(d, 5, "a")
         else:
             obj.scan_perChr_bySNPs(d, 5)
-    # the same calls on the clean chromosome run (the counts plan: max called counts within the grid)
-    obj.scan_precomputed_BG(good, 100, bg2, bg1, bg1b)
-    obj.scan_chooseChr_bySNPs(good, 5, "a")
+    # the same calls on the clean chromosome run (a counts plan: its called counts are within the grid)
+    r = obj.scan_precomputed_BG(good, 100, bg2, bg1, bg1b)
+    assert len(r) > 10 and all(v["T2D"] is not None for v in r.values())
+    assert len(obj.scan_chooseChr_bySNPs(good, 5, "a")) == 11
 
 
 def test_dense_primitives_vs_oracle(golden):
@@ -583,3 +585,56 @@ def test_sparse_windows_all_present(ws, n1p, n2p):
             ii = np.nonzero(w == u)[0]
             exp[(c, int(u))] = (lo + int(ii[0]), lo + int(ii[-1]) + 1)
     assert got == exp
+
+
+def test_wrapped_u8_bins_take_the_exact_path():
+    """k_scan_wl counts the 2D SFS in u8-packed bins: a window with >= 256 SNPs in one bin wraps a byte
+    (the atomic returns rank 255), and the window is re-evaluated exactly on a u32 histogram in global
+    memory.  Windows of 1,000 identical SNPs (one bin) among ordinary ones, against the oracle."""
+    from sfs2d.engine import ScanConfig
+    from sfs2d.pack import PackedSNPs
+    from sfs2d.synth import synth_genome
+    p = synth_genome(2, [6000, 3000], 25, 25, seed=77)
+    c = p.counts.copy()
+    c[1000:2000] = c[1000]          # one bin, 1,000 SNPs (SNP-count windows of 500: two wrapped windows)
+    c[4000:4700] = c[4001]
+    q = PackedSNPs(c, p.pos, p.chrom_off, p.chrom_names, p.ann_id, p.ann_names, p.pop1, p.pop2)
+    ocfg = O.Cfg(25, 25)
+    bgs = O.chrom_backgrounds(q, ocfg)
+    from sfs2d import _lib as L
+    wins, _ = O.snp_windows(q, 500)
+    _records_vs_oracle(q, ScanConfig(n1p=25, n2p=25, window_mode=L.WINDOW_SNPS, window=500), ocfg, wins,
+                       lambda k: bgs[k])
+    _records_vs_oracle(q, ScanConfig(n1p=25, n2p=25, window=200000), ocfg, O.bp_windows(q, 200000), lambda k: bgs[k])
+
+
+@pytest.mark.parametrize("lite", ["0", "1"])
+def test_scan_kernels_agree(monkeypatch, lite):
+    """k_scan_wl (six waves per SIMD, the default for counts plans on small grids) and k_scan_w
+    (SFS2D_LITE=0): both against the oracle on fixed-bp and SNP-count windows, with Fst."""
+    monkeypatch.setenv("SFS2D_LITE", lite)
+    from sfs2d import _lib as L
+    from sfs2d.engine import Engine, ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(3, [9000, 4000, 1], 25, 25, seed=1234)
+    ocfg = O.Cfg(25, 25)
+    bgs = O.chrom_backgrounds(p, ocfg)
+    _records_vs_oracle(p, ScanConfig(n1p=25, n2p=25, window=20000, fst=True), ocfg, O.bp_windows(p, 20000),
+                       lambda c: bgs[c])
+    wins, _ = O.snp_windows(p, 700)
+    _records_vs_oracle(p, ScanConfig(n1p=25, n2p=25, window_mode=L.WINDOW_SNPS, window=700), ocfg, wins,
+                       lambda c: bgs[c])
+    eng = Engine.get(0)
+    dev = eng.upload(p)
+    pl = eng.plan(dev, ScanConfig(n1p=25, n2p=25, window=20000, fst=True))
+    pl.run()
+    pl.check()
+    recs, fst = pl.read(), pl.read_fst()
+    live = (recs["flags"] & L.W_EMPTY) == 0
+    for i in np.nonzero(live)[0][::7]:
+        b, e = int(recs["begin"][i]), int(recs["end"][i])
+        want = O.window_fst(p, np.arange(b, e), ocfg)
+        a = float(fst[i])
+        assert (np.isnan(a) if want is None else abs(a - want) <= 1e-12 + 1e-10 * abs(want)), (i, a, want)
+    pl.close()
+    dev.close()

@@ -38,13 +38,23 @@ for rep in range(2):
         pl.run()
         pl.check()
         recs = pl.read()
+        fst = pl.read_fst()
         if ref is None:
-            ref = recs
-        same = recs.tobytes() == ref.tobytes()
+            ref = (recs, fst)
+        same = recs.tobytes() == ref[0].tobytes()
+        ints = all(np.array_equal(recs[f], ref[0][f]) for f in ("chrom", "wid", "begin", "end", "snp_count", "n2", "n1a", "n1b", "flags"))
+        rel = 0.0
+        for f in ("t2d", "t1d_p1", "t1d_p2"):
+            a, b = recs[f], ref[0][f]
+            m = np.isfinite(b) & (b != 0)
+            rel = max(rel, float(np.max(np.abs(a[m] - b[m]) / np.abs(b[m]))) if m.any() else 0.0)
+        fm = np.isfinite(ref[1]) & (ref[1] != 0)
+        frel = float(np.max(np.abs(fst[fm] - ref[1][fm]) / np.abs(ref[1][fm]))) if fm.any() else 0.0
         pl.set_timing(12, every=1)
         pl.run_many(12)
         _, (k1, k2, k3) = pl.timing_read()
         pl.set_timing(0)
         print(f"{which} rep {rep} {v:40s} k_prep {k1 * 1e3:8.1f} us  k_bg_slice {k2 * 1e3:6.1f}  k_scan_w {k3 * 1e3:8.1f} us"
-              f"  grid {pl.grids()[1] // 512} WGs  same={same}", flush=True)
+              f"  grid {pl.grids()[1] // 512} WGs  bytes-same={same} ints={ints} rel={rel:.1e} fst_rel={frel:.1e}"
+              f"  exact={pl.stats()}", flush=True)
         pl.close()
