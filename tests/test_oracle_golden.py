@@ -58,8 +58,6 @@ _G = gu.Golden()
 def test_oracle_matches_reference(golden, name, i):
     call = golden.calls(name)[i]
     p = golden.packed(name)
-    if name == "chr1" and call["fn"] != "combined_scan" and call["args"] != [500000]:
-        pytest.skip("chr1 non-500kb drivers covered by the slow suite")
     ok, out, _ = gu.run_capture(oracle_call, p, golden.cfg(name), call["fn"], call["args"])
     ref = call["out"]
     if not ref["ok"]:
@@ -69,16 +67,6 @@ def test_oracle_matches_reference(golden, name, i):
         return
     assert ok, f"oracle raised {out!r}"
     errs = gu.compare_results(out, gu.decode_results(ref["results"]))
-    assert not errs, errs[:10]
-
-
-@pytest.mark.slow
-@pytest.mark.parametrize("i", range(6))
-def test_oracle_chr1_all(golden, i):
-    call = golden.calls("chr1")[i]
-    p = golden.packed("chr1")
-    out = oracle_call(p, golden.cfg("chr1"), call["fn"], call["args"])
-    errs = gu.compare_results(out, gu.decode_results(call["out"]["results"]))
     assert not errs, errs[:10]
 
 
