@@ -1067,8 +1067,10 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   {
     const int64_t n = data->n;
     // ~1000+ tiles for big inputs (several workgroups per CU), >= 4096 SNPs each (flush amortised)
-    // (with Fst, <= 32k SNPs per tile keep a tile's windows in its LDS sums down to ~128-SNP windows)
-    const int64_t Tmax = (prm->flags & SFS2D_F_FST) ? 32768 : 65536;
+    // (with k_prep's Fst sums, <= 32k SNPs per tile keep a tile's windows in its LDS sums down to
+    // ~128-SNP windows; every tile flushes its LDS histogram, so no smaller tiles than that otherwise)
+    const bool kfst_t = (prm->flags & SFS2D_F_FST) && !pl->fst_win && !pl->fst_scan;
+    const int64_t Tmax = kfst_t ? 32768 : 65536;
     int64_t T = std::max<int64_t>(4096, std::min<int64_t>(Tmax, (n / 768 + 4095) / 4096 * 4096));
     if (const char* ev = std::getenv("SFS2D_TILE")) T = std::max<int64_t>(2048, std::atoll(ev) & ~int64_t(3));   // tuning
     // tile edges on absolute multiples of 4 SNPs (T is): only a chromosome's first and last step

@@ -15,8 +15,10 @@
 //   4. merge with dict semantics in file order: a key keeps its first slot, later records
 //      overwrite its values.
 // Errors stop at the first offending line in file order, as the reference's exception would.
+#include <sched.h>
 #include <zlib.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <climits>
@@ -24,6 +26,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <string_view>
 #include <thread>
@@ -189,6 +192,29 @@ inline uint64_t fnv(const char* s, size_t n) {
   return h;
 }
 
+// the threads this process may run at once: the CPUs of its affinity mask, capped by the cgroup's
+// CPU quota (cpu.max) and by OMP_NUM_THREADS when set -- a container's share of a large host, not
+// hardware_concurrency(), which counts every CPU of the machine
+int host_threads() {
+  int n = (int)std::thread::hardware_concurrency();
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) n = std::max(1, (int)CPU_COUNT(&set));
+  if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    long long period = 0;
+    if (std::fscanf(f, "%31s %lld", q, &period) == 2 && std::strcmp(q, "max") != 0 && period > 0) {
+      const long long quota = std::atoll(q);
+      if (quota > 0) n = std::min<int>(n, (int)std::max<long long>(1, (quota + period - 1) / period));
+    }
+    std::fclose(f);
+  }
+  if (const char* ev = std::getenv("OMP_NUM_THREADS")) {
+    const int k = std::atoi(ev);
+    if (k > 0) n = std::min(n, k);
+  }
+  return std::max(1, n);
+}
+
 struct Ctx {
   const char* t;
   size_t n;
@@ -199,11 +225,19 @@ struct Ctx {
 // The reference's loop body for one data line (twoDSFS_class.py:87-134).  Returns false on an
 // exception (p.fail set).
 bool parse_record(const Ctx& C, const Line& L, Part& p, std::string& tmp, std::vector<int32_t>& cnt) {
-  // the line as Python sees it: content + "\n" when it had a terminator
-  tmp.assign(C.t + L.b, L.e - L.b);
-  if (L.nl) tmp.push_back('\n');
-  const char* s = tmp.data();
-  const size_t n = tmp.size();
+  // the line as Python sees it: content + "\n" when it had a terminator (read in place when that
+  // terminator is a "\n" already; "\r" / "\r\n" lines are copied with it translated)
+  const char* s;
+  size_t n;
+  if (L.nl && C.t[L.e] == '\n') {
+    s = C.t + L.b;
+    n = L.e - L.b + 1;
+  } else {
+    tmp.assign(C.t + L.b, L.e - L.b);
+    if (L.nl) tmp.push_back('\n');
+    s = tmp.data();
+    n = tmp.size();
+  }
   // cols = line.split("\t"): field boundaries
   size_t fb[10], fe[10];
   int nf = 0;
@@ -304,15 +338,21 @@ bool parse_record(const Ctx& C, const Line& L, Part& p, std::string& tmp, std::v
   p.key_off.push_back((int64_t)p.keys.size());
   p.hash.push_back(fnv(p.keys.data() + k0, p.keys.size() - k0));
   p.chrom_len.push_back(ncols >= 2 ? (uint32_t)(fe[0] - fb[0]) : UINT32_MAX);
-  std::string an(annotation);
-  auto it = p.ann_ix.find(an);
-  int32_t aid;
-  if (it == p.ann_ix.end()) {
-    aid = (int32_t)p.ann_names.size();
-    p.ann_ix.emplace(an, aid);
-    p.ann_names.push_back(std::move(an));
+  // local annotation id: the previous record's, a linear search over a few names, else the map
+  int32_t aid = -1;
+  if (!p.ann.empty() && p.ann_names[p.ann.back()] == annotation) {
+    aid = p.ann.back();
+  } else if (p.ann_names.size() <= 16) {
+    for (size_t i = 0; i < p.ann_names.size(); ++i)
+      if (p.ann_names[i] == annotation) { aid = (int32_t)i; break; }
   } else {
-    aid = it->second;
+    auto it = p.ann_ix.find(std::string(annotation));
+    if (it != p.ann_ix.end()) aid = it->second;
+  }
+  if (aid < 0) {
+    aid = (int32_t)p.ann_names.size();
+    p.ann_ix.emplace(std::string(annotation), aid);
+    p.ann_names.emplace_back(annotation);
   }
   p.ann.push_back(aid);
   p.alle.push_back((uint8_t)ref);
@@ -340,6 +380,12 @@ void parse_chunk(const Ctx& C, size_t b, size_t e, Part& p) {
       p.fail_line = p.lines;
       return;
     }
+    if (p.hash.size() == 1) {   // room for the chunk's records at the first one's line length
+      const size_t est = (e - b) / std::max<size_t>(1, L.next - L.b) + 16;
+      p.hash.reserve(est); p.key_off.reserve(est + 1); p.chrom_len.reserve(est); p.ann.reserve(est);
+      p.alle.reserve(2 * est); p.calls.reserve(est * 2 * (size_t)C.P);
+      p.keys.reserve(est * (p.keys.size() + 2));
+    }
   }
 }
 
@@ -365,7 +411,7 @@ int sfs2d_vcf_read(const char* vcf_path, const char* popmap_path, int nthreads, 
   *out = nullptr;
   try {
     const auto t0 = Clock::now();
-    int T = nthreads > 0 ? nthreads : (int)std::thread::hardware_concurrency();
+    int T = nthreads > 0 ? nthreads : host_threads();
     if (T < 1) T = 1;
     // popmap (twoDSFS_class.py:57-64): line.strip().split("\t"), >= 2 columns
     std::vector<unsigned char> pmraw;
@@ -395,12 +441,16 @@ int sfs2d_vcf_read(const char* vcf_path, const char* popmap_path, int nthreads, 
     // the VCF text
     std::vector<unsigned char> raw;
     if (!read_file(vcf_path, raw)) { g_err = std::string("cannot read ") + vcf_path; return SFS2D_VCF_E_IO; }
-    std::string text;
+    std::string text;              // a plain gzip stream's text (one sequential inflate)
+    std::unique_ptr<char[]> tbuf;  // BGZF text: not zero-filled, first touched by the inflating threads
+    const char* tp = reinterpret_cast<const char*>(raw.data());   // the text (plain files: the bytes read)
+    size_t tn = raw.size();
     if (raw.size() >= 2 && raw[0] == 0x1f && raw[1] == 0x8b) {
       std::vector<Member> mem;
       if (bgzf_members(raw, mem)) {
-        size_t total = mem.empty() ? 0 : mem.back().out + mem.back().isize;
-        text.resize(total);
+        const size_t total = mem.empty() ? 0 : mem.back().out + mem.back().isize;
+        tbuf.reset(new char[total ? total : 1]);
+        char* const out = tbuf.get();
         std::atomic<size_t> next{0};
         std::atomic<bool> bad{false};
         auto work = [&]() {
@@ -408,7 +458,7 @@ int sfs2d_vcf_read(const char* vcf_path, const char* popmap_path, int nthreads, 
             const size_t i = next.fetch_add(1);
             if (i >= mem.size()) return;
             const Member& m = mem[i];
-            if (m.isize && !inflate_raw(&raw[m.cdata], m.clen, &text[m.out], m.isize)) bad = true;
+            if (m.isize && !inflate_raw(&raw[m.cdata], m.clen, out + m.out, m.isize)) bad = true;
           }
         };
         std::vector<std::thread> th;
@@ -416,19 +466,22 @@ int sfs2d_vcf_read(const char* vcf_path, const char* popmap_path, int nthreads, 
         work();
         for (auto& x : th) x.join();
         if (bad) { g_err = std::string("corrupt BGZF block in ") + vcf_path; return SFS2D_VCF_E_GZIP; }
+        tp = out;
+        tn = total;
       } else if (!inflate_seq(raw, text)) {
         g_err = std::string("corrupt gzip stream in ") + vcf_path;
         return SFS2D_VCF_E_GZIP;
+      } else {
+        tp = text.data();
+        tn = text.size();
       }
-    } else {
-      text.assign(reinterpret_cast<const char*>(raw.data()), raw.size());
+      std::vector<unsigned char>().swap(raw);
     }
-    std::vector<unsigned char>().swap(raw);
     const auto t1 = Clock::now();
 
     Ctx C;
-    C.t = text.data();
-    C.n = text.size();
+    C.t = tp;
+    C.n = tn;
     std::vector<std::string> pops;
     std::unordered_map<std::string, int32_t> pop_ix;
     auto header = [&](const Line& L) {   // header_cols = line.split(); samples [9:] found in the popmap
@@ -557,72 +610,137 @@ int sfs2d_vcf_read(const char* vcf_path, const char* popmap_path, int nthreads, 
     for (size_t pi = 0; pi < parts.size(); ++pi) base[pi + 1] = base[pi] + (int64_t)parts[pi].hash.size();
     total = base.back();
     auto rec_id = [](size_t pi, int64_t r) { return ((int64_t)pi << 40) | r; };   // (part, record)
-    std::vector<uint8_t> is_first((size_t)total, 0);
-    std::vector<int64_t> last_of((size_t)total, -1);   // first records: (part, record) of the key's last record
-    // >= 64k records per shard thread (SFS2D_VCF_MERGE_CHUNK overrides: the tests use tiny shards)
+    std::vector<int64_t> first_id, src_id;   // per slot: (part, record) of its first / last record
+    // keys unique by construction (a sorted VCF, the common case): the positions are plain decimals
+    // strictly increasing within each run of one chromosome, and no chromosome comes back after
+    // another -- then every record is its key's first and last, and the hash merge below is skipped
+    // >= 64k records per merge shard thread (SFS2D_VCF_MERGE_CHUNK overrides: the tests use tiny
+    // shards; SFS2D_VCF_HASH_MERGE=1 makes them take the hash merge on sorted files too)
     int64_t chunk = 65536;
     if (const char* ev = std::getenv("SFS2D_VCF_MERGE_CHUNK")) chunk = std::max<int64_t>(1, std::atoll(ev));
-    {
-      const int S = std::max(1, std::min<int>(T, (int)std::max<int64_t>(1, total / chunk)));
-      // SFS2D_VCF_MERGE_SKEW=1 (tests): every key in shard 0, the most uneven spread the hash can give
-      const char* skew_ev = std::getenv("SFS2D_VCF_MERGE_SKEW");
-      const bool skew = skew_ev && skew_ev[0] == '1';
-      auto shard_of = [&](uint64_t h) { return skew ? 0 : (int)((h >> 40) % (uint64_t)S); };
-      auto shard = [&](int t) {
-        // the table is sized from this shard's own record count (>= its distinct keys), so its load
-        // factor stays <= 1/2 however unevenly the hash spreads the keys over the shards
-        size_t mine = 0;
-        for (const Part& p : parts)
-          for (const uint64_t h : p.hash) mine += shard_of(h) == t;
-        size_t cap = 16;
-        while (cap < (mine + 1) * 2) cap <<= 1;
-        std::vector<int64_t> table(cap, -1);   // bucket -> (part, record) of the key's first record
-        for (size_t pi = 0; pi < parts.size(); ++pi) {
-          const Part& p = parts[pi];
-          for (size_t r = 0; r < p.hash.size(); ++r) {
-            const uint64_t h = p.hash[r];
-            if (shard_of(h) != t) continue;
-            const char* k = p.keys.data() + p.key_off[r];
-            const size_t kl = (size_t)(p.key_off[r + 1] - p.key_off[r]);
-            size_t bk = h & (cap - 1);
-            for (;;) {
-              const int64_t g = table[bk];
-              if (g < 0) {
-                const int64_t gi = base[pi] + (int64_t)r;
-                table[bk] = rec_id(pi, (int64_t)r);
-                is_first[(size_t)gi] = 1;
-                last_of[(size_t)gi] = rec_id(pi, (int64_t)r);
-                break;
-              }
-              const size_t qp = (size_t)(g >> 40);
-              const Part& q = parts[qp];
-              const int64_t fr = g & ((int64_t(1) << 40) - 1);
-              const size_t ql = (size_t)(q.key_off[fr + 1] - q.key_off[fr]);
-              if (q.hash[fr] == h && ql == kl && std::memcmp(q.keys.data() + q.key_off[fr], k, kl) == 0) {
-                last_of[(size_t)(base[qp] + fr)] = rec_id(pi, (int64_t)r);   // dict assignment: values replaced
-                break;
-              }
-              bk = (bk + 1) & (cap - 1);
-            }
+    const char* hm_ev = std::getenv("SFS2D_VCF_HASH_MERGE");
+    bool uniq = !(hm_ev && hm_ev[0] == '1');
+    if (uniq) {
+      struct Run { std::string_view chrom; int64_t lo, hi; };
+      std::vector<std::vector<Run>> runs(parts.size());
+      std::vector<uint8_t> ok(parts.size(), 1);
+      auto scan = [&](size_t pi) {
+        const Part& p = parts[pi];
+        std::vector<Run>& R = runs[pi];
+        for (size_t r = 0; r < p.hash.size(); ++r) {
+          const char* k = p.keys.data() + p.key_off[r];
+          const size_t kl = (size_t)(p.key_off[r + 1] - p.key_off[r]);
+          const uint32_t cl = p.chrom_len[r];
+          if (cl == UINT32_MAX || kl - cl - 1 == 0 || kl - cl - 1 > 18) { ok[pi] = 0; return; }
+          int64_t x = 0;
+          for (size_t i = cl + 1; i < kl; ++i) {
+            if (k[i] < '0' || k[i] > '9') { ok[pi] = 0; return; }
+            x = x * 10 + (k[i] - '0');
           }
+          const std::string_view ch(k, cl);
+          if (R.empty() || R.back().chrom != ch) R.push_back({ch, x, x});
+          else if (x <= R.back().hi) { ok[pi] = 0; return; }
+          else R.back().hi = x;
         }
       };
-      std::vector<std::thread> th;
-      for (int t = 1; t < S; ++t) th.emplace_back(shard, t);
-      shard(0);
-      for (auto& x : th) x.join();
-    }
-    std::vector<int64_t> first_id, src_id;   // per slot: (part, record) of its first / last record
-    first_id.reserve((size_t)total);
-    src_id.reserve((size_t)total);
-    for (size_t pi = 0; pi < parts.size(); ++pi)
-      for (int64_t r = 0; r < (int64_t)parts[pi].hash.size(); ++r)
-        if (is_first[(size_t)(base[pi] + r)]) {
-          first_id.push_back(rec_id(pi, r));
-          src_id.push_back(last_of[(size_t)(base[pi] + r)]);
+      {
+        std::atomic<size_t> next{0};
+        auto work = [&]() {
+          for (size_t i; (i = next.fetch_add(1)) < parts.size();) scan(i);
+        };
+        std::vector<std::thread> th;
+        for (int i = 1; i < T && i < (int)parts.size(); ++i) th.emplace_back(work);
+        work();
+        for (auto& x : th) x.join();
+      }
+      std::unordered_map<std::string_view, int> seen;
+      std::string_view cur;
+      int64_t hi = 0;
+      bool have = false;
+      for (size_t pi = 0; pi < parts.size() && uniq; ++pi) {
+        uniq = ok[pi] != 0;
+        for (size_t j = 0; j < runs[pi].size() && uniq; ++j) {
+          const Run& q = runs[pi][j];
+          if (have && q.chrom == cur) {
+            uniq = q.lo > hi;
+          } else {
+            uniq = seen.emplace(q.chrom, 1).second;
+            cur = q.chrom;
+            have = true;
+          }
+          hi = q.hi;
         }
-    std::vector<uint8_t>().swap(is_first);
-    std::vector<int64_t>().swap(last_of);
+      }
+    }
+    if (uniq) {
+      first_id.reserve((size_t)total);
+      for (size_t pi = 0; pi < parts.size(); ++pi)
+        for (int64_t r = 0; r < (int64_t)parts[pi].hash.size(); ++r) first_id.push_back(rec_id(pi, r));
+      src_id = first_id;
+    } else {
+      std::vector<uint8_t> is_first((size_t)total, 0);
+      std::vector<int64_t> last_of((size_t)total, -1);   // first records: (part, record) of the key's last record
+      {
+        const int S = std::max(1, std::min<int>(T, (int)std::max<int64_t>(1, total / chunk)));
+        // SFS2D_VCF_MERGE_SKEW=1 (tests): every key in shard 0, the most uneven spread the hash can give
+        const char* skew_ev = std::getenv("SFS2D_VCF_MERGE_SKEW");
+        const bool skew = skew_ev && skew_ev[0] == '1';
+        auto shard_of = [&](uint64_t h) { return skew ? 0 : (int)((h >> 40) % (uint64_t)S); };
+        auto shard = [&](int t) {
+          // the table is sized from this shard's own record count (>= its distinct keys), so its load
+          // factor stays <= 1/2 however unevenly the hash spreads the keys over the shards
+          size_t mine = 0;
+          for (const Part& p : parts)
+            for (const uint64_t h : p.hash) mine += shard_of(h) == t;
+          size_t cap = 16;
+          while (cap < (mine + 1) * 2) cap <<= 1;
+          std::vector<int64_t> table(cap, -1);   // bucket -> (part, record) of the key's first record
+          for (size_t pi = 0; pi < parts.size(); ++pi) {
+            const Part& p = parts[pi];
+            for (size_t r = 0; r < p.hash.size(); ++r) {
+              const uint64_t h = p.hash[r];
+              if (shard_of(h) != t) continue;
+              const char* k = p.keys.data() + p.key_off[r];
+              const size_t kl = (size_t)(p.key_off[r + 1] - p.key_off[r]);
+              size_t bk = h & (cap - 1);
+              for (;;) {
+                const int64_t g = table[bk];
+                if (g < 0) {
+                  const int64_t gi = base[pi] + (int64_t)r;
+                  table[bk] = rec_id(pi, (int64_t)r);
+                  is_first[(size_t)gi] = 1;
+                  last_of[(size_t)gi] = rec_id(pi, (int64_t)r);
+                  break;
+                }
+                const size_t qp = (size_t)(g >> 40);
+                const Part& q = parts[qp];
+                const int64_t fr = g & ((int64_t(1) << 40) - 1);
+                const size_t ql = (size_t)(q.key_off[fr + 1] - q.key_off[fr]);
+                if (q.hash[fr] == h && ql == kl && std::memcmp(q.keys.data() + q.key_off[fr], k, kl) == 0) {
+                  last_of[(size_t)(base[qp] + fr)] = rec_id(pi, (int64_t)r);   // dict assignment: values replaced
+                  break;
+                }
+                bk = (bk + 1) & (cap - 1);
+              }
+            }
+          }
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < S; ++t) th.emplace_back(shard, t);
+        shard(0);
+        for (auto& x : th) x.join();
+      }
+      first_id.reserve((size_t)total);
+      src_id.reserve((size_t)total);
+      for (size_t pi = 0; pi < parts.size(); ++pi)
+        for (int64_t r = 0; r < (int64_t)parts[pi].hash.size(); ++r)
+          if (is_first[(size_t)(base[pi] + r)]) {
+            first_id.push_back(rec_id(pi, r));
+            src_id.push_back(last_of[(size_t)(base[pi] + r)]);
+          }
+      std::vector<uint8_t>().swap(is_first);
+      std::vector<int64_t>().swap(last_of);
+    }
     auto part_of = [](int64_t id) { return (size_t)(id >> 40); };
     auto rec_of = [](int64_t id) { return id & ((int64_t(1) << 40) - 1); };
     auto* v = new sfs2d_vcf();

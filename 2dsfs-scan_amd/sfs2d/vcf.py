@@ -158,22 +158,30 @@ class VcfTable:
         order_names = sorted(range(len(self.chrom_names)), key=lambda c: self.chrom_names[c])
         rank[order_names] = np.arange(len(order_names))
         crank = rank[self.chrom] if self.n else np.zeros(0, np.int64)
-        order = np.lexsort((pos, crank))          # stable: dict order among equal (chrom, pos)
+        # a file already in (chromosome name, position) order (the common case) keeps its order:
+        # the stable sort would return the identity
+        dc = np.diff(crank)
+        if self.n and bool(np.all((dc > 0) | ((dc == 0) & (np.diff(pos) >= 0)))):
+            order = slice(None)
+        else:
+            order = np.lexsort((pos, crank))      # stable: dict order among equal (chrom, pos)
         crank_s = crank[order]
 
+        calls = self.calls if isinstance(order, slice) else self.calls[order]
+
         def pop_counts(pop):
+            """(ref, alt) of pop per record as uint32: calls.get(pop, (0, 0))"""
             if pop not in self.pops:
-                return np.zeros(self.n, np.int64), np.zeros(self.n, np.int64)
-            c = self.calls[order, self.pops.index(pop)].astype(np.int64)
-            c[c < 0] = 0                          # calls.get(pop, (0, 0))
+                z = np.zeros(self.n, np.uint32)
+                return z, z
+            c = np.maximum(calls[:, self.pops.index(pop), :], 0)
+            if c.size and int(c.max()) > MAX_COUNT:
+                raise ValueError("allele counts above 255 do not fit the packed u8x4 layout")
+            c = c.astype(np.uint32)
             return c[:, 0], c[:, 1]
         r1, a1 = pop_counts(pop1)
         r2, a2 = pop_counts(pop2)
-        for x in (r1, a1, r2, a2):
-            if x.size and x.max() > MAX_COUNT:
-                raise ValueError("allele counts above 255 do not fit the packed u8x4 layout")
-        counts = (r1.astype(np.uint32) | (a1.astype(np.uint32) << 8) | (r2.astype(np.uint32) << 16)
-                  | (a2.astype(np.uint32) << 24))
+        counts = r1 | (a1 << 8) | (r2 << 16) | (a2 << 24)
         bounds = np.nonzero(np.diff(crank_s))[0] + 1 if self.n else np.zeros(0, np.int64)
         offs = np.concatenate([[0], bounds, [self.n]]).astype(np.int64) if self.n else np.zeros(1, np.int64)
         names = [self.chrom_names[order_names[int(r)]] for r in crank_s[offs[:-1]]] if self.n else []

@@ -161,6 +161,52 @@ def test_merge_skewed_shards(tmp_path, monkeypatch):
         same_dict(V.read_vcf(path, pm, nthreads=nt).to_data_dict(), ref)
 
 
+def sorted_vcf(n, samples, seed, twist=None):
+    """A VCF in (chromosome, position) order -- the parser's no-merge fast path -- or, with twist, one
+    that breaks exactly one of that path's conditions (so the hash merge must take over)."""
+    rng = np.random.default_rng(seed)
+    head = ["##fileformat=VCFv4.2", "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t" + "\t".join(samples)]
+    gts = np.array(["0/0", "0/1", "1/1", "./.", "1/0"])
+    lines, per = [], n // 3
+    for c in range(3):
+        pos = np.cumsum(rng.integers(1, 40, per))
+        for q in pos.tolist():
+            g = gts[rng.integers(0, len(gts), len(samples))]
+            lines.append([f"chr{c + 1}", str(q), ".", "A", "G", ".", "PASS", "ANN=x|syn", "GT"] + list(g))
+    m = len(lines) // 2
+    if twist == "dup":              # a repeated key (dict semantics: first slot, last values)
+        lines[m][1] = lines[m - 1][1]
+    elif twist == "zero":           # "0<pos>": another key, the same integer position
+        lines[m][1] = "0" + lines[m - 1][1]
+    elif twist == "back":           # chr1 again after chr2
+        lines.insert(2 * per - 5, ["chr1", str(10 ** 9)] + lines[0][2:])
+    elif twist == "text":           # a position that is not a plain decimal
+        lines[m][1] = lines[m][1] + "x"
+    return ("\n".join(head + ["\t".join(x) for x in lines]) + "\n").encode()
+
+
+@pytest.mark.parametrize("twist", [None, "dup", "zero", "back", "text"])
+def test_sorted_fast_path(tmp_path, monkeypatch, twist):
+    """Sorted files skip the dict merge (no key can repeat); files breaking any of its conditions
+    take the hash merge.  Both agree with the oracle and with the forced hash merge."""
+    raw = sorted_vcf(60000, SAMPLES, seed=21, twist=twist)   # > 1 MB: several parse chunks
+    path = str(tmp_path / "o.vcf")
+    open(path, "wb").write(raw)
+    pm = str(tmp_path / "pm.txt")
+    write_popmap(pm, [(s, ["uv", "bv"][i % 2]) for i, s in enumerate(SAMPLES)])
+    ref = vcf_oracle.make_data_dict_vcf(path, pm)
+    for nt in (1, 5):
+        same_dict(V.read_vcf(path, pm, nthreads=nt).to_data_dict(), ref)
+    monkeypatch.setenv("SFS2D_VCF_HASH_MERGE", "1")
+    same_dict(V.read_vcf(path, pm, nthreads=5).to_data_dict(), ref)
+    if twist != "text":
+        a = V.read_vcf(path, pm, nthreads=3).to_packed()
+        monkeypatch.setenv("SFS2D_VCF_HASH_MERGE", "0")
+        b = V.read_vcf(path, pm, nthreads=3).to_packed()
+        assert np.array_equal(a.counts, b.counts) and np.array_equal(a.pos, b.pos)
+        assert np.array_equal(a.chrom_off, b.chrom_off) and a.chrom_names == b.chrom_names
+
+
 def test_bgzf_multi_block(tmp_path):
     sys.path.insert(0, GOLD)
     from gen_golden_vcf import bgzf_bytes   # BGZF writer (data only; no reference code)
