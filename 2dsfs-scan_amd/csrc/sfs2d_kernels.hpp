@@ -2724,16 +2724,23 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     // FSTIN: this lane's sums of A1 + A2, p1 + p2 and p1 p2 (fst_snp's num = A1 + A2 - 2 p1 p2,
     // den = p1 + p2 - 2 p1 p2, summed per part).  Every SNP takes part: those outside the 2D SFS --
     // bin (0,0) or, folded, both populations fixed for the alternative allele, and the unfolded last
-    // bin -- have num = den = 0, as have SNPs with fewer than 2 called alleles (table entries 0)
+    // bin -- have num = den = 0, as have SNPs with fewer than 2 called alleles in either population
+    // (both populations read table entry 0)
     double fA = 0.0, fP = 0.0, fM = 0.0;
     uint32_t n2 = 0, n1a = 0, n1b = 0, nlast = 0, nvar = 0;
     uint32_t kw[8];   // the 2D words of the first 8 rows, cleared after the window
     // FSTIN: the pair's (p, A) of both populations from the global (alt, ref) table, issued before the
     // next rows' loads so that waiting for them leaves those in flight (loads complete in order)
+    // (entry 0 = (0, 0): a SNP without >= 2 called alleles in BOTH populations reads it for both)
     auto fst_load = [&](uint32_t w0, uint32_t w1, double2 (&fq)[4]) {
       if (FSTIN) {
-        fq[0] = artg[w0 & 0xffffu]; fq[1] = artg[w0 >> 16];
-        fq[2] = artg[w1 & 0xffffu]; fq[3] = artg[w1 >> 16];
+        auto both2 = [](uint32_t w) {
+          return (__builtin_amdgcn_udot4(w, 0x00000101u, 0u, false) >= 2u) &
+                 (__builtin_amdgcn_udot4(w, 0x01010000u, 0u, false) >= 2u);
+        };
+        const bool ok0 = both2(w0), ok1 = both2(w1);
+        fq[0] = artg[ok0 ? w0 & 0xffffu : 0u]; fq[1] = artg[ok0 ? w0 >> 16 : 0u];
+        fq[2] = artg[ok1 ? w1 & 0xffffu : 0u]; fq[3] = artg[ok1 ? w1 >> 16 : 0u];
       }
     };
     // SNPs past the window's end: w = 0 (unconditional: a guard on the window's last rows cost more
@@ -3010,10 +3017,12 @@ __host__ __device__ inline int wl_hb_words(int nb2, int n1p, int n2p, int nt, in
   if (sliced) w = w > 2 * (nleaves + nnodes) ? w : 2 * (nleaves + nnodes);
   return w;
 }
-// LDS bytes of a k_scan_wl workgroup besides its static arrays: lp | D | histogram area
+// Fst's reciprocals (1/n, 1/(n(n-1))) in LDS for n <= 2 max(n1p, n2p) (an even count of double2)
+__host__ __device__ inline int wl_rtn(int n1p, int n2p) { return 2 * (n1p > n2p ? n1p : n2p) + 2; }
+// LDS bytes of a k_scan_wl workgroup besides its static arrays: lp | D | Fst reciprocals | histogram area
 __host__ __device__ inline size_t wl_lds_bytes(int nb2, int n1p, int n2p, int nt, int nleaves, int nnodes, int fused,
                                                int sliced) {
-  return sizeof(double) * (size_t)(((nt + 1) & ~1) + LDT) +
+  return sizeof(double) * (size_t)(((nt + 1) & ~1) + LDT + 2 * wl_rtn(n1p, n2p)) +
          4 * (size_t)wl_hb_words(nb2, n1p, n2p, nt, nleaves, nnodes, fused, sliced);
 }
 
@@ -3090,10 +3099,12 @@ __device__ __forceinline__ void scan_wl(double* ldsd, SCAN_W_ARGS) {
   const int lane = tid & (WAVE - 1);
   const Chunk ch = chunks[blockIdx.x];
   const int bg = bg_per_chrom ? (int)ch.chrom : 0;
-  const double2* artg = reinterpret_cast<const double2*>(dfg + 2 * LNT + 2 * RCPN);   // Fst (p, A) by (alt, ref)
+  const double2* rtg = reinterpret_cast<const double2*>(dfg + 2 * LNT);   // Fst (1/n, 1/(n(n-1))) by n
+  const int rtn = wl_rtn(P.n1p, P.n2p);
   double* LPl = ldsd;
   double* Dt = LPl + ((P.nt + 1) & ~1);
-  uint32_t* HB = reinterpret_cast<uint32_t*>(Dt + LDT);
+  double2* RT = reinterpret_cast<double2*>(Dt + LDT);
+  uint32_t* HB = reinterpret_cast<uint32_t*>(RT + rtn);
   const int h2w = wl_h2w(P.nb2);
   const int h1w = R1L * (P.n1p + 1);
   const int per = wl_per(P.nb2, P.n1p, P.n2p);
@@ -3120,6 +3131,7 @@ __device__ __forceinline__ void scan_wl(double* ldsd, SCAN_W_ARGS) {
 
   // ---- prologue: the chromosome's table in LDS (k_scan_w's three sources), D(r)
   const double dv = tid < LDT ? dfg[tid] : 0.0;
+  if (FSTIN && tid < rtn) RT[tid] = rtg[tid];
   BgHead hb;
   const size_t rs = (size_t)P.nchrom * P.nh;
   const uint32_t* Rc = repl + (size_t)par * REPL * rs + (size_t)ch.chrom * P.nh;
@@ -3207,6 +3219,7 @@ __device__ __forceinline__ void scan_wl(double* ldsd, SCAN_W_ARGS) {
   uint32_t awb = (uint32_t)(uintptr_t)((lds_u32*)W);
   asm volatile("" : "+s"(awb));
   const uint32_t dtb = (uint32_t)(uintptr_t)((lds_f64*)Dt), lpb = (uint32_t)(uintptr_t)((lds_f64*)LPl);
+  const uint32_t rtb = (uint32_t)(uintptr_t)((lds_f64*)RT), rtm = (uint32_t)rtn - 1u;
 
   // ---- batched finish (k_scan_w's flush, with the window's end stored and an explicit exact flag)
   uint32_t jb = 0;
@@ -3269,10 +3282,10 @@ __device__ __forceinline__ void scan_wl(double* ldsd, SCAN_W_ARGS) {
   }
   asm volatile("" : "+v"(sdst));
 
-  // ---- the window loop.  Every VMEM load is waited for in issue order (vmcnt), and the Fst gathers of
-  // a window's rows are waited for inside its row loop: so the next window's rows, its slot record and the
-  // pool atomic are issued right after the row loop (the rest of the window -- 1D pass, sums, batch --
-  // is their cover, with the other five waves of the SIMD), never before a gather they would hold back.
+  // ---- the window loop.  Every VMEM load is waited for in issue order (vmcnt): the next window's rows,
+  // its slot record and the pool atomic are issued right after the row loop (the rest of the window --
+  // 1D pass, sums, batch -- is their cover, with the other five waves of the SIMD), behind any streamed
+  // row load of this window they would otherwise hold back.
   auto window_of = [&](uint32_t sl, uint2 sr, uint32_t& b, uint32_t& e) {
     if (mode_bp) {   // slot record: first + 1, last + 1 (0: no SNP in the slot -> b == e)
       b = sr.x ? sr.x - 1u : 0u;
@@ -3306,20 +3319,14 @@ __device__ __forceinline__ void scan_wl(double* ldsd, SCAN_W_ARGS) {
   while (true) {
     MARK(40);
     const uint32_t nsnp = e - b;
-    double acc2 = 0.0, fA = 0.0, fP = 0.0, fM = 0.0;
+    double acc2 = 0.0, fN = 0.0, fD = 0.0;
     uint32_t n2 = 0;
     bool wrap = false;
     // one row of 64 SNPs: per SNP the 2D atomic (u8 bins) returns the SNP's rank r in its bin and the SNP
     // adds D(r) - lp_k; both folded 1D bins counted (lane & 1 replicas; bins 0 and n_p dropped at the end);
-    // Fst's (p, A) of both populations gathered from the (alt, ref) table (gather(), issued first, so that
-    // a streamed row's load can follow it and stay in flight).  Rows past e load as 0.
-    auto gather = [&](uint32_t w, double2& fa, double2& fb) {
-      if (FSTIN) {
-        fa = artg[w & 0xffffu];
-        fb = artg[w >> 16];
-      }
-    };
-    auto row = [&](uint32_t w, const double2& fa, const double2& fb) {
+    // FSTIN: fst_snp's (num, den) from the counts and the LDS reciprocals (0 unless both populations have
+    // >= 2 called alleles; SNPs outside the 2D SFS have num = den = 0).  Rows past e load as 0.
+    auto row = [&](uint32_t w) {
       uint32_t k2, gp;
       cls_k2g<4 * R1L>(P, w, k2, gp);
       const bool in2 = k2 != 0u;
@@ -3334,9 +3341,18 @@ __device__ __forceinline__ void scan_wl(double* ldsd, SCAN_W_ARGS) {
       __hip_atomic_fetch_add((lds_u32*)(uintptr_t)(a1b + (gp & 0xffffu)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       __hip_atomic_fetch_add((lds_u32*)(uintptr_t)(a2b + (gp >> 16)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (FSTIN) {
-        fA += fa.y + fb.y;
-        fP += fa.x + fb.x;
-        fM = fma(fa.x, fb.x, fM);
+        const uint32_t n1c = __builtin_amdgcn_udot4(w, 0x00000101u, 0u, false);
+        const uint32_t n2c = __builtin_amdgcn_udot4(w, 0x01010000u, 0u, false);
+        const bool ok = (n1c >= 2u) & (n2c >= 2u);
+        const uint32_t f1 = ok ? (w >> 8) & 0xffu : 0u, f2 = ok ? w >> 24 : 0u;
+        const uint32_t q1a = rtb + 16u * min(n1c, rtm), q2a = rtb + 16u * min(n2c, rtm);
+        const double r1x = ((lds_f64*)(uintptr_t)q1a)[0], r1y = ((lds_f64*)(uintptr_t)q1a)[1];
+        const double r2x = ((lds_f64*)(uintptr_t)q2a)[0], r2y = ((lds_f64*)(uintptr_t)q2a)[1];
+        const double p1 = (double)f1 * r1x, p2 = (double)f2 * r2x;
+        const double A1 = (double)__umul24(f1, f1 - 1u) * r1y, A2 = (double)__umul24(f2, f2 - 1u) * r2y;
+        const double m = p1 * p2;
+        fN += fma(-2.0, m, A1 + A2);
+        fD += fma(-2.0, m, p1 + p2);
       }
       const uint32_t r = in2 ? __builtin_amdgcn_ubfe(o, x, 8) : 0u;
       wrap |= r == 255u;
@@ -3347,11 +3363,7 @@ __device__ __forceinline__ void scan_wl(double* ldsd, SCAN_W_ARGS) {
     if (nsnp) {
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        if (64 * j < (int)nsnp) {
-          double2 fa, fb;
-          gather(u[j], fa, fb);
-          row(u[j], fa, fb);
-        }
+        if (64 * j < (int)nsnp) row(u[j]);
       if (nsnp > 8 * WAVE) {   // rows 8 on, streamed one row ahead (buffer loads: 0 past the window's end)
         const __amdgpu_buffer_rsrc_t rr = window_rows(bins, b, e, P.nm1);
         uint32_t ln = (uint32_t)lane * 4u;
@@ -3360,11 +3372,9 @@ __device__ __forceinline__ void scan_wl(double* ldsd, SCAN_W_ARGS) {
         uint32_t x0 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo, 0, 0);
         for (int j = 8; 64 * j < (int)nsnp; ++j) {
           const uint32_t w0 = x0;
-          double2 fa, fb;
-          gather(w0, fa, fb);
           vo += 256;
           x0 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo, 0, 0);
-          row(w0, fa, fb);
+          row(w0);
         }
       }
     }
@@ -3457,8 +3467,7 @@ __device__ __forceinline__ void scan_wl(double* ldsd, SCAN_W_ARGS) {
         uint4* q = reinterpret_cast<uint4*>(W);
         for (int k = lane; k < h2w / 4; k += WAVE) q[k] = make_uint4(0, 0, 0, 0);
       }
-      const double m2 = 2.0 * fM;
-      const double v = wave_sum5(acc2, acca, FSTIN ? fA - m2 : 0.0, FSTIN ? fP - m2 : 0.0, (uint32_t)lane);
+      const double v = wave_sum5(acc2, acca, FSTIN ? fN : 0.0, FSTIN ? fD : 0.0, (uint32_t)lane);
       if ((OWN5 >> lane) & 1ull) ((lds_f64*)(uintptr_t)(sdst + 8u * jb))[0] = v;
       const bool ex = __ballot(wrap) != 0ull || nsnp >= 65535u;
       if (lane == 0) {
@@ -3503,7 +3512,7 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) voi
 
 // K3 for large grids, one wavefront per window (LDS: the wave's histograms only)
 template <bool P16, bool FST, bool CNT>
-__global__ __launch_bounds__(WAVE) void k_scan_gw(SCAN_W_ARGS) {
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(4))) void k_scan_gw(SCAN_W_ARGS) {
   extern __shared__ double ldsd[];
   scan_w_body<P16, false, FST, true, CNT>(ldsd, SCAN_W_PASS);
 }

@@ -638,3 +638,41 @@ def test_scan_kernels_agree(monkeypatch, lite):
         assert (np.isnan(a) if want is None else abs(a - want) <= 1e-12 + 1e-10 * abs(want)), (i, a, want)
     pl.close()
     dev.close()
+
+
+@pytest.mark.parametrize("env", ["SFS2D_LITE=1", "SFS2D_LITE=0", "SFS2D_FST_SCAN=0"])
+def test_fst_low_called_counts(monkeypatch, env):
+    """SNPs with fewer than 2 called alleles in ONE population leave Hudson's Fst sums (oracle.window_fst
+    keeps SNPs with >= 2 in both): the scan kernels' per-SNP terms (k_scan_wl from the LDS reciprocals,
+    k_scan_w from the (alt, ref) table, k_prep's fixed-point sums) must drop them whatever the other
+    population holds."""
+    k, v = env.split("=")
+    monkeypatch.setenv(k, v)
+    from sfs2d import _lib as L
+    from sfs2d.engine import Engine, ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(2, [7000, 3000], 25, 25, seed=99)
+    c = p.counts.copy()
+    rng = np.random.default_rng(5)
+    low = rng.choice(len(c), size=len(c) // 6, replace=False)
+    pair = rng.integers(0, 3, size=len(low))                    # (ref, alt) = (0, 0), (1, 0), (0, 1)
+    r, a = np.array([0, 1, 0], np.uint32)[pair], np.array([0, 0, 1], np.uint32)[pair]
+    side = rng.integers(0, 2, size=len(low)).astype(bool)       # population 1 or 2
+    c[low[side]] = (c[low[side]] & 0xffff0000) | r[side] | (a[side] << 8)
+    c[low[~side]] = (c[low[~side]] & 0x0000ffff) | (r[~side] << 16) | (a[~side] << 24)
+    p.counts = c
+    ocfg = O.Cfg(25, 25)
+    eng = Engine.get(0)
+    dev = eng.upload(p)
+    pl = eng.plan(dev, ScanConfig(n1p=25, n2p=25, window=20000, fst=True))
+    pl.run()
+    pl.check()
+    recs, fst = pl.read(), pl.read_fst()
+    live = np.nonzero((recs["flags"][: len(fst)] & L.W_EMPTY) == 0)[0]
+    assert len(live) > 20
+    for i in live:
+        b, e = int(recs["begin"][i]), int(recs["end"][i])
+        want = O.window_fst(p, np.arange(b, e), ocfg)
+        assert _fst_close(float(fst[i]), want), (i, float(fst[i]), want)
+    pl.close()
+    dev.close()
