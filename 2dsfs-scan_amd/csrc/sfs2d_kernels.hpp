@@ -3340,6 +3340,17 @@ __device__ __forceinline__ void scan_wl(double* ldsd, SCAN_W_ARGS) {
         o = __hip_atomic_fetch_add((lds_u32*)(uintptr_t)wa, one2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       __hip_atomic_fetch_add((lds_u32*)(uintptr_t)(a1b + (gp & 0xffffu)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       __hip_atomic_fetch_add((lds_u32*)(uintptr_t)(a2b + (gp >> 16)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef SFS2D_WL_FSTTAB   // experiment: the (alt, ref) table in global memory, as k_scan_w
+      if (FSTIN) {
+        const bool ok = (__builtin_amdgcn_udot4(w, 0x00000101u, 0u, false) >= 2u) &
+                        (__builtin_amdgcn_udot4(w, 0x01010000u, 0u, false) >= 2u);
+        const double2* artg = reinterpret_cast<const double2*>(dfg + 2 * LNT + 2 * RCPN);
+        const double2 fa = artg[ok ? w & 0xffffu : 0u], fb = artg[ok ? w >> 16 : 0u];
+        const double m = fa.x * fb.x;
+        fN += fma(-2.0, m, fa.y + fb.y);
+        fD += fma(-2.0, m, fa.x + fb.x);
+      }
+#else
       if (FSTIN) {
         const uint32_t n1c = __builtin_amdgcn_udot4(w, 0x00000101u, 0u, false);
         const uint32_t n2c = __builtin_amdgcn_udot4(w, 0x01010000u, 0u, false);
@@ -3354,6 +3365,7 @@ __device__ __forceinline__ void scan_wl(double* ldsd, SCAN_W_ARGS) {
         fN += fma(-2.0, m, A1 + A2);
         fD += fma(-2.0, m, p1 + p2);
       }
+#endif
       const uint32_t r = in2 ? __builtin_amdgcn_ubfe(o, x, 8) : 0u;
       wrap |= r == 255u;
       const double d = ((lds_f64*)(uintptr_t)(dtb + 8u * r))[0];
