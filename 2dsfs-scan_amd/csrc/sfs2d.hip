@@ -1279,6 +1279,13 @@ int sfs2d_plan_grids(const sfs2d_plan* pl, int64_t* prep_threads, int64_t* scan_
   return 0;
 }
 
+const char* sfs2d_plan_scan_kernel(const sfs2d_plan* pl) {
+  if (!pl) return nullptr;
+  if (pl->lite) return "k_scan_wl";
+  if (pl->gw) return "k_scan_gw";
+  return pl->G == WAVE ? "k_scan_w" : "k_scan_g";
+}
+
 int sfs2d_plan_set_timing(sfs2d_plan* pl, int max_runs) { return sfs2d_plan_set_timing_sampled(pl, max_runs, 1); }
 
 int sfs2d_plan_set_timing_sampled(sfs2d_plan* pl, int max_runs, int every) {

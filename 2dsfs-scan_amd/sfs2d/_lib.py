@@ -39,7 +39,7 @@ EXPORTS = [
     "sfs2d_plan_fst_read", "sfs2d_plan_fst_buffer", "sfs2d_plan_read",
     "sfs2d_plan_bg_buffer", "sfs2d_plan_bg_words", "sfs2d_plan_bg_exchange", "sfs2d_plan_run_phase", "sfs2d_plan_check", "sfs2d_plan_time",
     "sfs2d_plan_destroy", "sfs2d_scan", "sfs2d_plan_set_timing", "sfs2d_plan_timing_read",
-    "sfs2d_plan_stats", "sfs2d_plan_grids", "sfs2d_plan_attach", "sfs2d_data_synth_sims",
+    "sfs2d_plan_stats", "sfs2d_plan_grids", "sfs2d_plan_scan_kernel", "sfs2d_plan_attach", "sfs2d_data_synth_sims",
     "sfs2d_data_read", "sfs2d_dist_unique_id", "sfs2d_dist_create", "sfs2d_dist_scan_gather",
     "sfs2d_dist_destroy", "sfs2d_dist_set_gather", "sfs2d_plan_run_streams",
     "sfs2d_dist_scan_gather_streams", "sfs2d_bg_hist_dev", "sfs2d_plan_bg_rows_dev", "sfs2d_plan_bg_rows_set_dev",
@@ -128,6 +128,8 @@ def lib():
     L.sfs2d_plan_set_timing.argtypes = [vp, C.c_int]
     L.sfs2d_plan_stats.argtypes = [vp, C.POINTER(C.c_uint32)]
     L.sfs2d_plan_grids.argtypes = [vp, C.POINTER(i64), C.POINTER(i64)]
+    L.sfs2d_plan_scan_kernel.argtypes = [vp]
+    L.sfs2d_plan_scan_kernel.restype = C.c_char_p
     L.sfs2d_plan_attach.argtypes = [vp, C.POINTER(Params), C.POINTER(vp)]
     L.sfs2d_data_synth_sims.argtypes = [vp, C.POINTER(SynthParams), vp, vp, i32, vp, i32, C.POINTER(vp)]
     L.sfs2d_data_read.argtypes = [vp, vp, vp, i64]

@@ -261,6 +261,10 @@ class Plan:
         self.eng.check(self.eng.lib.sfs2d_plan_grids(self.h, C.byref(a), C.byref(b)))
         return a.value, b.value
 
+    def scan_kernel(self) -> str:
+        """Name of the scan kernel this plan launches (the prefix of its rocprofv3 kernel name)."""
+        return self.eng.lib.sfs2d_plan_scan_kernel(self.h).decode()
+
     def stats(self) -> int:
         v = C.c_uint32()
         self.eng.check(self.eng.lib.sfs2d_plan_stats(self.h, C.byref(v)))

@@ -78,7 +78,7 @@ def pmc_traffic(kernel, grid):
     except (OSError, ValueError):
         return None, None
     for r in d.get("kernels", []):
-        if r.get("kernel", "").startswith(kernel) and int(r.get("grid", -1)) == int(grid):
+        if r.get("kernel", "").startswith(kernel + "<") and int(r.get("grid", -1)) == int(grid):
             return r["read_bytes"] + r["write_bytes"], d.get("source", path)
     return None, None
 
@@ -373,7 +373,7 @@ def config3_strong(cx, args):
                                  "note": "the same loop, T2D + T1D only (Hudson Fst not computed)"}
         for x in q:
             x.close()
-    nrec, grids = plans[0].nrec, plans[0].grids()
+    nrec, grids, kname = plans[0].nrec, plans[0].grids(), plans[0].scan_kernel()
     for x in plans:
         x.close()
     dev.close()
@@ -382,8 +382,8 @@ def config3_strong(cx, args):
            "host_enqueue_ms_per_step": r["t_enq"] / args.steps * 1e3,
            "device_ms_per_step": r["device_ms"] / args.steps, "gather_ms": r["gather_ms"],
            "windows": total_windows, "snps": p.n, "cuts": cuts,
-           "rank0": {"snps": sub.n, "windows": win_rank, "slots": nrec, "k_prep_ms": k1, "k_scan_w_ms": k3,
-                     "single_stream_pass_ms": one, "scan_grid_threads": grids[1]}}
+           "rank0": {"snps": sub.n, "windows": win_rank, "slots": nrec, "k_prep_ms": k1, "scan_ms": k3,
+                     "scan_kernel": kname, "single_stream_pass_ms": one, "scan_grid_threads": grids[1]}}
     out.update(extra)
     return out, p
 
@@ -401,7 +401,7 @@ def config2_weak(cx, args):
     r = run_loop(cx, plans, steps, max(args.warmup, 20), "config 2")
     k1, k2, k3 = kernel_times(plans[0])
     one = single_pass_ms(cx, plans[0], 40) if cx.rank == 0 else None
-    nrec, grids = plans[0].nrec, plans[0].grids()
+    nrec, grids, kname = plans[0].nrec, plans[0].grids(), plans[0].scan_kernel()
     for x in plans[::-1]:
         x.close()
     dev.close()
@@ -409,7 +409,7 @@ def config2_weak(cx, args):
     nwin = n_windows(r["mine"])
     b3 = algorithmic_bytes(p.n, nrec, nwin, "k3")
     ach = b3 / (k3 * 1e-3) / 1e9
-    traffic, tsrc = pmc_traffic("k_scan_w", grids[1])
+    traffic, tsrc = pmc_traffic(kname, grids[1])
     return {"value": total * steps / r["dt"], "unit": "windows/s", "scaling": "weak", "steps": steps,
             "ms_per_step": r["dt"] / steps * 1e3, "host_enqueue_ms_per_step": r["t_enq"] / steps * 1e3,
             "single_stream_pass_ms": one,
@@ -418,9 +418,9 @@ def config2_weak(cx, args):
             "windows_per_gpu": nwin, "windows_all_gpus": total,
             "parallelism": f"one chromosome per GPU, {ns} plans on {ns} HIP streams (passes overlap)"
                            + ("; one RCCL all-gather of the final tables" if cx.world > 1 else ""),
-            "kernels_ms": {"k_prep": k1, "k_bg_slice": k2, "k_scan_w": k3},
+            "kernels_ms": {"k_prep": k1, "k_bg_slice": k2, kname: k3},
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                         "traffic": traffic, "kernel": "k_scan_w", "ms": k3, "algorithmic_bytes": b3,
+                         "traffic": traffic, "kernel": kname, "ms": k3, "algorithmic_bytes": b3,
                          "note": "the 8 MB stream is MALL-resident: not an HBM measurement; traffic: "
                                  + (tsrc or "no PMC pass committed")}}
 
@@ -473,10 +473,10 @@ def main():
     if rank == 0:
         r0 = c3["rank0"]
         b3 = algorithmic_bytes(r0["snps"], r0["slots"], r0["windows"], "k3")
-        ach = b3 / (r0["k_scan_w_ms"] * 1e-3) / 1e9
+        ach = b3 / (r0["scan_ms"] * 1e-3) / 1e9
         bp = algorithmic_bytes(c3["snps"], 0, c3["windows"], "pipeline")
         step_s = c3["ms_per_step"] * 1e-3
-        traffic, tsrc = pmc_traffic("k_scan_w", r0["scan_grid_threads"])
+        traffic, tsrc = pmc_traffic(r0["scan_kernel"], r0["scan_grid_threads"])
         line = {
             "metric": METRIC, "value": c3["value"], "unit": "windows/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": c3["ms_per_step"], "higher_is_better": True, "scaling": "strong",
@@ -495,9 +495,9 @@ def main():
             "device_ms_per_step": c3["device_ms_per_step"], "gather_ms": c3["gather_ms"],
             "rank0": r0,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_scan_w",
-                         "ms": r0["k_scan_w_ms"], "algorithmic_bytes": b3,
-                         "note": "k_scan_w on rank 0's shard: 4 B/SNP + 96 B/slot per launch over its average duration "
+                         "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "kernel": r0["scan_kernel"],
+                         "ms": r0["scan_ms"], "algorithmic_bytes": b3,
+                         "note": r0["scan_kernel"] + " on rank 0's shard: 4 B/SNP + 96 B/slot per launch over its average duration "
                                  "(kernel start/end events in the dispatch packets, 16 runs on one stream after the "
                                  "timed loop); traffic: " + (tsrc or "no PMC pass committed")},
             "roofline_pipeline": {"bound": "hbm", "achieved": bp / step_s / 1e9, "peak": HBM_PEAK_GBS * world,

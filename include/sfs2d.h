@@ -213,6 +213,9 @@ int sfs2d_plan_attach(sfs2d_plan* base, const sfs2d_params* params, sfs2d_plan**
 /* launch geometry (threads per grid) of k_prep and of the scan kernel: matches the Grid_Size column
  * of rocprofv3 kernel traces, so profiles can be joined to a plan */
 int sfs2d_plan_grids(const sfs2d_plan* plan, int64_t* prep_threads, int64_t* scan_threads);
+/* name of the scan kernel the plan launches ("k_scan_wl", "k_scan_w", "k_scan_gw", "k_scan_g"; the
+ * prefix of its rocprofv3 kernel name), NULL for a null plan */
+const char* sfs2d_plan_scan_kernel(const sfs2d_plan* plan);
 /* cumulative number of windows re-evaluated on the exact path (|T| ~ 0: proportionality test) */
 int sfs2d_plan_stats(sfs2d_plan* plan, uint32_t* exact_windows);
 /* last run's error word (0 = ok, else SFS2D_E_KEY / SFS2D_E_GRID, or SFS2D_E_ARG for summed background
