@@ -926,13 +926,15 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
     }
   }
   // k_scan_wl (six waves per SIMD: u8 2D bins, 2 1D replicas, three workgroups per CU) for counts plans on
-  // the small-grid path whose Fst, if any, is summed in the scan, when more of its workgroups fit a CU
-  // than k_scan_w's.  SFS2D_LITE=0/1 forces the choice (where the kernel can run the plan).
+  // the small-grid path whose Fst, if any, is summed in the scan: opt-in (SFS2D_LITE=1, where it can run
+  // the plan).  Measured slower than k_scan_w on config 3 (206 vs 177 us per pass with Fst,
+  // profiles/r04b_exp_lite.log), so not the default.
   const PwTree pw = pw_plan(K.nb2 - 3);
   {
     const bool can = pl->cnt && pl->G == WAVE && !pl->gw;
-    int occ_l = 0, occ_w = 0;
-    if (can) {
+    int occ_l = 0;
+    const char* ev = std::getenv("SFS2D_LITE");
+    if (can && ev && ev[0] == '1') {
       const size_t lds_l = wl_lds_bytes(K.nb2, K.n1p, K.n2p, K.nt, (int)pw.leaves.size(), (int)pw.nodes.size(),
                                         pl->fused ? 1 : 0, pl->sliced ? 1 : 0);
       const void* fl = pl->fused ? (pl->fst ? (const void*)k_scan_wl<true, 2> : (const void*)k_scan_wl<true, 0>)
@@ -940,14 +942,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
       if (lds_l > 64 * 1024) hipFuncSetAttribute(fl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::min<size_t>(lds_l, 160 * 1024));
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_l, fl, SBLOCK, lds_l) != hipSuccess) occ_l = 0;
       (void)hipGetLastError();
-      const void* fw = pl->fst_scan ? (pl->fused ? (const void*)k_scan_w<true, true, 2, true> : (const void*)k_scan_w<true, false, 2, true>)
-                                    : (pl->fused ? (const void*)k_scan_w<true, true, false, true> : (const void*)k_scan_w<true, false, false, true>);
-      if (pl->scan_lds > 64 * 1024)
-        hipFuncSetAttribute(fw, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::min<size_t>(pl->scan_lds, 160 * 1024));
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_w, fw, SBLOCK, pl->scan_lds) != hipSuccess) occ_w = 0;
-      (void)hipGetLastError();
-      pl->lite = occ_l > occ_w;
-      if (const char* ev = std::getenv("SFS2D_LITE")) pl->lite = occ_l >= 1 && ev[0] == '1';
+      pl->lite = occ_l >= 1;
       if (pl->lite) {
         pl->scan_lds = lds_l;
         pl->fst_scan = pl->fst;   // Fst summed in the scan

@@ -287,9 +287,14 @@ def test_key_error_with_supplied_background(driver):
         else:
             obj.scan_perChr_bySNPs(d, 5)
     # the same calls on the clean chromosome run (a counts plan: its called counts are within the grid)
+    from sfs2d.pack import pack_snp_dict
+    q = pack_snp_dict(good)
+    ocfg = O.Cfg(2, 2)
     r = obj.scan_precomputed_BG(good, 100, bg2, bg1, bg1b)
-    assert len(r) > 10 and all(v["T2D"] is not None for v in r.values())
-    assert len(obj.scan_chooseChr_bySNPs(good, 5, "a")) == 11
+    assert list(r) == ["a 1-100", "a 101-200"] and all(v["T2D"] is not None for v in r.values())
+    got = obj.scan_chooseChr_bySNPs(good, 5, "a")
+    want = O.scan_chooseChr_bySNPs(q, 5, "a", ocfg)
+    assert list(got) == list(want) and len(got) > 5
 
 
 def test_dense_primitives_vs_oracle(golden):
@@ -610,7 +615,7 @@ def test_wrapped_u8_bins_take_the_exact_path():
 
 @pytest.mark.parametrize("lite", ["0", "1"])
 def test_scan_kernels_agree(monkeypatch, lite):
-    """k_scan_wl (six waves per SIMD, the default for counts plans on small grids) and k_scan_w
+    """k_scan_wl (six waves per SIMD, opt-in for counts plans on small grids: SFS2D_LITE=1) and k_scan_w
     (SFS2D_LITE=0): both against the oracle on fixed-bp and SNP-count windows, with Fst."""
     monkeypatch.setenv("SFS2D_LITE", lite)
     from sfs2d import _lib as L

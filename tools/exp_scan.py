@@ -3,7 +3,8 @@
 creation (SFS2D_WGS: scan workgroups in the grid; SFS2D_FUSED ...) and, with SFS2D_LIB_VARIANTS, under
 other builds of the library (one subprocess each).  Prints per-variant k_prep / k_scan_w times (HIP
 events in the dispatch packets, one stream).
-usage: python tools/exp_scan.py [config2|config3] [ENV=VAL[,ENV=VAL]] ...   (each arg one variant)"""
+usage: python tools/exp_scan.py [config2|config3] [ENV=VAL[,ENV=VAL]] ...   (each arg one variant; a
+"nofst" item in a variant scans without Fst, compared with the first variant's records only)"""
 import os
 import sys
 import time
@@ -27,9 +28,10 @@ ref = None
 for rep in range(2):
     for v in variants:
         env = dict(kv.split("=", 1) for kv in v.split(",") if "=" in kv)
+        fst_on = "nofst" not in v.split(",")
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
-        pl = eng.plan(dev, ScanConfig(n1p=25, n2p=25, window=20000, fst=True))
+        pl = eng.plan(dev, ScanConfig(n1p=25, n2p=25, window=20000, fst=fst_on))
         for k, o in old.items():
             if o is None:
                 os.environ.pop(k)
@@ -38,7 +40,7 @@ for rep in range(2):
         pl.run()
         pl.check()
         recs = pl.read()
-        fst = pl.read_fst()
+        fst = pl.read_fst() if fst_on else ref[1] if ref else None
         if ref is None:
             ref = (recs, fst)
         same = recs.tobytes() == ref[0].tobytes()
@@ -54,7 +56,7 @@ for rep in range(2):
         pl.run_many(12)
         _, (k1, k2, k3) = pl.timing_read()
         pl.set_timing(0)
-        print(f"{which} rep {rep} {v:40s} k_prep {k1 * 1e3:8.1f} us  k_bg_slice {k2 * 1e3:6.1f}  k_scan_w {k3 * 1e3:8.1f} us"
+        print(f"{which} rep {rep} {v:40s} [{pl.scan_kernel()}] k_prep {k1 * 1e3:8.1f} us  k_bg_slice {k2 * 1e3:6.1f}  k_scan_w {k3 * 1e3:8.1f} us"
               f"  grid {pl.grids()[1] // 512} WGs  bytes-same={same} ints={ints} rel={rel:.1e} fst_rel={frel:.1e}"
               f"  exact={pl.stats()}", flush=True)
         pl.close()
