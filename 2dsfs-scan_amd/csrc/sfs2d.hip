@@ -124,6 +124,9 @@ struct sfs2d_data {
   // max_nc1 <= n1 and max_nc2 <= n2 -- then no SNP can raise KeyError (a > 2 pop_size) or leave the
   // grid after the fold; otherwise the plan takes the bins pipeline, whose k_prep raises the error
   uint32_t max_nc1 = 0xffffffffu, max_nc2 = 0xffffffffu;
+  // some SNP has fewer than 2 called alleles in a population (unknown: true): Fst summed in the scan
+  // must then drop such SNPs explicitly (k_scan_w<..., 3, ...>); without any, the unmasked terms are exact
+  bool low_nc = true;
 };
 
 struct sfs2d_plan {
@@ -197,6 +200,7 @@ struct sfs2d_plan {
   bool fst_win = false;           // Fst by window kernels (fst_windows) instead of k_prep's sums
   bool fst_scan = false;          // Fst summed by k_scan_w itself (counts plans, small grids): k_prep has no Fst work
   bool lite = false;              // k_scan_wl instead of k_scan_w (counts plans, small grids: six waves per SIMD)
+  bool fst_mask = true;           // Fst in the scan: the data set has SNPs with < 2 called alleles (k_scan_w FST 3)
   int nfst = 0;                   // k_bg_slice's extra Fst workgroups
 };
 
@@ -312,8 +316,13 @@ hipError_t launch_scan_c(sfs2d_plan* pl, sfs2d_window* out) {
   } else if (pl->G == WAVE) {
     if constexpr (CNT) {
       if (pl->fst_scan) {
-        if (pl->fused) launch_scan_w<P16, true, 2, CNT>(pl, out, per_chrom, bp);
-        else launch_scan_w<P16, false, 2, CNT>(pl, out, per_chrom, bp);
+        if (pl->fst_mask) {
+          if (pl->fused) launch_scan_w<P16, true, 3, CNT>(pl, out, per_chrom, bp);
+          else launch_scan_w<P16, false, 3, CNT>(pl, out, per_chrom, bp);
+        } else {
+          if (pl->fused) launch_scan_w<P16, true, 2, CNT>(pl, out, per_chrom, bp);
+          else launch_scan_w<P16, false, 2, CNT>(pl, out, per_chrom, bp);
+        }
         return hipGetLastError();
       }
     }
@@ -561,13 +570,17 @@ int sfs2d_data_upload(sfs2d_ctx* ctx, const uint32_t* counts, const uint32_t* po
   d->host_pos.assign(pos, pos + n);
   {
     uint32_t m1 = 0, m2 = 0;
+    bool low = false;
     for (int64_t i = 0; i < n; ++i) {
       const uint32_t c = counts[i];
-      m1 = std::max(m1, (c & 0xffu) + ((c >> 8) & 0xffu));
-      m2 = std::max(m2, ((c >> 16) & 0xffu) + (c >> 24));
+      const uint32_t n1c = (c & 0xffu) + ((c >> 8) & 0xffu), n2c = ((c >> 16) & 0xffu) + (c >> 24);
+      m1 = std::max(m1, n1c);
+      m2 = std::max(m2, n2c);
+      low |= std::min(n1c, n2c) < 2u;
     }
     d->max_nc1 = m1;
     d->max_nc2 = m2;
+    d->low_nc = low;
   }
   for (int c = 0; c < nchrom; ++c) {
     int64_t s = d->chrom_off[c], t = d->chrom_off[c + 1];
@@ -610,9 +623,9 @@ int sfs2d_data_wrap_device(sfs2d_ctx* ctx, const uint32_t* d_counts, const uint3
   d->strict = true;   // contract: positions strictly increasing within each chromosome
   if (n > 0) {   // the largest called counts (see max_nc1), one pass over the caller's counts
     uint32_t* d_m = nullptr;
-    uint32_t hm[2] = {0, 0};
-    hipError_t e = hipMalloc((void**)&d_m, 2 * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMemsetAsync(d_m, 0, 2 * sizeof(uint32_t), CTX_STREAM(ctx));
+    uint32_t hm[3] = {0, 0, 0};
+    hipError_t e = hipMalloc((void**)&d_m, 3 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemsetAsync(d_m, 0, 3 * sizeof(uint32_t), CTX_STREAM(ctx));
     if (e == hipSuccess) {
       const unsigned grid = (unsigned)std::min<int64_t>(4096, (n + 1023) / 1024);
       hipLaunchKernelGGL(k_max_called, dim3(grid), dim3(256), 0, CTX_STREAM(ctx), d->counts, (unsigned long long)n, d_m);
@@ -628,8 +641,10 @@ int sfs2d_data_wrap_device(sfs2d_ctx* ctx, const uint32_t* d_counts, const uint3
     }
     d->max_nc1 = hm[0];
     d->max_nc2 = hm[1];
+    d->low_nc = hm[2] != 0u;
   } else {
     d->max_nc1 = d->max_nc2 = 0;
+    d->low_nc = false;
   }
   *out = d;
   return 0;
@@ -949,6 +964,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
       }
     }
   }
+  pl->fst_mask = data->low_nc;
   pl->fst_win = pl->sliced && bp && pl->fst && !pl->fst_scan;
   pl->nfst = pl->fst_win ? (int)std::min<int64_t>(1024, std::max<int64_t>(1, (pl->nslots + 7) / 8)) : 0;   // ~1 window per wave
   if (pl->scan_lds > 64 * 1024) {
@@ -964,6 +980,8 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
                           (const void*)k_scan_w<true, false, true, true>, (const void*)k_scan_w<false, false, true, true>,
                           (const void*)k_scan_w<true, true, 2, true>, (const void*)k_scan_w<false, true, 2, true>,
                           (const void*)k_scan_w<true, false, 2, true>, (const void*)k_scan_w<false, false, 2, true>,
+                          (const void*)k_scan_w<true, true, 3, true>, (const void*)k_scan_w<false, true, 3, true>,
+                          (const void*)k_scan_w<true, false, 3, true>, (const void*)k_scan_w<false, false, 3, true>,
                           (const void*)k_scan_g<true, false, false>, (const void*)k_scan_g<false, false, false>,
                           (const void*)k_scan_g<true, true, false>, (const void*)k_scan_g<false, true, false>,
                           (const void*)k_scan_g<true, false, true>, (const void*)k_scan_g<false, false, true>,

@@ -521,24 +521,30 @@ __global__ void k_init_lnx(double* lnx, double* dtab, double* ftab, double* rtab
 }
 
 // the largest called allele counts r1 + a1 / r2 + a2 over a data set (sfs2d_data_wrap_device: whether a
-// counts plan may skip validating the counts); m[2] zeroed by the caller
+// counts plan may skip validating the counts) and whether some SNP has < 2 called alleles in a population
+// (whether Fst summed in the scan must mask such SNPs); m[3] zeroed by the caller
 __global__ __launch_bounds__(256) void k_max_called(const uint32_t* __restrict__ counts, unsigned long long n,
                                                     uint32_t* __restrict__ m) {
   uint32_t m1 = 0, m2 = 0;
+  bool low = false;   // m[2]: some SNP with < 2 called alleles in a population
   for (unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (unsigned long long)gridDim.x * 256) {
     const uint32_t c = counts[i];
-    m1 = max(m1, __builtin_amdgcn_udot4(c, 0x00000101u, 0u, false));
-    m2 = max(m2, __builtin_amdgcn_udot4(c, 0x01010000u, 0u, false));
+    const uint32_t n1c = __builtin_amdgcn_udot4(c, 0x00000101u, 0u, false), n2c = __builtin_amdgcn_udot4(c, 0x01010000u, 0u, false);
+    m1 = max(m1, n1c);
+    m2 = max(m2, n2c);
+    low |= min(n1c, n2c) < 2u;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     m1 = max(m1, (uint32_t)__shfl_xor((int)m1, o, WAVE));
     m2 = max(m2, (uint32_t)__shfl_xor((int)m2, o, WAVE));
   }
+  const bool any_low = __ballot(low) != 0ull;
   if ((threadIdx.x & (WAVE - 1)) == 0) {
     atomicMax(&m[0], m1);
     atomicMax(&m[1], m2);
+    if (any_low) atomicMax(&m[2], 1u);
   }
 }
 
@@ -2389,10 +2395,12 @@ __device__ __forceinline__ void lds_copy_d(double* dst, const double* __restrict
 // FST: 0 no Fst; 1 k_prep's fixed-point sums of the slot, read and cleared; 2 (counts plans) Hudson's
 // terms summed here, per SNP of the rows the window streams anyway (fst_snp on the counts in registers,
 // membership = an inner 2D bin; the unfolded last bin in the rare pass), fp64 lane sums in a fixed order
-// and two wave sums per window: k_prep then runs without the Fst work (DESIGN.md "Fst placement")
+// and two wave sums per window: k_prep then runs without the Fst work (DESIGN.md "Fst placement");
+// 3: as 2, for data sets where some SNP has < 2 called alleles in a population (those SNPs masked out)
 template <bool P16, bool FUSED, int FST, bool CNT>
 __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
-  constexpr bool FSTIN = FST == 2;
+  constexpr bool FSTIN = FST >= 2;
+  constexpr bool FMASK = FST == 3;
   static_assert(!FSTIN || CNT, "Fst in the scan reads the counts");
   constexpr int NWV = SBLOCK / WAVE;
   constexpr int SB = 8;    // windows per batch (see flush; LDS-limited: the 2 KB of the retired trash words)
@@ -2731,12 +2739,13 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     uint32_t kw[8];   // the 2D words of the first 8 rows, cleared after the window
     // FSTIN: the pair's (p, A) of both populations from the global (alt, ref) table, issued before the
     // next rows' loads so that waiting for them leaves those in flight (loads complete in order)
-    // (entry 0 = (0, 0): a SNP without >= 2 called alleles in BOTH populations reads it for both)
+    // (FMASK: entry 0 = (0, 0) for both populations of an SNP without >= 2 called alleles in both --
+    // a data set without such SNPs skips the test: a population's entry alone is 0 below n = 2)
     auto fst_load = [&](uint32_t w0, uint32_t w1, double2 (&fq)[4]) {
       if (FSTIN) {
         auto both2 = [](uint32_t w) {
-          return (__builtin_amdgcn_udot4(w, 0x00000101u, 0u, false) >= 2u) &
-                 (__builtin_amdgcn_udot4(w, 0x01010000u, 0u, false) >= 2u);
+          return !FMASK || ((__builtin_amdgcn_udot4(w, 0x00000101u, 0u, false) >= 2u) &
+                            (__builtin_amdgcn_udot4(w, 0x01010000u, 0u, false) >= 2u));
         };
         const bool ok0 = both2(w0), ok1 = both2(w1);
         fq[0] = artg[ok0 ? w0 & 0xffffu : 0u]; fq[1] = artg[ok0 ? w0 >> 16 : 0u];
@@ -2782,11 +2791,18 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
         // five fp64 operations per SNP on the table's (p, A) (computed from (1/n, 1/(n(n-1))) they took
         // ~20 VALU instructions in a VALU-bound loop; an LDS table measured slower: the loop's LDS pipe
         // is busy, profiles/r03k_fst_scan.txt)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          fA += fq[2 * q].y + fq[2 * q + 1].y;
-          fP += fq[2 * q].x + fq[2 * q + 1].x;
-          fM = fma(fq[2 * q].x, fq[2 * q + 1].x, fM);
+        // (the window's first pair assigns: "x + 0.0" is no identity in fp64 (-0.0), so the adds to the
+        // zero-initialised sums would stay in the code)
+        const double a0 = fq[0].y + fq[1].y, a1 = fq[2].y + fq[3].y;
+        const double p0 = fq[0].x + fq[1].x, p1 = fq[2].x + fq[3].x;
+        if (j == 0) {
+          fA = a0 + a1;
+          fP = p0 + p1;
+          fM = fma(fq[2].x, fq[3].x, fq[0].x * fq[1].x);
+        } else {
+          fA += a0 + a1;
+          fP += p0 + p1;
+          fM = fma(fq[2].x, fq[3].x, fma(fq[0].x, fq[1].x, fM));
         }
       }
       // the ranks once both SNPs' atomics are issued (extracted right after its own atomic, each rank's
@@ -2801,8 +2817,8 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
         d[q] = Dt[min(rk[q], (uint32_t)LNT - 1u)];
         lp[q] = LPl[kk[q]];
       }
-#pragma unroll
-      for (int q = 0; q < 2; ++q) acc2 += d[q] - lp[q];
+      const double t = (d[0] - lp[0]) + (d[1] - lp[1]);
+      acc2 = j == 0 ? t : acc2 + t;
     };
     MARK(19);
 #pragma unroll
