@@ -56,6 +56,10 @@ constexpr int FBLOCK = 1024;      // k_bg_finalize workgroup
 constexpr int KBLOCK = 512;       // k_bg_slice workgroup
 constexpr int LNX_N = 1 << 20;    // ln(k) table for k < LNX_N (bin counts / window totals)
 constexpr int LNT = 512;          // D(r) and x ln x tables staged in LDS by k_scan_w
+constexpr int LNF = 256;          // k_scan_w: x ln x entries in LDS (x < LNF; the 1D pass and the flush, per window)
+// Fst's reciprocals (1/n, 1/(n(n-1))) in LDS (k_scan_w, k_scan_wl) for n <= 2 max(n1p, n2p): an even
+// count of double2
+__host__ __device__ inline int wl_rtn(int n1p, int n2p) { return 2 * (n1p > n2p ? n1p : n2p) + 2; }
 constexpr int RCPN = 512;         // (1/k, 1/(k(k-1))) for k < 512 (Fst: called allele counts ref + alt <= 510), after the LNT tables
 constexpr int FSTAR = 65536;      // Fst per population and SNP: (p, A) by (alt, ref) = one u16 half of the counts word, after RCPN
 constexpr int REPL = 4;           // replicas of the per-chromosome background histograms
@@ -1569,9 +1573,10 @@ struct Win {
   bool has;
 };
 
-// F(x) = x ln x from the LDS table, the global ln table beyond it
+// F(x) = x ln x from the LDS table (N entries), the global ln table beyond it
+template <int N = LNT>
 __device__ __forceinline__ double xlnx(uint32_t x, const double* Ft, const double* lnx) {
-  return x < (uint32_t)LNT ? Ft[x] : (double)x * lnx[x];
+  return x < (uint32_t)N ? Ft[x] : (double)x * lnx[x];
 }
 
 // The fused prologue of k_scan_w (kept out of line: it runs once per workgroup and its registers
@@ -2415,15 +2420,15 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   const int lane = tid & (WAVE - 1);
   const Chunk ch = chunks[blockIdx.x];
   const int bg = bg_per_chrom ? (int)ch.chrom : 0;
-  // FSTIN: one population's (p, A) by the (alt, ref) half of the counts word (k_init_lnx; L1-resident: the
-  // called counts cluster near 2 pop_size)
-  const double2* artg = reinterpret_cast<const double2*>(dfg + 2 * LNT + 2 * RCPN);
 
-  // LDS: lp table (nt, rounded up to even: the histograms are 16-B aligned) | D | F | histograms
+  // LDS: lp table (nt, rounded up to even: the histograms are 16-B aligned) | D (LNT) | F (LNF) |
+  // FSTIN: Fst's (1/n, 1/(n(n-1))) for n <= 2 max pop_size (wl_rtn) | histograms
   double* LPl = ldsd;
   double* Dt = LPl + ((P.nt + 1) & ~1);   // LNT
-  double* Ft = Dt + LNT;                  // LNT
-  uint32_t* HB = reinterpret_cast<uint32_t*>(Ft + LNT);
+  double* Ft = Dt + LNT;                  // LNF
+  double2* RT = reinterpret_cast<double2*>(Ft + LNF);
+  const int rtn = FSTIN ? wl_rtn(P.n1p, P.n2p) : 0;
+  uint32_t* HB = reinterpret_cast<uint32_t*>(RT + rtn);
   const int h2w = P16 ? ((P.nb2 + 1) / 2 + 3) & ~3 : (P.nb2 + 3) & ~3;
   const int h1w = R1 * (P.n1p + 1), h1wb = R1 * (P.n2p + 1);
   const int per = h2w + h1w + h1wb;   // (no trash words: SNPs outside the 2D SFS skip the atomic)
@@ -2469,8 +2474,11 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   const bool dyn = ch.slot_lo + ch.nstatic < ch.slot_hi;
   const uint32_t dbase = ch.slot_lo + ch.nstatic + pool;
   uint32_t* myctr = ctr + (((size_t)cpar * P.nchrom + ch.chrom) * CTR_POOLS + pool) * CTR_STRIDE;
-  uint32_t gq = 0;
-  if (active && dyn && lane == 0) gq = atomicAdd(myctr, 1u);
+  uint32_t gq1 = 0, gq = 0;   // two pool atomics in flight from the start (the schedule runs two ahead)
+  if (active && dyn && lane == 0) {
+    gq1 = atomicAdd(myctr, 1u);
+    gq = atomicAdd(myctr, 1u);
+  }
   if (blockIdx.x == 0)   // the other parity's counters, for the next run
     for (int k = tid; k < P.nchrom * CTR_POOLS; k += SBLOCK) ctr[((size_t)(1 - cpar) * P.nchrom * CTR_POOLS + k) * CTR_STRIDE] = 0u;
 
@@ -2479,8 +2487,9 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   // the prologue's global loads in flight together (each dependent round trip to L2 / MALL cost ~1 us
   // of config 2's ~4 us prologue): the D / F tables (two doubles per thread), and for sliced plans the
   // leaf sums, the tree nodes and the head's inputs, then the lp table
-  static_assert(2 * LNT == 2 * SBLOCK, "two D / F doubles per thread");
-  const double dfv0 = dfg[tid], dfv1 = dfg[tid + SBLOCK];
+  static_assert(LNT == SBLOCK && LNF <= SBLOCK, "one D and at most one F double per thread");
+  const double dfv0 = dfg[tid], dfv1 = tid < LNF ? dfg[LNT + tid] : 0.0;
+  const double2 rtv = (FSTIN && tid < rtn) ? reinterpret_cast<const double2*>(dfg + 2 * LNT)[tid] : make_double2(0.0, 0.0);
   BgHead hb;
   const size_t rs = (size_t)P.nchrom * P.nh;     // replica stride
   const uint32_t* Rc = repl + (size_t)par * REPL * rs + (size_t)ch.chrom * P.nh;
@@ -2496,7 +2505,8 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     }
     lds_copy_d(LPl, LPg + (size_t)bg * P.nt, P.nt);
     Dt[tid] = dfv0;
-    Dt[tid + SBLOCK] = dfv1;
+    if (tid < LNF) Ft[tid] = dfv1;
+    if (FSTIN && tid < rtn) RT[tid] = rtv;
     if (sliced) {
       // this run's per-chromosome table from k_bg_slice (proportions, logs, 1D part final) and its
       // leaf sums: numpy's tree over the leaves, then scipy's p[-1] rule on the 2D table -- the
@@ -2540,7 +2550,8 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     }
   } else {
     Dt[tid] = dfv0;
-    Dt[tid + SBLOCK] = dfv1;
+    if (tid < LNF) Ft[tid] = dfv1;
+    if (FSTIN && tid < rtn) RT[tid] = rtv;
     fused_table(P.nb2, P.nh, P.nt, P.n1p, P.n2p, P.n1, P.n2, P.t1a, P.t1b, P.nchrom, ch.chrom,
                 ch.first == 0 && (int)ch.chrom == write_chrom, bg,
                 Rc, rs, repl, bcount, par, tab, LPg, head, LPl, HB, leaves, nleaves, nodes, nnodes, nlevels, lnx,
@@ -2575,6 +2586,9 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   asm volatile("" : "+v"(a1b), "+v"(a2b));
   uint32_t awb = (uint32_t)(uintptr_t)((lds_u32*)W);   // the wave's 2D words (LDS byte address, uniform)
   asm volatile("" : "+s"(awb));
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(3))) d2v lds_d2;   // (16-B aligned: one ds_read_b128)
+  const uint32_t rtb = (uint32_t)(uintptr_t)((lds_d2*)RT);   // Fst's reciprocals (LDS byte address)
   // ---- batched finish.  Lane j of the B* registers holds the j-th window this wavefront has
   // scanned since the last flush (slot, SNP range, counts, the three sums); per window only the
   // sums' wave reductions run, and the T values, the zero / NaN rules, the Fst value and the 64-B
@@ -2597,9 +2611,9 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     const uint32_t Bse = Bsb + nsnp;
     WinOut w;
     w.snp_count = Bnv >> 16; w.n2 = Bn2 & 0xffffu; w.n2_all = Bn2 >> 16; w.n1a = Bn1 & 0xffffu; w.n1b = Bn1 >> 16;
-    w.t2d = 2.0 * (B2 - xlnx(w.n2, Ft, lnx));
-    w.t1a = 2.0 * (Ba - xlnx(w.n1a, Ft, lnx));
-    w.t1b = 2.0 * (Bb - xlnx(w.n1b, Ft, lnx));
+    w.t2d = 2.0 * (B2 - xlnx<LNF>(w.n2, Ft, lnx));
+    w.t1a = 2.0 * (Ba - xlnx<LNF>(w.n1a, Ft, lnx));
+    w.t1b = 2.0 * (Bb - xlnx<LNF>(w.n1b, Ft, lnx));
     // |T| this small may be an exactly proportional window: the exact evaluation below
     const bool exact = mine && !empty &&
                        (nsnp == 0xffffu || suspect_zero(w.t2d, w.n2) || suspect_zero(w.t1a, w.n1a) ||
@@ -2687,33 +2701,40 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   };
 
 
+  // the schedule runs two windows ahead: at window i's start the rows of window i+1 are issued (its slot
+  // record arrived during window i-1), window i+2's slot record is loaded (its pool index arrived during
+  // window i-1) and the pool atomic for window i+3 issued -- a window's rows get a whole window's time to
+  // arrive from HBM, and nothing in the row loop waits on a global load (Fst from LDS)
+  auto pool_slot = [&](uint32_t g) -> uint32_t {
+    const uint32_t j = __builtin_amdgcn_readfirstlane(g);
+    return dyn && dbase + npool * j < ch.slot_hi ? dbase + npool * j : ch.slot_hi;
+  };
   Win cur;
   bounds(s, sr0, cur);
+  uint32_t s1 = pool_slot(gq1);
+  uint2 sr1 = (mode_bp && s1 < ch.slot_hi) ? slots[s1] : make_uint2(0, 0);
+  uint2 srs = make_uint2(0, 0);   // the slot record of window s, for the rows issued after a flush
   STAMP(11);
   int it = 0;
-  uint32_t sn = ch.slot_hi;
-  uint2 srn = make_uint2(0, 0);
   for (;;) {
   while (s < ch.slot_hi) {
     // the batch's last window prefetches nothing: the flush after it (with the rare exact
     // evaluations) then runs with no rows in flight and no row registers live
     const bool fill = jb + 1u < (uint32_t)SB;
-    sn = ch.slot_hi;
-    if (dyn) {
-      const uint32_t j = __builtin_amdgcn_readfirstlane(gq);
-      sn = dbase + npool * j < ch.slot_hi ? dbase + npool * j : ch.slot_hi;
-      if (sn < ch.slot_hi && lane == 0) gq = atomicAdd(myctr, 1u);
-    }
-    const bool more = sn < ch.slot_hi;
-    srn = (mode_bp && more) ? slots[sn] : make_uint2(0, 0);
+    const bool more = s1 < ch.slot_hi;
+    const uint2 sr1u = make_uint2(__builtin_amdgcn_readfirstlane(sr1.x), __builtin_amdgcn_readfirstlane(sr1.y));
+    Win nxt;
+    nxt.has = false;
+    if (more && fill) bounds(s1, sr1u, nxt);
+    const uint32_t s2 = more ? pool_slot(gq) : ch.slot_hi;
+    const uint2 sr2 = (mode_bp && s2 < ch.slot_hi) ? slots[s2] : make_uint2(0, 0);
+    if (s2 < ch.slot_hi && lane == 0) gq = atomicAdd(myctr, 1u);
     if (!cur.has) {
       put(s, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0.0, 0.0, 0.0, make_ulonglong2(0ull, 0ull));   // (no SNP: no Fst sums)
       ++jb;
-      Win nxt;
-      nxt.has = false;
-      if (more && fill) bounds(sn, srn, nxt);
       cur = nxt;
-      s = sn;
+      s = s1; srs = sr1u;
+      s1 = s2; sr1 = sr2;
       if (!fill) break;
       continue;
     }
@@ -2737,19 +2758,30 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     double fA = 0.0, fP = 0.0, fM = 0.0;
     uint32_t n2 = 0, n1a = 0, n1b = 0, nlast = 0, nvar = 0;
     uint32_t kw[8];   // the 2D words of the first 8 rows, cleared after the window
-    // FSTIN: the pair's (p, A) of both populations from the global (alt, ref) table, issued before the
-    // next rows' loads so that waiting for them leaves those in flight (loads complete in order)
-    // (FMASK: entry 0 = (0, 0) for both populations of an SNP without >= 2 called alleles in both --
-    // a data set without such SNPs skips the test: a population's entry alone is 0 below n = 2)
+    // FSTIN: the pair's (p, A) of both populations, p = a / n and A = a (a - 1) / (n (n - 1)) from the
+    // LDS reciprocals (1/n, 1/(n(n-1))) (0 for n < 2): no global loads in the row loop, so that the next
+    // window's rows, issued at this window's start, are never waited for here (loads complete in order).
+    // (FMASK: a = 0 in both populations of an SNP without >= 2 called alleles in both -- a data set
+    // without such SNPs skips the test: a population alone below n = 2 reads (0, 0))
     auto fst_load = [&](uint32_t w0, uint32_t w1, double2 (&fq)[4]) {
       if (FSTIN) {
-        auto both2 = [](uint32_t w) {
-          return !FMASK || ((__builtin_amdgcn_udot4(w, 0x00000101u, 0u, false) >= 2u) &
-                            (__builtin_amdgcn_udot4(w, 0x01010000u, 0u, false) >= 2u));
-        };
-        const bool ok0 = both2(w0), ok1 = both2(w1);
-        fq[0] = artg[ok0 ? w0 & 0xffffu : 0u]; fq[1] = artg[ok0 ? w0 >> 16 : 0u];
-        fq[2] = artg[ok1 ? w1 & 0xffffu : 0u]; fq[3] = artg[ok1 ? w1 >> 16 : 0u];
+        const uint32_t ww[2] = {w0, w1};
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const uint32_t w = ww[q];
+          const uint32_t n1c = __builtin_amdgcn_udot4(w, 0x00000101u, 0u, false);
+          const uint32_t n2c = __builtin_amdgcn_udot4(w, 0x01010000u, 0u, false);
+          uint32_t a1 = __builtin_amdgcn_ubfe(w, 8, 8), a2 = w >> 24;
+          if (FMASK) {
+            const bool ok = min(n1c, n2c) >= 2u;
+            a1 = ok ? a1 : 0u;
+            a2 = ok ? a2 : 0u;
+          }
+          const d2v r1 = *(const lds_d2*)(uintptr_t)(rtb + 16u * n1c);
+          const d2v r2 = *(const lds_d2*)(uintptr_t)(rtb + 16u * n2c);
+          fq[2 * q] = make_double2((double)a1 * r1.x, (double)__umul24(a1, a1 - 1u) * r1.y);
+          fq[2 * q + 1] = make_double2((double)a2 * r2.x, (double)__umul24(a2, a2 - 1u) * r2.y);
+        }
       }
     };
     // SNPs past the window's end: w = 0 (unconditional: a guard on the window's last rows cost more
@@ -2848,6 +2880,10 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
           x1 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo + 256, 0, 0);
           pair(w0, w1, j, false, fq);
         }
+        // the last prefetch, consumed here: left in flight, its registers' reuse after the join of this
+        // (rare) path with the common one put a wait for every outstanding load -- the next window's rows
+        // included -- into every window
+        asm volatile("" ::"v"(x0), "v"(x1));
       } else {
         uint32_t x0 = 64 * 8 < lim ? qb[ln + 64 * 8] : 0u, x1 = 64 * 9 < lim ? qb[ln + 64 * 9] : 0u;
         for (int j = 8; 64 * j < (int)nsnp; j += 2) {
@@ -2876,7 +2912,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     // bins with x > LNT-1 SNPs: the ranks from LNT-1 on add F(x) - F(LNT-1) (read before the clear)
     if (clampd) {
       constexpr uint32_t L1 = LNT - 1;
-      const double fl = Ft[L1];
+      const double fl = (double)L1 * lnx[L1];   // F(LNT-1), as k_init_lnx's table entry
       for (int k = lane; k < h2w; k += WAVE) {
         const uint32_t v = W[k];
         const uint32_t xa = P16 ? (v & 0xffffu) : v, xb = P16 ? (v >> 16) : 0u;
@@ -2893,15 +2929,6 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       uint4* q = reinterpret_cast<uint4*>(W);
       for (int k = lane; k < h2w / 4; k += WAVE) q[k] = make_uint4(0, 0, 0, 0);
     }
-    // next window: its slot record is in, issue its first rows now (under the 1D pass and the sums);
-    // the record is wave-uniform: in SGPRs it survives the batch's flush without a VGPR spill
-    srn.x = __builtin_amdgcn_readfirstlane(srn.x);
-    srn.y = __builtin_amdgcn_readfirstlane(srn.y);
-    Win nxt;
-    nxt.has = false;
-#ifndef SFS2D_LATE_PF
-    if (more && fill) bounds(sn, srn, nxt);
-#endif
     MARK(24);
     // 1D spectra: one lane per folded inner bin reads (and clears) its R1 replicas; with <= 32 inner
     // bins per population, lanes 0-31 take population 1 and lanes 32-63 population 2 (acca)
@@ -2919,7 +2946,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
         const uint4 v = *q;
         *q = make_uint4(0, 0, 0, 0);
         x = (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
-        if (k >= 1 && k < np && x) acca = xlnx(x, Ft, lnx) - (double)x * LPl[(pa ? P.t1a : P.t1b) + k];
+        if (k >= 1 && k < np && x) acca = xlnx<LNF>(x, Ft, lnx) - (double)x * LPl[(pa ? P.t1a : P.t1b) + k];
       }
       n1a = slots - (uint32_t)__builtin_amdgcn_readlane((int)x, 0) - (uint32_t)__builtin_amdgcn_readlane((int)x, P.n1p);
       n1b = slots - (uint32_t)__builtin_amdgcn_readlane((int)x, 32) -
@@ -2935,7 +2962,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
           *q = make_uint4(0, 0, 0, 0);
           const uint32_t x = (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
           xa[j] = x;
-          if (k >= 1 && k < P.n1p && x) acca += xlnx(x, Ft, lnx) - (double)x * LPl[P.t1a + k];
+          if (k >= 1 && k < P.n1p && x) acca += xlnx<LNF>(x, Ft, lnx) - (double)x * LPl[P.t1a + k];
         }
         if (k <= P.n2p) {
           uint4* q = reinterpret_cast<uint4*>(H1b + k * R1);
@@ -2943,7 +2970,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
           *q = make_uint4(0, 0, 0, 0);
           const uint32_t x = (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
           xb[j] = x;
-          if (k >= 1 && k < P.n2p && x) accb += xlnx(x, Ft, lnx) - (double)x * LPl[P.t1b + k];
+          if (k >= 1 && k < P.n2p && x) accb += xlnx<LNF>(x, Ft, lnx) - (double)x * LPl[P.t1b + k];
         }
       }
       const uint32_t ea = P.n1p >= WAVE ? (uint32_t)__builtin_amdgcn_readlane((int)xa[1], P.n1p - WAVE)
@@ -2973,21 +3000,19 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       MARK(26);
       put(s, cur.b, nsnp, n2, n1a, n1b, nvar, nlast, s2, sa, sb, fq);
     }
-#ifdef SFS2D_LATE_PF
-    if (more && fill) bounds(sn, srn, nxt);
-#endif
     ++jb;
     group_sync<WAVE>();
     if (it == 0) STAMP(14);
     MARK(28);
     ++it;
     cur = nxt;
-    s = sn;
+    s = s1; srs = sr1u;
+    s1 = s2; sr1 = sr2;
     if (!fill) break;
   }
   if (jb) flush();   // (a full batch, or the wavefront's last windows)
   if (s >= ch.slot_hi) break;
-  bounds(s, srn, cur);   // the next batch's first window
+  bounds(s, srs, cur);   // the next batch's first window
   }
   STAMP(15);
   WV_STAMP(it);
@@ -3033,8 +3058,6 @@ __host__ __device__ inline int wl_hb_words(int nb2, int n1p, int n2p, int nt, in
   if (sliced) w = w > 2 * (nleaves + nnodes) ? w : 2 * (nleaves + nnodes);
   return w;
 }
-// Fst's reciprocals (1/n, 1/(n(n-1))) in LDS for n <= 2 max(n1p, n2p) (an even count of double2)
-__host__ __device__ inline int wl_rtn(int n1p, int n2p) { return 2 * (n1p > n2p ? n1p : n2p) + 2; }
 // LDS bytes of a k_scan_wl workgroup besides its static arrays: lp | D | Fst reciprocals | histogram area
 __host__ __device__ inline size_t wl_lds_bytes(int nb2, int n1p, int n2p, int nt, int nleaves, int nnodes, int fused,
                                                int sliced) {
@@ -3404,6 +3427,7 @@ __device__ __forceinline__ void scan_wl(double* ldsd, SCAN_W_ARGS) {
           x0 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo, 0, 0);
           row(w0);
         }
+        asm volatile("" ::"v"(x0));   // (the last prefetch consumed on this path: see k_scan_w)
       }
     }
     MARK(41);

@@ -214,7 +214,7 @@ def launch_ranks(n):
 class Ctx:
     """What both workloads share on a rank: the process group, the engine and the library's stream."""
 
-    def __init__(self, world, rank, local):
+    def __init__(self, world, rank, local, nstreams=3):
         import torch
         import torch.distributed as dist
         from sfs2d.engine import Engine
@@ -225,6 +225,11 @@ class Ctx:
         self.scan_s = torch.cuda.Stream(device=local)   # the HIP library's stream (and the final gather's)
         torch.cuda.set_stream(self.scan_s)
         self.eng.set_stream(self.scan_s.cuda_stream)
+        # the passes' streams, created once for every loop of the run: HIP maps streams onto the
+        # process's few hardware queues (4) in creation order, and a loop whose streams came after the
+        # earlier loops' shared queues (serialised passes: config 2 at 38 us per pass instead of 13)
+        self.streams = [self.scan_s.cuda_stream] + [torch.cuda.Stream(device=local).cuda_stream
+                                                    for _ in range(max(2, nstreams) - 1)]
 
     def max_over_ranks(self, x, dtype=None):
         if self.world == 1:
@@ -246,7 +251,9 @@ def run_loop(cx, plans, steps, warmup, label):
     ns = len(plans)
     nrec = plans[0].nrec
     rows = int(cx.max_over_ranks(nrec))   # tables padded to the largest shard (rows flagged empty)
-    sstreams = [cx.scan_s.cuda_stream] + [torch.cuda.Stream(device=cx.local).cuda_stream for _ in range(ns - 1)]
+    if ns > len(cx.streams):
+        raise ValueError(f"{label}: {ns} plans, {len(cx.streams)} streams")
+    sstreams = cx.streams[:ns]
     outs = [torch.zeros((rows, 64), dtype=torch.uint8, device=cx.cdev) for _ in range(ns)]
     for o in outs:
         o[nrec:, 39] = 0x80   # padding rows: flags = SFS2D_W_EMPTY
@@ -465,7 +472,7 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29517")
         dist.init_process_group("nccl", rank=rank, world_size=world)
         world = dist.get_world_size()   # n_gpus from the communicator
-    cx = Ctx(world, rank, local)
+    cx = Ctx(world, rank, local, max(2, args.streams))
 
     c3, genome = config3_strong(cx, args)
     c2 = None if args.no_config2 else config2_weak(cx, args)
