@@ -876,6 +876,47 @@ int sfs2d_vcf_columns(const sfs2d_vcf* v, const int32_t** chrom, const int64_t**
   return SFS2D_VCF_OK;
 }
 
+int sfs2d_vcf_pack(const sfs2d_vcf* v, const int32_t* chrom_rank, int32_t pop1, int32_t pop2, uint32_t* counts,
+                   uint32_t* pos, uint16_t* ann) {
+  if (!v || !chrom_rank || !counts || !pos || !ann) return SFS2D_VCF_E_ARG;
+  const int P = (int)v->pops.size();
+  if (pop1 >= P || pop2 >= P || v->anns.size() > 65535) return pop1 >= P || pop2 >= P ? SFS2D_VCF_E_ARG : 1;
+  const int64_t n = v->n;
+  const int T = std::max(1, std::min<int>(host_threads(), (int)std::max<int64_t>(1, n / 65536)));
+  std::vector<uint8_t> bad(T, 0);
+  auto work = [&](int t) {
+    const int64_t lo = n * t / T, hi = n * (t + 1) / T;
+    for (int64_t i = lo; i < hi; ++i) {
+      const int64_t x = v->pos[i];
+      if (x < 0 || x > 0xffffffffll) { bad[t] = 1; return; }   // (INT64_MIN: not a plain decimal)
+      if (i > 0) {   // scan order: chromosome rank non-decreasing, positions non-decreasing within one
+        const int32_t r0 = chrom_rank[v->chrom[i - 1]], r1 = chrom_rank[v->chrom[i]];
+        if (r1 < r0 || (r1 == r0 && v->pos[i - 1] > x)) { bad[t] = 1; return; }
+      }
+      uint32_t c = 0;
+      const int32_t* q = &v->calls[(size_t)i * 2 * P];
+      if (pop1 >= 0 && q[2 * pop1] >= 0) {
+        if (q[2 * pop1] > 255 || q[2 * pop1 + 1] > 255) { bad[t] = 1; return; }
+        c |= (uint32_t)q[2 * pop1] | (uint32_t)q[2 * pop1 + 1] << 8;
+      }
+      if (pop2 >= 0 && q[2 * pop2] >= 0) {
+        if (q[2 * pop2] > 255 || q[2 * pop2 + 1] > 255) { bad[t] = 1; return; }
+        c |= (uint32_t)q[2 * pop2] << 16 | (uint32_t)q[2 * pop2 + 1] << 24;
+      }
+      counts[i] = c;
+      pos[i] = (uint32_t)x;
+      ann[i] = (uint16_t)v->ann[i];
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+  for (uint8_t b : bad)
+    if (b) return 1;
+  return SFS2D_VCF_OK;
+}
+
 int sfs2d_vcf_stats(const sfs2d_vcf* v, int64_t* text_bytes, int64_t* lines, double* t_inflate, double* t_parse,
                     double* t_merge) {
   if (!v) return SFS2D_VCF_E_ARG;

@@ -85,13 +85,12 @@ def main(argv=None):
         a.window = [20000]
 
     import twoDSFS_class as T
-    from sfs2d.vcf import read_vcf
+    from sfs2d.vcf import make_packed_vcf
 
     t0 = time.perf_counter()
-    tab = read_vcf(a.vcf, a.popmap, nthreads=a.threads)
-    packed = tab.to_packed(a.pop1, a.pop2)
+    packed = make_packed_vcf(a.vcf, a.popmap, a.pop1, a.pop2, nthreads=a.threads)
     t1 = time.perf_counter()
-    print(f"ingest: {tab.n} SNPs, {packed.nchrom} chromosomes in {t1 - t0:.2f} s", file=sys.stderr)
+    print(f"ingest: {packed.n} SNPs, {packed.nchrom} chromosomes in {t1 - t0:.3f} s", file=sys.stderr)
     chr_ids = T.load_chr_ids(a.chromosomes) if a.chromosomes else {}
     pixy = read_pixy_fst(a.pixy_fst) if a.pixy_fst else None
     obj = T.LikelihoodInference_jointSFS(a.vcf, a.popmap, pop1=a.pop1, pop2=a.pop2, pop1_size=a.pop1_size,

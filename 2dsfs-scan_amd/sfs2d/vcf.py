@@ -32,7 +32,7 @@ INGEST_PATH = os.environ.get("SFS2D_INGEST_LIB", os.path.join(HERE, "..", "csrc"
 EXPORTS = [
     "sfs2d_vcf_read", "sfs2d_vcf_free", "sfs2d_vcf_last_error", "sfs2d_vcf_num_records", "sfs2d_vcf_num_pops",
     "sfs2d_vcf_pop_name", "sfs2d_vcf_num_chroms", "sfs2d_vcf_chrom_name", "sfs2d_vcf_num_annotations",
-    "sfs2d_vcf_annotation", "sfs2d_vcf_columns", "sfs2d_vcf_stats",
+    "sfs2d_vcf_annotation", "sfs2d_vcf_columns", "sfs2d_vcf_stats", "sfs2d_vcf_pack",
 ]
 E_INDEX, E_VALUE = -3, -4
 
@@ -60,6 +60,7 @@ def ingest_lib():
         getattr(L, f).restype = C.c_char_p
     L.sfs2d_vcf_columns.argtypes = [vp] + [C.POINTER(vp)] * 7
     L.sfs2d_vcf_stats.argtypes = [vp, C.POINTER(i64), C.POINTER(i64)] + [C.POINTER(C.c_double)] * 3
+    L.sfs2d_vcf_pack.argtypes = [vp, vp, C.c_int32, C.c_int32, vp, vp, vp]
     _ilib = L
     return L
 
@@ -191,8 +192,8 @@ class VcfTable:
                           self.ann[order].astype(np.uint16), list(self.ann_names), pop1, pop2)
 
 
-def read_vcf(vcf_filename, popinfo_filename, nthreads: int = 0) -> VcfTable:
-    """Parse with the native multithreaded parser; raises the reference's exception types."""
+def _open(vcf_filename, popinfo_filename, nthreads):
+    """The native parse; raises the reference's exception types.  Returns the library's handle."""
     L = ingest_lib()
     h = C.c_void_p()
     rc = L.sfs2d_vcf_read(os.fsencode(str(vcf_filename)), os.fsencode(str(popinfo_filename)), int(nthreads),
@@ -206,31 +207,74 @@ def read_vcf(vcf_filename, popinfo_filename, nthreads: int = 0) -> VcfTable:
         if rc == -1:
             raise FileNotFoundError(msg)
         raise Sfs2dError(rc, msg)
+    return L, h
+
+
+def _names(L, h):
+    dec = (lambda b: b.decode("utf-8", "surrogateescape"))
+    pops = [dec(L.sfs2d_vcf_pop_name(h, i)) for i in range(int(L.sfs2d_vcf_num_pops(h)))]
+    chroms = [dec(L.sfs2d_vcf_chrom_name(h, i)) for i in range(L.sfs2d_vcf_num_chroms(h))]
+    anns = [dec(L.sfs2d_vcf_annotation(h, i)) for i in range(L.sfs2d_vcf_num_annotations(h))]
+    return pops, chroms, anns
+
+
+def _table(L, h) -> VcfTable:
+    n = int(L.sfs2d_vcf_num_records(h))
+    pops, chroms, anns = _names(L, h)
+    P = len(pops)
+    ptrs = [C.c_void_p() for _ in range(7)]
+    L.sfs2d_vcf_columns(h, *[C.byref(p) for p in ptrs])
+    chrom = _view(ptrs[0].value, np.int32, n)
+    pos = _view(ptrs[1].value, np.int64, n)
+    pos_off = _view(ptrs[3].value, np.int64, n + 1)
+    blob = C.string_at(ptrs[2].value, int(pos_off[-1])) if n and pos_off[-1] else b""
+    texts = _PosTexts(blob, pos_off)
+    ann = _view(ptrs[4].value, np.int32, n)
+    alle = _view(ptrs[5].value, np.uint8, 2 * n).reshape(n, 2)
+    calls = _view(ptrs[6].value, np.int32, n * P * 2).reshape(n, P, 2)
+    tb, ln = C.c_int64(), C.c_int64()
+    t = [C.c_double() for _ in range(3)]
+    L.sfs2d_vcf_stats(h, C.byref(tb), C.byref(ln), *[C.byref(x) for x in t])
+    stats = {"text_bytes": tb.value, "lines": ln.value, "t_inflate": t[0].value, "t_parse": t[1].value,
+             "t_merge": t[2].value}
+    return VcfTable(pops, chroms, anns, chrom, pos, texts, ann, alle, calls, stats)
+
+
+def read_vcf(vcf_filename, popinfo_filename, nthreads: int = 0) -> VcfTable:
+    """Parse with the native multithreaded parser; raises the reference's exception types."""
+    L, h = _open(vcf_filename, popinfo_filename, nthreads)
     try:
-        n = int(L.sfs2d_vcf_num_records(h))
-        P = int(L.sfs2d_vcf_num_pops(h))
-        dec = (lambda b: b.decode("utf-8", "surrogateescape"))
-        pops = [dec(L.sfs2d_vcf_pop_name(h, i)) for i in range(P)]
-        chroms = [dec(L.sfs2d_vcf_chrom_name(h, i)) for i in range(L.sfs2d_vcf_num_chroms(h))]
-        anns = [dec(L.sfs2d_vcf_annotation(h, i)) for i in range(L.sfs2d_vcf_num_annotations(h))]
-        ptrs = [C.c_void_p() for _ in range(7)]
-        L.sfs2d_vcf_columns(h, *[C.byref(p) for p in ptrs])
-        chrom = _view(ptrs[0].value, np.int32, n)
-        pos = _view(ptrs[1].value, np.int64, n)
-        pos_off = _view(ptrs[3].value, np.int64, n + 1)
-        blob = C.string_at(ptrs[2].value, int(pos_off[-1])) if n and pos_off[-1] else b""
-        texts = _PosTexts(blob, pos_off)
-        ann = _view(ptrs[4].value, np.int32, n)
-        alle = _view(ptrs[5].value, np.uint8, 2 * n).reshape(n, 2)
-        calls = _view(ptrs[6].value, np.int32, n * P * 2).reshape(n, P, 2)
-        tb, ln = C.c_int64(), C.c_int64()
-        t = [C.c_double() for _ in range(3)]
-        L.sfs2d_vcf_stats(h, C.byref(tb), C.byref(ln), *[C.byref(x) for x in t])
-        stats = {"text_bytes": tb.value, "lines": ln.value, "t_inflate": t[0].value, "t_parse": t[1].value,
-                 "t_merge": t[2].value}
+        return _table(L, h)
     finally:
         L.sfs2d_vcf_free(h)
-    return VcfTable(pops, chroms, anns, chrom, pos, texts, ann, alle, calls, stats)
+
+
+def _packed_fast(L, h, pop1, pop2):
+    """VcfTable.to_packed for a file already in scan order, packed natively (sfs2d_vcf_pack) from the
+    library's table without copying its columns; None when that path does not apply."""
+    n = int(L.sfs2d_vcf_num_records(h))
+    pops, chroms, anns = _names(L, h)
+    if n == 0 or any("-" in c for c in chroms):
+        return None
+    order_names = sorted(range(len(chroms)), key=lambda c: chroms[c])
+    rank = np.empty(len(chroms), np.int32)
+    rank[order_names] = np.arange(len(order_names), dtype=np.int32)
+    counts = np.empty(n, np.uint32)
+    pos = np.empty(n, np.uint32)
+    ann = np.empty(n, np.uint16)
+    i1 = pops.index(pop1) if pop1 in pops else -1
+    i2 = pops.index(pop2) if pop2 in pops else -1
+    rc = L.sfs2d_vcf_pack(h, rank.ctypes.data, i1, i2, counts.ctypes.data, pos.ctypes.data, ann.ctypes.data)
+    if rc != 0:
+        return None
+    ptrs = [C.c_void_p() for _ in range(7)]
+    L.sfs2d_vcf_columns(h, *[C.byref(p) for p in ptrs])
+    chrom = np.frombuffer((C.c_char * (4 * n)).from_address(ptrs[0].value), dtype=np.int32)   # borrowed
+    crank = rank[chrom]
+    bounds = np.nonzero(np.diff(crank))[0] + 1
+    offs = np.concatenate([[0], bounds, [n]]).astype(np.int64)
+    names = [chroms[order_names[int(r)]] for r in crank[offs[:-1]]]
+    return PackedSNPs(counts, pos, offs, names, ann, list(anns), pop1, pop2)
 
 
 def make_data_dict_vcf(vcf_filename, popinfo_filename):
@@ -240,5 +284,12 @@ def make_data_dict_vcf(vcf_filename, popinfo_filename):
 
 def make_packed_vcf(vcf_filename, popinfo_filename, pop1: str = "uv", pop2: str = "bv",
                     nthreads: int = 0) -> PackedSNPs:
-    """VCF + popmap straight to the packed scan-order arrays (no dict)."""
-    return read_vcf(vcf_filename, popinfo_filename, nthreads).to_packed(pop1, pop2)
+    """VCF + popmap straight to the packed scan-order arrays (no dict): natively for a file in scan
+    order, else through VcfTable.to_packed (which also raises the reference's errors)."""
+    L, h = _open(vcf_filename, popinfo_filename, nthreads)
+    try:
+        p = _packed_fast(L, h, pop1, pop2)
+        tab = None if p is not None else _table(L, h)
+    finally:
+        L.sfs2d_vcf_free(h)
+    return p if p is not None else tab.to_packed(pop1, pop2)

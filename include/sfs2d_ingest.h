@@ -67,6 +67,20 @@ const char* sfs2d_vcf_annotation(const sfs2d_vcf* v, int32_t i);
 int sfs2d_vcf_columns(const sfs2d_vcf* v, const int32_t** chrom, const int64_t** pos, const char** pos_blob,
                       const int64_t** pos_off, const int32_t** ann, const uint8_t** alleles, const int32_t** calls);
 
+/* The scan-ready packed arrays of two populations straight from the table -- pack_snp_dict(
+ * make_data_dict_vcf(...), pop1, pop2) without the dict (twoDSFS_class.py:828-835 order: chromosome
+ * name, then integer position) -- for the common file already in that order:
+ *   chrom_rank[c]  the rank of chromosome c's name among the sorted names (the caller's sort)
+ *   pop1, pop2     population indices, or -1 for a population absent from the popmap (counts 0)
+ *   counts[n]      ref1 | alt1 << 8 | ref2 << 16 | alt2 << 24 (a population missing from a record: 0)
+ *   pos[n]         POS as uint32;  ann[n]: annotation index as uint16
+ * Returns 0 when packed; 1 when the fast path does not apply -- the records are not in scan order,
+ * a POS is not a plain decimal or does not fit uint32, an allele count exceeds 255 or there are more
+ * than 65535 annotations -- and the caller then packs in its general path (which raises the
+ * reference's errors); SFS2D_VCF_E_ARG for bad arguments. */
+int sfs2d_vcf_pack(const sfs2d_vcf* v, const int32_t* chrom_rank, int32_t pop1, int32_t pop2, uint32_t* counts,
+                   uint32_t* pos, uint16_t* ann);
+
 /* statistics of the last read: bytes of text, data lines, seconds in inflate / parse / merge */
 int sfs2d_vcf_stats(const sfs2d_vcf* v, int64_t* text_bytes, int64_t* lines, double* t_inflate, double* t_parse,
                     double* t_merge);

@@ -203,8 +203,16 @@ def test_sorted_fast_path(tmp_path, monkeypatch, twist):
         a = V.read_vcf(path, pm, nthreads=3).to_packed()
         monkeypatch.setenv("SFS2D_VCF_HASH_MERGE", "0")
         b = V.read_vcf(path, pm, nthreads=3).to_packed()
-        assert np.array_equal(a.counts, b.counts) and np.array_equal(a.pos, b.pos)
-        assert np.array_equal(a.chrom_off, b.chrom_off) and a.chrom_names == b.chrom_names
+        c = V.make_packed_vcf(path, pm, nthreads=3)   # the native pack (scan-ordered files) or its fallback
+        for q in (b, c):
+            assert np.array_equal(a.counts, q.counts) and np.array_equal(a.pos, q.pos)
+            assert np.array_equal(a.chrom_off, q.chrom_off) and a.chrom_names == q.chrom_names
+            assert np.array_equal(a.ann_id, q.ann_id) and a.ann_names == q.ann_names
+    else:   # int() of the POS text raises in the general path, which the native pack falls back to
+        with pytest.raises(ValueError):
+            V.read_vcf(path, pm).to_packed()
+        with pytest.raises(ValueError):
+            V.make_packed_vcf(path, pm)
 
 
 def test_bgzf_multi_block(tmp_path):
