@@ -745,6 +745,7 @@ static int make_kparams(sfs2d_ctx* ctx, const sfs2d_params* prm, int nchrom, KPa
   K->nb2 = (K->n1 + 1) * (K->n2 + 1);
   K->h1a = K->nb2; K->h1b = K->nb2 + K->n1 + 1; K->nh = (K->h1b + K->n2 + 1 + 3) & ~3;   // 16-B rows
   K->t1a = K->nb2; K->t1b = K->nb2 + K->n1p + 1; K->nt = K->t1b + K->n2p + 1;
+  K->rtn = wl_rtn(K->n1p, K->n2p);   // (plans: widened to the data's largest called count)
   K->fold = prm->fold ? 1 : 0;
   K->fold_thr = prm->fold ? K->n1p + K->n2p : 0x7fffffff;
   K->ann_want = prm->ann_want;
@@ -813,6 +814,11 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   pl->K.kmul = (uint32_t)(pl->K.n2 + 1) | (1u << 16);
   pl->K.n12 = (uint32_t)pl->K.n1 | ((uint32_t)pl->K.n2 << 16);
   pl->K.lim12 = (uint32_t)(pl->K.n1p - 1) | ((uint32_t)(pl->K.n2p - 1) << 16);
+  {   // Fst's reciprocals in LDS cover the data's largest called count: the reference counts SNPs whose
+      // r + a exceeds 2 pop_size as long as the key stays in the grid (u8 counts: n <= 510)
+    const uint32_t mx = std::min<uint32_t>(510u, std::max(data->max_nc1, data->max_nc2));
+    pl->K.rtn = std::max(wl_rtn(K.n1p, K.n2p), (int)((mx + 2u) & ~1u));
+  }
   if (pl->nslots > 0x7fffffffll) { delete pl; return set_err(ctx, SFS2D_E_ARG, "too many window slots (window too small)"); }
   pl->extra_rec = ((prm->flags & SFS2D_F_PREV_EXTRA) && bp && any) ? pl->nslots : -1;
   pl->nrec = pl->nslots + (pl->extra_rec >= 0 ? 1 : 0);
@@ -867,7 +873,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
       const int h2w = pl->p16 ? (((K.nb2 + 1) / 2 + 3) & ~3) : ((K.nb2 + 3) & ~3);
       const int per = h2w + R1 * (K.n1p + 1) + R1 * (K.n2p + 1);   // (no trash words: scan_w_small)
       const size_t hist_words = std::max<size_t>((size_t)(SBLOCK / WAVE) * per, (size_t)FUSED_VCNT + K.nt + 16);
-      const size_t rt = (prm->flags & SFS2D_F_FST) ? 2 * (size_t)wl_rtn(K.n1p, K.n2p) : 0;
+      const size_t rt = (prm->flags & SFS2D_F_FST) ? 2 * (size_t)pl->K.rtn : 0;
       pl->scan_lds = sizeof(double) * (size_t)(((K.nt + 1) & ~1) + LNT + LNF + rt) + hist_words * 4;
       // with the static LDS of the variant that uses most (the batched finish's per-wave arrays, Fst);
       // grids whose workgroup does not fit the 160 KB (e.g. 81 x 81) take the large-grid kernels
@@ -953,7 +959,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
     const char* ev = std::getenv("SFS2D_LITE");
     if (can && ev && ev[0] == '1') {
       const size_t lds_l = wl_lds_bytes(K.nb2, K.n1p, K.n2p, K.nt, (int)pw.leaves.size(), (int)pw.nodes.size(),
-                                        pl->fused ? 1 : 0, pl->sliced ? 1 : 0);
+                                        pl->fused ? 1 : 0, pl->sliced ? 1 : 0, pl->K.rtn);
       const void* fl = pl->fused ? (pl->fst ? (const void*)k_scan_wl<true, 2> : (const void*)k_scan_wl<true, 0>)
                                  : (pl->fst ? (const void*)k_scan_wl<false, 2> : (const void*)k_scan_wl<false, 0>);
       if (lds_l > 64 * 1024) hipFuncSetAttribute(fl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::min<size_t>(lds_l, 160 * 1024));

@@ -131,6 +131,8 @@ struct KParams {
   uint32_t nm1;          // the data set's last SNP index (counts-reading scans clamp their row loads to it)
   uint32_t kmul;         // bytes (n2+1, 0, 1, 0): the 2D key x1*(n2+1) + x2 as one byte dot product
   uint32_t n12, lim12;   // u16 pairs (n1, n2), (n1p-1, n2p-1): both folded 1D bins in packed 16-bit ops
+  int rtn;               // Fst's (1/n, 1/(n(n-1))) entries in LDS (k_scan_w, k_scan_wl): n up to the data's
+                         // largest called count (even; >= wl_rtn(n1p, n2p))
 };
 
 struct Tile {   // k_prep work item: SNPs [begin, end) of chromosome chrom = [cb, ce), slots from sbase
@@ -141,7 +143,7 @@ constexpr int SCAN_PAD = 512;   // readable words past the end of the per-SNP bi
 constexpr int CTR_POOLS = 8;     // k_scan_w dynamic window pools per chromosome
 constexpr int CTR_STRIDE = 16;   // one 64-B line per pool counter
 #ifndef SFS2D_PREP_PREFETCH
-#define SFS2D_PREP_PREFETCH 1
+#define SFS2D_PREP_PREFETCH 2
 #endif
 #ifndef SFS2D_FST_LDS
 #define SFS2D_FST_LDS 256
@@ -881,21 +883,23 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
     x.xp = 0;
     x.xn = 0;
     if (DO_SEG) {   // neighbour positions at the wave edges and past the tile end
+      // (buffer loads on the chromosome's positions, issued by every lane, out of range -- 0, no
+      // access -- where no neighbour is needed: no branch around them, so the count of loads in
+      // flight is the same on every path and a step waits only for its own buffer)
+      const __amdgpu_buffer_rsrc_t pr =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(pos + t.cb), (short)0, (int)((t.ce - t.cb) * 4u), 0x00020000);
+      const uint32_t none = (t.ce - t.cb) * 4u;
       const bool edge_next = lane == WAVE - 1 || ia + 4 >= t.end;
-      if (lane == 0 && ia > 0) x.xp = pos[min(ia, alast + 4u) - 1];
-      if (edge_next && ia + 4 < t.ce) x.xn = pos[ia + 4];
+      const uint32_t op = (lane == 0 && ia > t.cb) ? (min(ia, alast + 4u) - 1u - t.cb) * 4u : none;
+      const uint32_t on = (edge_next && ia + 4 < t.ce) ? (ia + 4u - t.cb) * 4u : none;
+      x.xp = __builtin_amdgcn_raw_buffer_load_b32(pr, (int)op, 0, 0);
+      x.xn = __builtin_amdgcn_raw_buffer_load_b32(pr, (int)on, 0, 0);
     }
     return x;
   };
-  StepIn nxt = load_step(ab);
-  for (uint32_t base = ab; base < t.end; base += STEP) {
+  // one step of the tile: the SNPs [base, base + STEP), from its loaded vectors
+  auto body = [&](uint32_t base, const StepIn& cur) {
     const uint32_t ia = base + 4 * threadIdx.x;
-#if SFS2D_PREP_PREFETCH
-    const StepIn cur = nxt;
-    if (base + STEP < t.end) nxt = load_step(base + STEP);   // block-uniform
-#else
-    const StepIn cur = base == ab ? nxt : load_step(base);
-#endif
     const uint4 ca = cur.c, pa = cur.p;
     const uint2 aav = cur.a;
     uint32_t wpa = 0, wna = 0;
@@ -929,7 +933,33 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
       asm volatile("; HOT_END");
 #endif
     }
+  };
+#if SFS2D_PREP_PREFETCH >= 2
+  // two steps of loads in flight per wave: two buffers in turn (loop unrolled by two, so that no
+  // buffer is copied while its loads are pending), each reloaded for the step after next once its
+  // step is done.  The reloads are unconditional (past the tile they re-read its last vector, never
+  // used): with a path-independent count of loads in flight the compiler waits for exactly the
+  // buffer a step needs (vmcnt(n)), not for all of them
+  StepIn bufA = load_step(ab), bufB = load_step(ab + STEP);
+  for (uint32_t base = ab; base < t.end; base += 2 * STEP) {
+    body(base, bufA);
+    bufA = load_step(base + 2 * STEP);
+    if (base + STEP >= t.end) break;
+    body(base + STEP, bufB);
+    bufB = load_step(base + 3 * STEP);
   }
+#else
+  StepIn nxt = load_step(ab);
+  for (uint32_t base = ab; base < t.end; base += STEP) {
+#if SFS2D_PREP_PREFETCH
+    const StepIn cur = nxt;
+    if (base + STEP < t.end) nxt = load_step(base + STEP);   // block-uniform
+#else
+    const StepIn cur = base == ab ? nxt : load_step(base);
+#endif
+    body(base, cur);
+  }
+#endif
   STAMP(22);
   if (err) atomicOr(err_word, err);
   if (DO_BG) {
@@ -2422,12 +2452,12 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   const int bg = bg_per_chrom ? (int)ch.chrom : 0;
 
   // LDS: lp table (nt, rounded up to even: the histograms are 16-B aligned) | D (LNT) | F (LNF) |
-  // FSTIN: Fst's (1/n, 1/(n(n-1))) for n <= 2 max pop_size (wl_rtn) | histograms
+  // FSTIN: Fst's (1/n, 1/(n(n-1))) for n < P.rtn | histograms
   double* LPl = ldsd;
   double* Dt = LPl + ((P.nt + 1) & ~1);   // LNT
   double* Ft = Dt + LNT;                  // LNF
   double2* RT = reinterpret_cast<double2*>(Ft + LNF);
-  const int rtn = FSTIN ? wl_rtn(P.n1p, P.n2p) : 0;
+  const int rtn = FSTIN ? P.rtn : 0;
   uint32_t* HB = reinterpret_cast<uint32_t*>(RT + rtn);
   const int h2w = P16 ? ((P.nb2 + 1) / 2 + 3) & ~3 : (P.nb2 + 3) & ~3;
   const int h1w = R1 * (P.n1p + 1), h1wb = R1 * (P.n2p + 1);
@@ -3060,8 +3090,8 @@ __host__ __device__ inline int wl_hb_words(int nb2, int n1p, int n2p, int nt, in
 }
 // LDS bytes of a k_scan_wl workgroup besides its static arrays: lp | D | Fst reciprocals | histogram area
 __host__ __device__ inline size_t wl_lds_bytes(int nb2, int n1p, int n2p, int nt, int nleaves, int nnodes, int fused,
-                                               int sliced) {
-  return sizeof(double) * (size_t)(((nt + 1) & ~1) + LDT + 2 * wl_rtn(n1p, n2p)) +
+                                               int sliced, int rtn) {
+  return sizeof(double) * (size_t)(((nt + 1) & ~1) + LDT + 2 * rtn) +
          4 * (size_t)wl_hb_words(nb2, n1p, n2p, nt, nleaves, nnodes, fused, sliced);
 }
 
@@ -3139,7 +3169,7 @@ __device__ __forceinline__ void scan_wl(double* ldsd, SCAN_W_ARGS) {
   const Chunk ch = chunks[blockIdx.x];
   const int bg = bg_per_chrom ? (int)ch.chrom : 0;
   const double2* rtg = reinterpret_cast<const double2*>(dfg + 2 * LNT);   // Fst (1/n, 1/(n(n-1))) by n
-  const int rtn = wl_rtn(P.n1p, P.n2p);
+  const int rtn = P.rtn;
   double* LPl = ldsd;
   double* Dt = LPl + ((P.nt + 1) & ~1);
   double2* RT = reinterpret_cast<double2*>(Dt + LDT);
