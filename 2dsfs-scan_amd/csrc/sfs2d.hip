@@ -873,7 +873,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
       const int h2w = pl->p16 ? (((K.nb2 + 1) / 2 + 3) & ~3) : ((K.nb2 + 3) & ~3);
       const int per = h2w + R1 * (K.n1p + 1) + R1 * (K.n2p + 1);   // (no trash words: scan_w_small)
       const size_t hist_words = std::max<size_t>((size_t)(SBLOCK / WAVE) * per, (size_t)FUSED_VCNT + K.nt + 16);
-      const size_t rt = (prm->flags & SFS2D_F_FST) ? 4 * (size_t)pl->K.rtn : 0;   // reciprocals + (a, a (a-1))
+      const size_t rt = (prm->flags & SFS2D_F_FST) ? 2 * (size_t)pl->K.rtn : 0;
       pl->scan_lds = sizeof(double) * (size_t)(((K.nt + 1) & ~1) + LNT + LNF + rt) + hist_words * 4;
       // with the static LDS of the variant that uses most (the batched finish's per-wave arrays, Fst);
       // grids whose workgroup does not fit the 160 KB (e.g. 81 x 81) take the large-grid kernels

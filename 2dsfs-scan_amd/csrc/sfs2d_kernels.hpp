@@ -2458,8 +2458,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   double* Ft = Dt + LNT;                  // LNF
   double2* RT = reinterpret_cast<double2*>(Ft + LNF);
   const int rtn = FSTIN ? P.rtn : 0;
-  double2* AT = RT + rtn;                 // FSTIN: (a, a (a - 1)) as doubles, a < rtn
-  uint32_t* HB = reinterpret_cast<uint32_t*>(AT + rtn);
+  uint32_t* HB = reinterpret_cast<uint32_t*>(RT + rtn);
   const int h2w = P16 ? ((P.nb2 + 1) / 2 + 3) & ~3 : (P.nb2 + 3) & ~3;
   const int h1w = R1 * (P.n1p + 1), h1wb = R1 * (P.n2p + 1);
   const int per = h2w + h1w + h1wb;   // (no trash words: SNPs outside the 2D SFS skip the atomic)
@@ -2537,7 +2536,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     lds_copy_d(LPl, LPg + (size_t)bg * P.nt, P.nt);
     Dt[tid] = dfv0;
     if (tid < LNF) Ft[tid] = dfv1;
-    if (FSTIN && tid < rtn) { RT[tid] = rtv; AT[tid] = make_double2((double)tid, (double)(tid * (tid - 1))); }
+    if (FSTIN && tid < rtn) RT[tid] = rtv;
     if (sliced) {
       // this run's per-chromosome table from k_bg_slice (proportions, logs, 1D part final) and its
       // leaf sums: numpy's tree over the leaves, then scipy's p[-1] rule on the 2D table -- the
@@ -2582,7 +2581,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   } else {
     Dt[tid] = dfv0;
     if (tid < LNF) Ft[tid] = dfv1;
-    if (FSTIN && tid < rtn) { RT[tid] = rtv; AT[tid] = make_double2((double)tid, (double)(tid * (tid - 1))); }
+    if (FSTIN && tid < rtn) RT[tid] = rtv;
     fused_table(P.nb2, P.nh, P.nt, P.n1p, P.n2p, P.n1, P.n2, P.t1a, P.t1b, P.nchrom, ch.chrom,
                 ch.first == 0 && (int)ch.chrom == write_chrom, bg,
                 Rc, rs, repl, bcount, par, tab, LPg, head, LPl, HB, leaves, nleaves, nodes, nnodes, nlevels, lnx,
@@ -2620,7 +2619,6 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   typedef double d2v __attribute__((ext_vector_type(2)));
   typedef __attribute__((address_space(3))) d2v lds_d2;   // (16-B aligned: one ds_read_b128)
   const uint32_t rtb = (uint32_t)(uintptr_t)((lds_d2*)RT);   // Fst's reciprocals (LDS byte address)
-  const uint32_t atb = (uint32_t)(uintptr_t)((lds_d2*)AT);   // (a, a (a - 1)) as doubles
   // ---- batched finish.  Lane j of the B* registers holds the j-th window this wavefront has
   // scanned since the last flush (slot, SNP range, counts, the three sums); per window only the
   // sums' wave reductions run, and the T values, the zero / NaN rules, the Fst value and the 64-B
@@ -2809,14 +2807,26 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
             a1 = ok ? a1 : 0u;
             a2 = ok ? a2 : 0u;
           }
-          // (a and a (a - 1) as doubles from a table too: two conversions, a subtract and a multiply
-          // fewer per population in a VALU-heavy loop)
+          // (a and a (a - 1) converted here: an LDS table of them, two more LDS reads per SNP, made the
+          // pass slower -- 143 -> 158 us on config 3: the loop's LDS pipe is the busier one)
+#ifdef SFS2D_FST_VALU_RCP   // experiment: the reciprocals by v_rcp_f64 + one Newton step, no LDS reads
+          auto rcp2 = [](uint32_t n) {
+            const double nd = (double)max(n, 2u), md = fma(nd, nd, -nd);   // n (n - 1), exact
+            double x = __builtin_amdgcn_rcp(nd), y = __builtin_amdgcn_rcp(md);
+            x = fma(x, fma(-nd, x, 1.0), x);
+            y = fma(y, fma(-md, y, 1.0), y);
+            d2v r;
+            r.x = x;
+            r.y = y;
+            return r;
+          };
+          const d2v r1 = rcp2(n1c), r2 = rcp2(n2c);
+#else
           const d2v r1 = *(const lds_d2*)(uintptr_t)(rtb + 16u * n1c);
           const d2v r2 = *(const lds_d2*)(uintptr_t)(rtb + 16u * n2c);
-          const d2v x1 = *(const lds_d2*)(uintptr_t)(atb + 16u * a1);
-          const d2v x2 = *(const lds_d2*)(uintptr_t)(atb + 16u * a2);
-          fq[2 * q] = make_double2(x1.x * r1.x, x1.y * r1.y);
-          fq[2 * q + 1] = make_double2(x2.x * r2.x, x2.y * r2.y);
+#endif
+          fq[2 * q] = make_double2((double)a1 * r1.x, (double)__umul24(a1, a1 - 1u) * r1.y);
+          fq[2 * q + 1] = make_double2((double)a2 * r2.x, (double)__umul24(a2, a2 - 1u) * r2.y);
         }
       }
     };
