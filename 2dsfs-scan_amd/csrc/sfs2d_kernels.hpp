@@ -2862,21 +2862,8 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
         // every SNP slot adds to one bin of each folded 1D spectrum (no range test, no trash select: the
         // window's end drops bins 0 and n_p and counts n1a / n1b from them)
         const uint32_t u1 = a1b + (gp & 0xffffu), u2 = a2b + (gp >> 16);
-#ifdef SFS2D_1D_ALL_SLOTS   // (comparison build: the slots past the window's end counted in bin 0 too)
         __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u1, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u2, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
-        // the slots past the window's end (w = 0) would all add to bin 0 of their replica -- same-address
-        // atomics, serialised: a full row of them is ~16 extra LDS cycles per spectrum -- so a row that is
-        // not full counts only its live lanes, and a row wholly past the end nothing (uniform tests)
-        if (64 * (j + q + 1) <= (int)nsnp) {
-          __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u1, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u2, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else if (64 * (j + q) < lim) {
-          __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u1, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u2, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-#endif
       }
       if (FSTIN) {   // (SNPs past e: counts 0, no called allele, terms 0)
         // five fp64 operations per SNP on the table's (p, A) (computed from (1/n, 1/(n(n-1))) they took
@@ -2995,11 +2982,9 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     // spectrum: n1a / n1b = slots - bin 0 - bin n_p)
     double acca = 0.0, accb = 0.0;
     constexpr uint32_t S1 = P16 ? 16u : 0u;
-#ifdef SFS2D_1D_ALL_SLOTS
+    // (counting only the live slots -- a partial row's live lanes, no row past the end -- measured 1%
+    // slower: its uniform tests cost more than the same-address atomics of the padding)
     const uint32_t slots = 128u * ((nsnp + 127u) / 128u);
-#else
-    const uint32_t slots = nsnp;   // the SNP slots counted in the 1D spectra (the live ones)
-#endif
     if (half1d) {
       const bool pa = lane < 32;
       const int k = lane & 31, np = pa ? P.n1p : P.n2p;

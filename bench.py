@@ -43,6 +43,7 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
+SETTLE_S = 0.3          # untimed passes before each loop's warmup (the GPU's clock ramp; run_loop)
 POP = 25
 WS = 20000
 C3_NCHROM, C3_PER, C3_SEED = 32, 1_562_500, 777
@@ -278,6 +279,15 @@ def run_loop(cx, plans, steps, warmup, label):
 
     plans[0].run(optrs[0])
     plans[0].check()
+    # device settle (untimed): passes for SETTLE_S of wall time before the warmup, so that the timed
+    # steps run at the GPU's sustained clock rather than on its ramp out of idle (a 100-step timed loop
+    # is ~20 ms: measured 0.195 ms per step after 10 warmup passes, 0.181 after 600)
+    t_s = time.perf_counter()
+    settle = 0
+    while time.perf_counter() - t_s < SETTLE_S:
+        Plan.run_streams(plans, sstreams, 8 * ns, optrs)
+        torch.cuda.synchronize()
+        settle += 8 * ns
     Plan.run_streams(plans, sstreams, warmup * ns, optrs)
     gather_final(last, False)
     torch.cuda.synchronize()
@@ -309,7 +319,7 @@ def run_loop(cx, plans, steps, warmup, label):
     else:
         allr = mine
     return {"dt": dt, "device_ms": dev_ms, "gather_ms": gat_ms, "t_enq": t_enq, "rows": rows,
-            "gathered": allr, "mine": mine, "streams": ns}
+            "gathered": allr, "mine": mine, "streams": ns, "settle_passes": settle}
 
 
 def kernel_times(plan, runs=16):
@@ -388,6 +398,8 @@ def config3_strong(cx, args):
     out = {"value": total_windows * args.steps / r["dt"], "ms_per_step": step_s * 1e3,
            "host_enqueue_ms_per_step": r["t_enq"] / args.steps * 1e3,
            "device_ms_per_step": r["device_ms"] / args.steps, "gather_ms": r["gather_ms"],
+           "settle": {"seconds": SETTLE_S, "passes": r["settle_passes"],
+                      "note": "untimed passes before the warmup so that the timed steps run at the sustained clock"},
            "windows": total_windows, "snps": p.n, "cuts": cuts,
            "rank0": {"snps": sub.n, "windows": win_rank, "slots": nrec, "k_prep_ms": k1, "scan_ms": k3,
                      "scan_kernel": kname, "single_stream_pass_ms": one, "scan_grid_threads": grids[1]}}
@@ -499,7 +511,7 @@ def main():
                                       "overlapped" + ("; one RCCL all-gather of the final window tables in the "
                                                       "timed region" if world > 1 else "")},
             "host_enqueue_ms_per_step": c3["host_enqueue_ms_per_step"],
-            "device_ms_per_step": c3["device_ms_per_step"], "gather_ms": c3["gather_ms"],
+            "device_ms_per_step": c3["device_ms_per_step"], "gather_ms": c3["gather_ms"], "settle": c3["settle"],
             "rank0": r0,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "kernel": r0["scan_kernel"],
