@@ -293,6 +293,10 @@ def run_loop(cx, plans, steps, warmup, label):
     torch.cuda.synchronize()
     if cx.world > 1:
         dist.barrier()
+    # k_prep / scan-kernel durations over the timed steps themselves (start / end events in the
+    # kernels' dispatch packets, every pass of every plan): the overlapped launches the roofline prices
+    for q in plans:
+        q.set_timing(steps, every=1, kernels=5)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev[0].record(cx.scan_s)
@@ -303,6 +307,11 @@ def run_loop(cx, plans, steps, warmup, label):
     if cx.world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    kt = [q.timing_read() for q in plans]
+    for q in plans:
+        q.set_timing(0)
+    nk = sum(n for n, _ in kt)
+    k_timed = (sum(n * k[0] for n, k in kt) / max(1, nk), sum(n * k[2] for n, k in kt) / max(1, nk))
     dt = float(cx.max_over_ranks(dt))
     dev_ms = float(cx.max_over_ranks(float(ev[0].elapsed_time(ev[1]))))
     gat_ms = float(cx.max_over_ranks(float(ev[1].elapsed_time(ev[2]))))
@@ -319,7 +328,8 @@ def run_loop(cx, plans, steps, warmup, label):
     else:
         allr = mine
     return {"dt": dt, "device_ms": dev_ms, "gather_ms": gat_ms, "t_enq": t_enq, "rows": rows,
-            "gathered": allr, "mine": mine, "streams": ns, "settle_passes": settle}
+            "gathered": allr, "mine": mine, "streams": ns, "settle_passes": settle,
+            "k_timed_ms": k_timed, "k_timed_samples": nk}
 
 
 def kernel_times(plan, runs=16):
@@ -401,7 +411,9 @@ def config3_strong(cx, args):
            "settle": {"seconds": SETTLE_S, "passes": r["settle_passes"],
                       "note": "untimed passes before the warmup so that the timed steps run at the sustained clock"},
            "windows": total_windows, "snps": p.n, "cuts": cuts,
-           "rank0": {"snps": sub.n, "windows": win_rank, "slots": nrec, "k_prep_ms": k1, "scan_ms": k3,
+           "rank0": {"snps": sub.n, "windows": win_rank, "slots": nrec,
+                     "k_prep_ms": r["k_timed_ms"][0], "scan_ms": r["k_timed_ms"][1],
+                     "timed_samples": r["k_timed_samples"], "k_prep_alone_ms": k1, "scan_alone_ms": k3,
                      "scan_kernel": kname, "single_stream_pass_ms": one, "scan_grid_threads": grids[1]}}
     out.update(extra)
     return out, p
@@ -516,9 +528,10 @@ def main():
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "kernel": r0["scan_kernel"],
                          "ms": r0["scan_ms"], "algorithmic_bytes": b3,
-                         "note": r0["scan_kernel"] + " on rank 0's shard: 4 B/SNP + 96 B/slot per launch over its average duration "
-                                 "(kernel start/end events in the dispatch packets, 16 runs on one stream after the "
-                                 "timed loop); traffic: " + (tsrc or "no PMC pass committed")},
+                         "note": r0["scan_kernel"] + " on rank 0's shard: 4 B/SNP + 96 B/slot per launch over its average "
+                                 "duration in the timed steps (start / end events in the kernels' dispatch packets, "
+                                 "every pass of both plans, overlapped with the other stream's k_prep; alone on one "
+                                 "stream: rank0.scan_alone_ms); traffic: " + (tsrc or "no PMC pass committed")},
             "roofline_pipeline": {"bound": "hbm", "achieved": bp / step_s / 1e9, "peak": HBM_PEAK_GBS * world,
                                   "unit": "GB/s", "frac": bp / step_s / 1e9 / (HBM_PEAK_GBS * world),
                                   "note": "whole step over all GPUs (SURVEY 8(d): 12 B/SNP + 64 B/window) over "
