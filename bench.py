@@ -22,11 +22,14 @@ on 3 streams), the round-1..3 headline, with its own roofline and the single-str
 GPU) and exits with their status; under torchrun, WORLD_SIZE must equal N, and a box with fewer
 than N GPUs fails instead of reporting fewer.
 
+Each loop runs untimed passes for SETTLE_S of wall time before its W warmup steps (the GPU's clock
+ramp out of idle: a 100-step config-3 loop is ~20 ms), then times exactly K steps.
+
 Prints ONE JSON line on rank 0.  ``roofline``: the dominant kernel (k_scan_w) of the headline workload,
-algorithmic bytes per launch over its duration from HIP events in its dispatch packets in a
-single-stream pass after the timed loop (on the stream it runs on).  ``cpu_baseline``: the C oracle
-(the reference's dense per-window algorithm, OpenMP) on the box's host cores over a bounded sample of
-the same genome (its first chromosome).
+algorithmic bytes per launch over its average duration in the timed steps (HIP start / end events in
+its dispatch packets, every 4th pass of each plan, on the stream it runs on; its one-stream duration is
+rank0.scan_alone_ms).  ``cpu_baseline``: the C oracle (the reference's dense per-window algorithm,
+OpenMP) on the box's host cores over a bounded sample of the same genome (its first chromosome).
 """
 from __future__ import annotations
 
