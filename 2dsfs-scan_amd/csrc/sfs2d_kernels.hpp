@@ -2020,7 +2020,7 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
       if (FST && lane == 0) fst_out[s] = __builtin_nan("");
       Win nxt;
       nxt.has = false;
-      if (more) bounds(sn, srn, nxt);
+      if (more) bounds(sn, make_uint2(__builtin_amdgcn_readfirstlane(srn.x), __builtin_amdgcn_readfirstlane(srn.y)), nxt);
       cur = nxt;
       continue;
     }
@@ -2155,10 +2155,11 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
     if (FST && lane == 0) fq = reinterpret_cast<const ulonglong2*>(fsum)[s];
     const bool ov = !GL && nsnp > (uint32_t)(LNT - 1);   // some rank may have passed the D table (GL: ranks < 256)
     if (it == 0) STAMP(12);
-    // next window: its slot record is in, issue its first steps now
+    // next window: its slot record is in, issue its first steps now (the record made wave-uniform
+    // here: its load, issued at the window's start, was otherwise waited for right there)
     Win nxt;
     nxt.has = false;
-    if (more) bounds(sn, srn, nxt);
+    if (more) bounds(sn, make_uint2(__builtin_amdgcn_readfirstlane(srn.x), __builtin_amdgcn_readfirstlane(srn.y)), nxt);
     group_sync<WAVE>();
     // 1D spectra: one lane per folded inner bin reads (and clears) its R1 replicas; with <= 32 inner
     // bins per population, lanes 0-31 take population 1 and lanes 32-63 population 2 (acca)
