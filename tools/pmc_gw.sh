@@ -1,7 +1,7 @@
 #!/bin/bash
 # SQ counter passes over the large-grid scan (config 4 shape, 250 replicates generated on the device)
 # and over config 3 (k_scan_w), one counter group per run, kernel trace only.
-# usage: bash tools/pmc_gw.sh <tag>
+# usage: bash tools/pmc_gw.sh <tag> [4]   (4: the config-4 passes only)
 set -o pipefail
 TAG=${1:-gw}
 export TMPDIR=/tmp
@@ -16,8 +16,10 @@ O4=gpurun_out/$TAG/pmc_config4
 O3=gpurun_out/$TAG/pmc_config3
 PMC=$P1 run $O4 p1 python3 tools/sims_config4.py 250 1 3 &&
 PMC=$P2 run $O4 p2 python3 tools/sims_config4.py 250 1 3 &&
+PMC=FETCH_SIZE run $O4 p3 python3 tools/sims_config4.py 250 1 3 &&
+python3 tools/pmc_summary.py $O4 > gpurun_out/$TAG/pmc_config4.csv &&
+if [ "$2" = 4 ]; then echo "rc=0"; exit 0; fi &&
 PMC=$P1 run $O3 p1 python3 tools/profile_scan.py config3 3 fst &&
 PMC=$P2 run $O3 p2 python3 tools/profile_scan.py config3 3 fst &&
-python3 tools/pmc_summary.py $O4 > gpurun_out/$TAG/pmc_config4.csv &&
 python3 tools/pmc_summary.py $O3 > gpurun_out/$TAG/pmc_config3.csv
 echo "rc=$?"
