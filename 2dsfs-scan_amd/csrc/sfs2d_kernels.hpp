@@ -1989,7 +1989,7 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
       for (int c = tid; c < P.nchrom; c += SBLOCK) bcount[(size_t)(1 - par) * P.nchrom + c] = 0u;
   }
   if (!active) return;
-  const double Dreg = GL ? dfg[lane] : 0.0;     // GL: D(lane)
+  const double Dreg = (GL && lane < 63) ? dfg[lane] : 0.0;   // GL: D(lane), lane 63: 0 (ranks from 63 on)
   constexpr bool P16H = P16 && !GL;               // u16-packed 2D bins (GL: u8)
   const uint32_t one1 = P16H ? 0x10000u : 1u;   // 1D increment (P16: counts in the upper halves)
   uint32_t* const H1a_l = H1a + rep;            // this lane's replica column of the 1D histograms
@@ -2035,13 +2035,18 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
     double acc2 = 0.0;
     uint32_t n2 = 0, nlast = 0, n1a = 0, n1b = 0, nvar = 0;
     bool ovf = false;   // GL: some u8 bin of this lane wrapped
-    uint32_t kw[8];   // the 2D words of the first 8 steps, cleared after the window
+    bool big = false;   // GL: some bin of this lane passed rank 63 (its later ranks added 0; see below)
+    // the 2D words of the last 8 steps (a shift register: computed values, no loads, so its moves never
+    // wait), cleared after a window of <= 6 steps; initially the lane's trash word
+    uint32_t kw[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) kw[j] = trash;
     // A pair of rows in two halves, software-pipelined as in k_scan_w: issue() classifies, issues the
     // LDS atomics and (GL) the lp loads from the global table; finish() turns the returned ranks and lp
     // into D(r) - lp_k.  The loops issue pair j before they finish pair j - 2: a pair's atomics and its
     // L2 round trip for lp return under the next pair's work.
     struct PairSt { uint32_t ov[2], xs[2], kk[2]; double lp[2]; };
-    auto issue = [&](uint32_t w0, uint32_t w1, int j, bool keep) {
+    auto issue = [&](uint32_t w0, uint32_t w1, int j) {
       PairSt st;
       // SNPs past e are excluded (unconditional: cheaper than a guard; CNT: the window-ranged loads
       // returned 0 there)
@@ -2059,7 +2064,10 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
         n2 += 64u - (uint32_t)__popcll(__ballot(k2 == 0u));   // (the compare the selects below use)
         n1a += __popcll(__ballot(g1 != 0u));
         n1b += __popcll(__ballot(g2 != 0u));
-        if (GL) st.lp[q] = LPl[k2];   // (the global table; bin 0 is not zeroed there: finish selects 0)
+        // (the global table, whose bin 0 is not zeroed: excluded SNPs read D's last entry, 0, instead --
+        // an address select here, not a select of the loaded value in finish(), which the scheduler
+        // hoisted next to the load and so waited for the gather on the spot)
+        if (GL) st.lp[q] = *(k2 ? LPl + k2 : Dt + (LNT - 1));
         const uint32_t word = k2 ? (GL ? (k2 >> 2) : P16 ? (k2 >> 1) : k2) : trash;
         // the byte / half's shift: the hardware reads shift operands' low five bits, so k2 << 3 (GL)
         // or k2 << 4 serves without a mask (the bins word's low bits are k2's)
@@ -2070,76 +2078,73 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
         st.ov[q] = atomicAdd(&W[word], k2 ? one2 : 0u);
         st.xs[q] = sh;
         st.kk[q] = k2;
-        if (keep) kw[(j + q) & 7] = word;
+        kw[q] = kw[q + 2]; kw[q + 2] = kw[q + 4]; kw[q + 4] = kw[q + 6]; kw[q + 6] = word;
         const uint32_t u1 = g1 ? a1b + g1 * (4u * RG) : atr, u2 = g2 ? a2b + g2 * (4u * RG) : atr;
         __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u1, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u2, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       return st;
     };
-    auto finish = [&](const PairSt& st) {
-      uint32_t rk[2];
+    // dlook(): the pair's D(r) look-ups, issued as soon as its ranks are in (GL: lane shuffles, before
+    // the next pair's atomics, so that waiting for them is not waiting for those too -- LDS operations
+    // complete in order); finish(): D(r) - lp_k into the sum
+    auto dlook = [&](const PairSt& st, double (&d)[2]) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         if (GL) {   // (the trash word's low byte counts 1D increments: excluded SNPs take rank 0)
           const uint32_t r = __builtin_amdgcn_ubfe(st.ov[q], st.xs[q], 8);
-          rk[q] = st.kk[q] ? r : 0u;
+          const uint32_t rk = st.kk[q] ? r : 0u;
           ovf |= (st.kk[q] != 0u) & (r == 255u);
+          // D(r) for r < 63 from the lanes' registers, lane 63 holding 0: ranks from 63 on add 0 here and
+          // the window's end adds F(x) - F(63) for each bin past 63 (a global read of D for them, even
+          // in a branch never taken, put a wait for every outstanding load -- the next pair's lp gathers
+          // and rows -- into every pair; config 4's bins never pass ~20 SNPs)
+          d[q] = __shfl(Dreg, (int)min(rk, 63u));
+          big |= rk >= 63u;
         } else {
-          rk[q] = P16 ? __builtin_amdgcn_ubfe(st.ov[q], st.xs[q], 16) : (st.kk[q] ? st.ov[q] : 0u);
+          const uint32_t rk = P16 ? __builtin_amdgcn_ubfe(st.ov[q], st.xs[q], 16) : (st.kk[q] ? st.ov[q] : 0u);
+          d[q] = Dt[min(rk, (uint32_t)LNT - 1u)];   // D[LNT-1] = 0: ranks past the table add 0
         }
       }
-      double d[2], lp[2];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        if (GL) {   // D(r) for r < 64 from the lanes' registers, the global table beyond
-          d[q] = __shfl(Dreg, (int)(rk[q] & 63u));
-          if (rk[q] >= 64u) d[q] = Dt[min(rk[q], (uint32_t)LNT - 1u)];
-          lp[q] = st.kk[q] ? st.lp[q] : 0.0;
-        } else {
-          d[q] = Dt[min(rk[q], (uint32_t)LNT - 1u)];   // D[LNT-1] = 0: ranks past the table add 0
-          lp[q] = LPl[st.kk[q]];
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 2; ++q) acc2 += d[q] - lp[q];
     };
-    PairSt pend;   // the issued pair not yet finished (every window has >= 1 SNP: pair 0 runs)
+    auto finish = [&](const PairSt& st, const double (&d)[2]) {
 #pragma unroll
-    for (int j = 0; j < 8; j += 2)
-      if (64 * j < (int)nsnp) {
-        const PairSt st = issue(cur.u[j], cur.u[j + 1], j, true);
-        if (j > 0) finish(pend);
-        pend = st;
-      }
-    if (nsnp > 8 * WAVE) {
-      if (CNT) {   // buffer loads (range-checked), rows masked in pair()
-        const __amdgpu_buffer_rsrc_t rr = window_rows(bins, cur.b, cur.e, P.nm1);
-        int vo = lane * 4 + 256 * 8;
-        uint32_t x0 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo, 0, 0), x1 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo + 256, 0, 0);
-        for (int j = 8; 64 * j < (int)nsnp; j += 2) {
-          const uint32_t w0 = x0, w1 = x1;
-          vo += 512;
-          x0 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo, 0, 0);   // one pair ahead
-          x1 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo + 256, 0, 0);
-          const PairSt st = issue(w0, w1, j, false);
-          finish(pend);
-          pend = st;
-        }
-      } else {
-        const uint32_t* qb = bins + cur.b + lane;
-        uint32_t x0 = 64 * 8 < lim ? qb[64 * 8] : 0u, x1 = 64 * 9 < lim ? qb[64 * 9] : 0u;
-        for (int j = 8; 64 * j < (int)nsnp; j += 2) {
-          const uint32_t w0 = x0, w1 = x1;
-          x0 = 64 * (j + 2) < lim ? qb[64 * (j + 2)] : 0u;   // one pair ahead
-          x1 = 64 * (j + 3) < lim ? qb[64 * (j + 3)] : 0u;
-          const PairSt st = issue(w0, w1, j, false);
-          finish(pend);
-          pend = st;
-        }
-      }
+      for (int q = 0; q < 2; ++q) acc2 += d[q] - (GL ? st.lp[q] : LPl[st.kk[q]]);
+    };
+    // The pairs as a rolled loop, two per trip in fixed slots A / B (a pending pair carried through a
+    // branch join is copied there, and a copy of registers with loads in flight waits for them: unrolled
+    // with the window's length tests, every pair waited for the lp gathers it had just issued -- an L2
+    // round trip per pair).  Pair 0 first, then trips of two: the pair count is rounded up to odd (a
+    // padding pair's rows are past the window's end, zeros: excluded SNPs).  Rows are buffer loads
+    // (range-checked: 0 past the end), two pairs ahead; pairs 0-2 came with the window (bounds()).
+    const __amdgpu_buffer_rsrc_t rr = window_rows(bins, cur.b, cur.e, P.nm1);
+    uint32_t ro = (uint32_t)lane * 4u;
+    asm volatile("" : "+v"(ro));   // (one base + the loads' immediate offsets)
+    auto row = [&](int r) -> uint32_t { return __builtin_amdgcn_raw_buffer_load_b32(rr, (int)ro + 256 * r, 0, 0); };
+    const int npair = (((int)nsnp + 2 * WAVE - 1) / (2 * WAVE)) | 1;
+    PairSt B = issue(cur.u[0], cur.u[1], 0);
+    double dB[2], dA[2];
+    dlook(B, dB);
+    uint32_t x0 = cur.u[2], x1 = cur.u[3], y0 = cur.u[4], y1 = cur.u[5];
+    // (scheduling barriers keep each pair's finish after the next pair's issue: hoisted to the loop's
+    // top, it waited there for everything in flight)
+    for (int p = 1; p < npair; p += 2) {
+      const PairSt A = issue(x0, x1, 2 * p);
+      x0 = row(2 * p + 4);
+      x1 = row(2 * p + 5);
+      __builtin_amdgcn_sched_barrier(0);
+      finish(B, dB);
+      dlook(A, dA);
+      __builtin_amdgcn_sched_barrier(0);
+      B = issue(y0, y1, 2 * p + 2);
+      y0 = row(2 * p + 6);
+      y1 = row(2 * p + 7);
+      __builtin_amdgcn_sched_barrier(0);
+      finish(A, dA);
+      dlook(B, dB);
+      __builtin_amdgcn_sched_barrier(0);
     }
-    finish(pend);
+    finish(B, dB);
     if (!P.fold || filt) {   // rare settings: unfolded (SNPs in the excluded last 2D bin), variant_type filter
       for (uint32_t i0 = cur.b; i0 < cur.e; i0 += WAVE) {   // wave-uniform trip count
         const uint32_t w = i0 + lane < cur.e ? snp_word<CNT>(P, bins, i0 + lane) : 0u;
@@ -2185,6 +2190,19 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
         accb += x ? xlnx(x, Ft, lnx) - (double)x * LPl[P.t1b + k] : 0.0;
       }
     }
+    // GL: bins with x > 63 SNPs (u8: x <= 254, or the window is re-evaluated exactly below) add
+    // F(x) - F(63) (read before the clear)
+    if (GL && __ballot(big) != 0ull) {
+      const double f63 = Ft[63];
+      for (int k = lane; k < h2w; k += WAVE) {
+        const uint32_t v = W[k];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const uint32_t x = (v >> (8 * b)) & 0xffu;
+          if (x > 63u) acc2 += xlnx(x, Ft, lnx) - f63;
+        }
+      }
+    }
     // bins with x > LNT-1 SNPs: the ranks from LNT-1 on add F(x) - F(LNT-1) (read before the clear)
     if (ov) {
       constexpr uint32_t L1 = LNT - 1;
@@ -2196,11 +2214,10 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
         if (xb > L1) acc2 += (double)xb * lnx_of(lnx, xb) - fl;
       }
     }
-    // clear the 2D words this window touched
-    if (nsnp <= 8 * WAVE) {
+    // clear the 2D words this window touched (<= 6 steps: all in kw, with trash words)
+    if (nsnp <= 6 * WAVE) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (64 * j < (int)nsnp) W[kw[j]] = 0u;
+      for (int j = 0; j < 8; ++j) W[kw[j]] = 0u;
     } else {
       uint4* q = reinterpret_cast<uint4*>(W);
       for (int k = lane; k < h2w / 4; k += WAVE) q[k] = make_uint4(0, 0, 0, 0);

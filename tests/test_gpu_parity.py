@@ -505,6 +505,33 @@ def test_large_grid_u8_bins_wrap(n1p, n2p):
                            lambda c: bgs[c])
 
 
+@pytest.mark.parametrize("n1p,n2p", [(50, 50), (100, 75)])
+def test_large_grid_bins_past_63(n1p, n2p):
+    """k_scan_gw takes D(r) for ranks r < 63 from lane shuffles and adds F(x) - F(63) at the window's
+    end for each bin holding x > 63 SNPs (no wrap: x < 255): windows with one bin holding ~50 to ~100
+    SNPs (every 4th / 6th / 7th SNP forced into one bin), fixed-bp and SNP-count windows, against the
+    oracle."""
+    from sfs2d import _lib as L
+    from sfs2d.engine import ScanConfig
+    from sfs2d.pack import PackedSNPs, pack_counts
+    from sfs2d.synth import synth_genome
+    p = synth_genome(3, [6000, 3000, 2500], n1p, n2p, seed=63)
+    r1, a1 = (p.counts & 0xff).astype(np.int64), ((p.counts >> 8) & 0xff).astype(np.int64)
+    r2, a2 = ((p.counts >> 16) & 0xff).astype(np.int64), (p.counts >> 24).astype(np.int64)
+    i = np.arange(p.n)
+    c = np.searchsorted(p.chrom_off, i, side="right") - 1
+    same = (i - p.chrom_off[c]) % np.array([4, 6, 7])[c] == 0
+    r1 = np.where(same, 2 * n1p - 3, r1); a1 = np.where(same, 3, a1)
+    r2 = np.where(same, 2 * n2p - 1, r2); a2 = np.where(same, 1, a2)
+    q = PackedSNPs(pack_counts(r1, a1, r2, a2), p.pos, p.chrom_off, p.chrom_names, p.ann_id, p.ann_names)
+    ocfg = O.Cfg(n1p, n2p)
+    bgs = O.chrom_backgrounds(q, ocfg)
+    for mode, ws in ((L.WINDOW_BP, 20000), (L.WINDOW_SNPS, 400)):
+        wins = O.snp_windows(q, ws)[0] if mode == L.WINDOW_SNPS else O.bp_windows(q, ws)
+        _records_vs_oracle(q, ScanConfig(n1p=n1p, n2p=n2p, window_mode=mode, window=ws), ocfg, wins,
+                           lambda c: bgs[c])
+
+
 @pytest.mark.parametrize("gw", ["0", "1"])
 def test_largest_grid(monkeypatch, gw):
     """The largest grid the u8 allele counts allow (pop_size 127: 255 x 255 = 65,025 bins, 16-bit 2D
