@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Diagnostic: per-phase wall-clock stamps of block 0 of each kernel (needs libsfs2d_stamps.so,
-built with -DSFS2D_STAMPS).  usage: SFS2D_LIB=.../libsfs2d_stamps.so python tools/stamps.py config2"""
+built with -DSFS2D_STAMPS).  usage: SFS2D_LIB=.../libsfs2d_stamps.so python tools/stamps.py config2|config3 [chromosomes]|config5"""
 import ctypes as C
 import numpy as np
 import os
@@ -17,8 +17,9 @@ if which == "config5":   # 201 x 151 grid, 500-SNP windows (large-grid kernels, 
     p = synth_genome(1, 1_000_000, 100, 75, seed=55)
     cfg = ScanConfig(n1p=100, n2p=75, window_mode=L.WINDOW_SNPS, window=500)
 else:
-    p = synth_genome(1 if which == "config2" else 32, 1_000_000 if which == "config2" else 1_562_500, 25, 25, seed=1)
-    cfg = ScanConfig(n1p=25, n2p=25, window=20000, fst=True)
+    nch = int(sys.argv[2]) if len(sys.argv) > 2 else 32   # config3 [chromosomes]: a rank's share
+    p = synth_genome(1 if which == "config2" else nch, 1_000_000 if which == "config2" else 1_562_500, 25, 25, seed=1)
+    cfg = ScanConfig(n1p=25, n2p=25, window=20000, fst=True, scan_wgs_per_cu=1 if which == "config3" else 0)
 eng = Engine.get(0)
 dev = eng.upload(p)
 pl = eng.plan(dev, cfg)
@@ -71,6 +72,7 @@ print(which, f"k_scan_w waves: {live.sum()}  windows/wave min/med/max {w[live,1]
       f"  end min/med/max {en[live].min():.1f}/{np.median(en[live]):.1f}/{en[live].max():.1f} us")
 if which != "config2":
     # workgroups are interleaved over the grid: block b scans chromosome b % 32 (equal chromosomes)
-    chrom = (np.arange(nb * 8) // 8) % 32
-    ce = [(en[chrom == c].min(), en[chrom == c].max(), int(w[chrom == c, 1].sum())) for c in range(32)]
+    nc = 32 if which == "config5" else nch
+    chrom = (np.arange(nb * 8) // 8) % nc
+    ce = [(en[chrom == c].min(), en[chrom == c].max(), int(w[chrom == c, 1].sum())) for c in range(nc)]
     print(which, "per chromosome end min-max / windows:", " ".join(f"{a:.0f}-{b:.0f}/{n}" for a, b, n in ce))
