@@ -17,6 +17,7 @@ helper record.
 """
 from __future__ import annotations
 
+import contextlib
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -248,6 +249,25 @@ def _all_gather_dev(out, world):
     return g.cpu().numpy()
 
 
+@contextlib.contextmanager
+def _one_stream(eng, dev):
+    """torch's ops on the exchange buffers, the collectives and the library's kernels ordered on ONE
+    stream: a fresh (non-null) torch stream made current and handed to the library.  (Handing it torch's
+    default stream does not work: its handle is 0, and NULL selects the library's own non-blocking
+    stream, which nothing orders against the default stream -- the kernels could read an exchange buffer
+    before its zero fill or its all-reduced copy had landed.)"""
+    import torch
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        eng.set_stream(s.cuda_stream)
+        try:
+            yield s
+        finally:
+            s.synchronize()
+            eng.set_stream(None)
+
+
 def _split_device(p, cfg, bg, split_scan, device, cuts, c0s, sub, c0, rank, world, last):
     """scan_records_split for jobs that exchange in HBM (engine.SplitJob).  Two collectives per scan,
     both on device buffers: ONE all-reduce of [every chromosome's background rows | per rank: failed,
@@ -264,44 +284,42 @@ def _split_device(p, cfg, bg, split_scan, device, cuts, c0s, sub, c0, rank, worl
     W = hist_width(cfg)
     H = p.nchrom * W
     lo, hi = cuts[rank], cuts[rank + 1]
-    eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)   # kernels ordered with torch's / RCCL's ops
     job = None
-    try:
-        buf = torch.zeros(H + 2 * world, dtype=torch.int64, device=dev)
-        err, nrec = None, 0
-        if hi > lo:
-            try:
-                job = split_scan(sub, dataclasses.replace(cfg, prev_extra=bool(cfg.prev_extra) and rank == last), bg)
-                nrec = job.rows()
-                if W:
-                    job.partial_dev(buf.data_ptr() + 8 * c0 * W, W)
-            except Exception as e:  # noqa: BLE001  (every rank takes the fallback)
-                err = e
-        buf[H + 2 * rank] = 1 if err is not None else 0
-        buf[H + 2 * rank + 1] = nrec
-        _all_reduce_dev(buf)
-        STATS["allreduce"] += 1 if W else 0
-        tail = buf[H:].cpu().numpy().reshape(world, 2)
-        if tail[:, 0].any():
-            return None
-        rows = int(tail[:, 1].max())
-        out = torch.zeros((rows + 1, 64), dtype=torch.uint8, device=dev)   # + this rank's status row
-        if job is not None:
-            try:
-                job.finish_dev(buf.data_ptr() + 8 * c0 * W if W else None, W, out.data_ptr())
-            except Exception:  # noqa: BLE001
-                out[rows, 0] = 1
-        g = _all_gather_dev(out, world).reshape(world, rows + 1, 64)
-        if g[:, rows, 0].any():
-            return None
-        tables = [np.ascontiguousarray(g[r, : int(tail[r, 1])]).view(L.WINDOW_DTYPE).reshape(-1) for r in range(world)]
-        return _merge_split(tables, cuts, c0s, bool(cfg.prev_extra),
-                            int(cfg.window) if cfg.window_mode == L.WINDOW_SNPS else 0, p.chrom_off)
-    finally:
-        if job is not None:
-            job.close()
-        torch.cuda.current_stream(dev).synchronize()
-        eng.set_stream(None)
+    with _one_stream(eng, dev):   # kernels ordered with torch's / RCCL's ops
+        try:
+            buf = torch.zeros(H + 2 * world, dtype=torch.int64, device=dev)
+            err, nrec = None, 0
+            if hi > lo:
+                try:
+                    job = split_scan(sub, dataclasses.replace(cfg, prev_extra=bool(cfg.prev_extra) and rank == last), bg)
+                    nrec = job.rows()
+                    if W:
+                        job.partial_dev(buf.data_ptr() + 8 * c0 * W, W)
+                except Exception as e:  # noqa: BLE001  (every rank takes the fallback)
+                    err = e
+            buf[H + 2 * rank] = 1 if err is not None else 0
+            buf[H + 2 * rank + 1] = nrec
+            _all_reduce_dev(buf)
+            STATS["allreduce"] += 1 if W else 0
+            tail = buf[H:].cpu().numpy().reshape(world, 2)
+            if tail[:, 0].any():
+                return None
+            rows = int(tail[:, 1].max())
+            out = torch.zeros((rows + 1, 64), dtype=torch.uint8, device=dev)   # + this rank's status row
+            if job is not None:
+                try:
+                    job.finish_dev(buf.data_ptr() + 8 * c0 * W if W else None, W, out.data_ptr())
+                except Exception:  # noqa: BLE001
+                    out[rows, 0] = 1
+            g = _all_gather_dev(out, world).reshape(world, rows + 1, 64)
+            if g[:, rows, 0].any():
+                return None
+            tables = [np.ascontiguousarray(g[r, : int(tail[r, 1])]).view(L.WINDOW_DTYPE).reshape(-1) for r in range(world)]
+            return _merge_split(tables, cuts, c0s, bool(cfg.prev_extra),
+                                int(cfg.window) if cfg.window_mode == L.WINDOW_SNPS else 0, p.chrom_off)
+        finally:
+            if job is not None:
+                job.close()
 
 
 def _rows_on_device(split_scan) -> bool:
@@ -406,19 +424,18 @@ def sharded_bg_hist(p, cfg, device: int = 0, chrom: int = -1):
     if b > a:
         sub, _ = p.slice_snps(a, b)
         eng = Engine.get(device)
-        eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-        d = eng.upload(sub)
-        try:
-            eng.bg_hist_dev(d, cfg, -1, buf.data_ptr())
-        except KeyError:
-            code = 1
-        except L.Sfs2dError as e:
-            if e.code != L.E_GRID:
-                raise
-            code = 2
-        finally:
-            d.close()
-            eng.set_stream(None)
+        with _one_stream(eng, dev):   # the histogram kernels ordered after buf's zero fill
+            d = eng.upload(sub)
+            try:
+                eng.bg_hist_dev(d, cfg, -1, buf.data_ptr())
+            except KeyError:
+                code = 1
+            except L.Sfs2dError as e:
+                if e.code != L.E_GRID:
+                    raise
+                code = 2
+            finally:
+                d.close()
     buf[W + rank] = code
     _all_reduce_dev(buf)
     h = buf.cpu().numpy()
