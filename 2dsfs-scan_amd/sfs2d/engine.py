@@ -75,6 +75,12 @@ class Engine:
             raise L.Sfs2dError(rc, msg)
 
     def set_stream(self, stream_handle: Optional[int]):
+        """Enqueue the library's work on the HIP stream ``stream_handle`` (None: the ctx's own stream).
+        Handle 0 -- torch's default stream -- is refused: the C API reads NULL as the ctx's own
+        non-blocking stream, which would silently not be ordered with the caller's work (share a
+        ``torch.cuda.Stream`` instead)."""
+        if stream_handle is not None and int(stream_handle) == 0:
+            raise ValueError("stream handle 0 (the default stream) cannot be shared; pass a torch.cuda.Stream's handle")
         self.check(self.lib.sfs2d_ctx_set_stream(self.h, C.c_void_p(stream_handle) if stream_handle else None))
 
     def upload(self, p: PackedSNPs) -> "DeviceData":
