@@ -184,6 +184,9 @@ def end_to_end(n_rec=1_000_000, nchrom=8, seed=3):
                         "script's three scans) from the file on disk to the three CSVs written, second run"}
 
 
+SHARED_GPU = os.environ.get("SFS2D_BENCH_SHARED_GPU") == "1"
+
+
 def launch_ranks(n):
     """``--gpus N`` with no launcher around this process: start N rank processes of this script
     (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rendezvous on 127.0.0.1) before this process
@@ -224,6 +227,7 @@ class Ctx:
         from sfs2d.engine import Engine
         self.torch, self.dist = torch, dist
         self.world, self.rank, self.local = world, rank, local
+        self.shared = SHARED_GPU and world > 1   # rehearsal: all ranks on GPU 0, gloo (see main)
         self.cdev = f"cuda:{local}"
         self.eng = Engine.get(local)
         self.scan_s = torch.cuda.Stream(device=local)   # the HIP library's stream (and the final gather's)
@@ -239,7 +243,8 @@ class Ctx:
         if self.world == 1:
             return x
         torch = self.torch
-        t = torch.tensor([x], dtype=dtype or (torch.float64 if isinstance(x, float) else torch.int64), device=self.cdev)
+        t = torch.tensor([x], dtype=dtype or (torch.float64 if isinstance(x, float) else torch.int64),
+                         device="cpu" if self.shared else self.cdev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return t.item()
 
@@ -275,7 +280,12 @@ def run_loop(cx, plans, steps, warmup, label, time_kernels=False):
             cx.scan_s.wait_event(e)
         if timed:
             ev[1].record(cx.scan_s)
-        if cx.world > 1:
+        if cx.world > 1 and cx.shared:
+            # SFS2D_BENCH_SHARED_GPU (a rehearsal of N > 1 with every rank on one GPU, gloo): host-staged
+            parts = [torch.empty_like(outs[k], device="cpu") for _ in range(cx.world)]
+            dist.all_gather(parts, outs[k].cpu())
+            gathered.copy_(torch.cat(parts).to(cx.cdev))
+        elif cx.world > 1:
             dist.all_gather_into_tensor(gathered, outs[k])
         if timed:
             ev[2].record(cx.scan_s)
@@ -494,13 +504,15 @@ def main():
     import torch.distributed as dist
 
     ndev = torch.cuda.device_count()
-    if ndev < world or local >= ndev:
+    if SHARED_GPU:
+        local = 0   # rehearsal of the N > 1 code path on a one-GPU box: not a scaling measurement
+    elif ndev < world or local >= ndev:
         raise RuntimeError(f"bench.py --gpus {world}: rank {rank} needs device {local}, {ndev} visible")
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
-        dist.init_process_group("nccl", rank=rank, world_size=world)
+        dist.init_process_group("gloo" if SHARED_GPU else "nccl", rank=rank, world_size=world)
         world = dist.get_world_size()   # n_gpus from the communicator
     cx = Ctx(world, rank, local, max(2, args.streams))
 
@@ -552,6 +564,8 @@ def main():
             line["cpu_baseline"] = cpu_baseline(genome.subset_chroms([0]))
         if not args.no_e2e and world == 1:
             line["end_to_end_vcf_csv"] = end_to_end()
+        if SHARED_GPU and world > 1:
+            line["shared_gpu_rehearsal"] = "SFS2D_BENCH_SHARED_GPU: every rank on GPU 0 over gloo -- a code-path check, not a measurement"
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
