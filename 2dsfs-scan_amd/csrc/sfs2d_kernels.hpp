@@ -1841,29 +1841,25 @@ __device__ __forceinline__ void fused_table(int nb2, int nh, int nt, int n1p, in
 
 __device__ __forceinline__ void wave_sum3(double a, double b, double c, double& sa, double& sb, double& sc);
 
-template <bool P16, bool FUSED, bool FST, bool GL, bool CNT>
-__device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
-  static_assert(!(GL && FUSED), "k_scan_gw reads finished tables");
-  constexpr int NT = GL ? WAVE : SBLOCK;   // threads per workgroup
-  __shared__ BgHead sh_hb;
+template <bool P16, bool FST, bool CNT>
+__device__ __forceinline__ void scan_gw_body(double* ldsd, SCAN_W_ARGS) {
   STAMP(10);
   BLK_STAMP(1, 0);
   const int tid = threadIdx.x;
-  const int wv = GL ? 0 : __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & (WAVE - 1);
   const Chunk ch = chunks[blockIdx.x];
   const int bg = bg_per_chrom ? (int)ch.chrom : 0;
 
-  // LDS (!GL): lp table (nt, rounded up to even: the histograms are 16-B aligned) | D | F | histograms
-  double* LPl = GL ? LPg + (size_t)bg * P.nt : ldsd;
-  double* Dt = GL ? const_cast<double*>(dfg) : LPl + ((P.nt + 1) & ~1);   // LNT
-  double* Ft = Dt + LNT;                                                   // LNT
-  uint32_t* HB = GL ? reinterpret_cast<uint32_t*>(ldsd) : reinterpret_cast<uint32_t*>(Ft + LNT);
-  const int h2w = GL ? ((P.nb2 + 3) / 4 + 3) & ~3 : P16 ? ((P.nb2 + 1) / 2 + 3) & ~3 : (P.nb2 + 3) & ~3;
-  constexpr int RG = GL ? R1GW : R1;   // 1D replicas
+  // the tables in global memory (L2-resident): the background's lp table, D and F; LDS holds the wave's
+  // histograms only: u8-packed 2D bins | RG x folded pop-1 1D | RG x pop-2 1D | 64 lane trash words
+  const double* LPl = LPg + (size_t)bg * P.nt;
+  const double* Dt = dfg;       // LNT
+  const double* Ft = Dt + LNT;  // LNT
+  const int h2w = ((P.nb2 + 3) / 4 + 3) & ~3;
+  constexpr int RG = R1GW;   // 1D replicas
   const int h1w = RG * (P.n1p + 1), h1wb = RG * (P.n2p + 1);
   const int per = h2w + h1w + h1wb + TRASH;
-  uint32_t* W = HB + wv * per;
+  uint32_t* W = reinterpret_cast<uint32_t*>(ldsd);
   uint32_t* H1a = W + h2w;
   uint32_t* H1b = H1a + h1w;
   const uint32_t trash = (uint32_t)(h2w + h1w + h1wb + lane);   // word offset from W
@@ -1898,7 +1894,7 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
   };
   // window schedule: one static window per wavefront, then the chromosome's pool counters (an
   // atomic is always one window ahead of its use, so its latency hides under a window's work)
-  uint32_t s = ch.slot_lo + ch.first + wv;
+  uint32_t s = ch.slot_lo + ch.first;
   const bool active = s < ch.slot_hi;
   const uint2 sr0 = (active && mode_bp) ? slots[s] : make_uint2(0, 0);   // in flight during the table work
   const uint32_t npool = ch.pool & 0xffffu, pool = ch.pool >> 16;
@@ -1908,90 +1904,19 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
   uint32_t gq = 0;
   if (active && dyn && lane == 0) gq = atomicAdd(myctr, 1u);
   if (blockIdx.x == 0)   // the other parity's counters, for the next run
-    for (int k = tid; k < P.nchrom * CTR_POOLS; k += NT) ctr[((size_t)(1 - cpar) * P.nchrom * CTR_POOLS + k) * CTR_STRIDE] = 0u;
+    for (int k = tid; k < P.nchrom * CTR_POOLS; k += WAVE) ctr[((size_t)(1 - cpar) * P.nchrom * CTR_POOLS + k) * CTR_STRIDE] = 0u;
 
-  if (!GL)
-    for (int k = tid; k < 2 * LNT; k += SBLOCK) Dt[k] = dfg[k];
-  BgHead hb;
-  const size_t rs = (size_t)P.nchrom * P.nh;     // replica stride
-  const uint32_t* Rc = repl + (size_t)par * REPL * rs + (size_t)ch.chrom * P.nh;
-  if (GL) {
-    hb = head[bg];
-  } else if (!FUSED) {
-    const double* LP = LPg + (size_t)bg * P.nt;
-    for (int k = tid; k < P.nt; k += SBLOCK) LPl[k] = LP[k];
-    if (sliced) {
-      // this run's per-chromosome table from k_bg_slice (proportions, logs, 1D part final) and its
-      // leaf sums: numpy's tree over the leaves, then scipy's p[-1] rule on the 2D table -- the
-      // combination k_bg_slice's last block would do, here in every workgroup (no grid-wide
-      // completion step between the kernels).  Scratch: the histogram area (zeroed below).
-      const bool writer = ch.first == 0 && (int)ch.chrom == write_chrom;
-      double* lsum = reinterpret_cast<double*>(HB);
-      if (tid < nleaves) lsum[tid] = leafsum[(size_t)bg * nleaves + tid];
-      const int4 my_node = tid < nnodes ? nodes[tid] : make_int4(0, 0, -1, 0);
-      __syncthreads();
-      for (int l = 0; l < nlevels; ++l) {
-        if (my_node.z == l) lsum[nleaves + tid] = lsum[my_node.x] + lsum[my_node.y];
-        __syncthreads();
-      }
-      if (tid == 0) {
-        const double B2 = (double)bcount[(size_t)par * P.nchrom + bg];
-        const Bg1D o = bg1d[bg];
-        uint32_t flags = o.flags;
-        if (B2 == 0.0) flags |= BGF_B2_ZERO;
-        const int M2 = P.nb2 - 2;
-        if (M2 >= 1 && B2 != 0.0) {
-          const double S = (nleaves + nnodes) ? lsum[nleaves + nnodes - 1] : 0.0;
-          const double padj = 1.0 - S;
-          if (padj < -1e-15) {
-            flags |= BGF_NAN2;
-          } else if (fabs(padj) > 1e-15) {
-            const double l2 = log(padj);
-            LPl[M2] = l2;
-            if (writer) { tab[(size_t)bg * P.nt + M2].lp = l2; LPg[(size_t)bg * P.nt + M2] = l2; }
-          }
-        }
-        BgHead h;
-        h.B2 = B2; h.B1a = o.B1a; h.B1b = o.B1b; h.flags = flags; h.pad = 0;
-        sh_hb = h;
-        if (writer) head[bg] = h;
-      }
-      if (blockIdx.x == 0)   // the other parity's inner sums, for the next run
-        for (int c = tid; c < P.nchrom; c += SBLOCK) bcount[(size_t)(1 - par) * P.nchrom + c] = 0u;
-      __syncthreads();
-      hb = sh_hb;
-    } else {
-      hb = head[bg];
-    }
-  } else {
-    fused_table(P.nb2, P.nh, P.nt, P.n1p, P.n2p, P.n1, P.n2, P.t1a, P.t1b, P.nchrom, ch.chrom,
-                ch.first == 0 && (int)ch.chrom == write_chrom, bg,
-                Rc, rs, repl, bcount, par, tab, LPg, head, LPl, HB, leaves, nleaves, nodes, nnodes, nlevels, lnx,
-                &sh_hb, reinterpret_cast<double*>(HB) + 1536, HB + FUSED_VCNT);
-    hb = sh_hb;
-  }
+  const BgHead hb = head[bg];
   for (int k = lane; k < per / 4; k += WAVE) reinterpret_cast<uint4*>(W)[k] = make_uint4(0, 0, 0, 0);
-  if (!GL && tid == 0) LPl[0] = 0.0;   // bin 0 ((0,0), never counted): excluded SNPs read it and add 0
   __syncthreads();
   const bool filt = P.ann_want >= 0;
   const bool half1d = P.n1p <= 33 && P.n2p <= 33;
   const uint32_t zflags = bg_zero_flags(hb);
   const bool nan2 = hb.flags & BGF_NAN2, nan1a = hb.flags & BGF_NAN1A, nan1b = hb.flags & BGF_NAN1B;
 
-  if (FUSED) {
-    // the other parity's replicas and inner sums: zeroed for the next run, a slice per workgroup
-    // (after the last barrier: nothing waits for these stores)
-    uint32_t* Ro = repl + (size_t)(1 - par) * REPL * rs;
-    const size_t tot = (size_t)REPL * rs, share = (tot + gridDim.x - 1) / gridDim.x;
-    const size_t lo = (size_t)blockIdx.x * share, hi = lo + share < tot ? lo + share : tot;
-    for (size_t k = lo + tid; k < hi; k += SBLOCK) Ro[k] = 0u;
-    if (blockIdx.x == 0)
-      for (int c = tid; c < P.nchrom; c += SBLOCK) bcount[(size_t)(1 - par) * P.nchrom + c] = 0u;
-  }
   if (!active) return;
-  const double Dreg = (GL && lane < 63) ? dfg[lane] : 0.0;   // GL: D(lane), lane 63: 0 (ranks from 63 on)
-  constexpr bool P16H = P16 && !GL;               // u16-packed 2D bins (GL: u8)
-  const uint32_t one1 = P16H ? 0x10000u : 1u;   // 1D increment (P16: counts in the upper halves)
+  const double Dreg = lane < 63 ? dfg[lane] : 0.0;   // D(lane), lane 63: 0 (ranks from 63 on)
+  const uint32_t one1 = 1u;                         // 1D increment
   uint32_t* const H1a_l = H1a + rep;            // this lane's replica column of the 1D histograms
   uint32_t* const H1b_l = H1b + rep;
   uint32_t* const T_l = W + trash;
@@ -2024,25 +1949,23 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
       cur = nxt;
       continue;
     }
-    // SNP j of this lane is b + lane + 64 j: steps of 64 SNPs in pairs, the first 8 steps from the
-    // prefetched registers (a step wholly past e is skipped; SNPs past e are w = 0, i.e. excluded).
-    // Counters are wave-uniform ballot counts.  Excluded SNPs (k2 = 0) add 0 to the lane's trash
-    // word, whose lower half therefore stays 0 and gives rank 0, D(0) = 0 and LPl[0] = 0; the 1D
-    // atomics add to the upper halves (P16), so a 1D increment landing in the trash cannot disturb it.
+    // SNP j of this lane is b + lane + 64 j: steps (rows) of 64 SNPs in pairs (SNPs past e are w = 0,
+    // i.e. excluded).  Counters are wave-uniform ballot counts.  Excluded SNPs (k2 = 0) add 0 to the
+    // lane's trash word and take rank 0 and lp 0; 1D increments outside the inner bins land there too.
     const uint32_t nsnp = cur.e - cur.b;
     const int lim = (int)nsnp - lane;
 
     double acc2 = 0.0;
     uint32_t n2 = 0, nlast = 0, n1a = 0, n1b = 0, nvar = 0;
-    bool ovf = false;   // GL: some u8 bin of this lane wrapped
-    bool big = false;   // GL: some bin of this lane passed rank 63 (its later ranks added 0; see below)
+    bool ovf = false;   // some u8 bin of this lane wrapped
+    bool big = false;   // some bin of this lane passed rank 63 (its later ranks added 0; see below)
     // the 2D words of the last 8 steps (a shift register: computed values, no loads, so its moves never
     // wait), cleared after a window of <= 6 steps; initially the lane's trash word
     uint32_t kw[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) kw[j] = trash;
     // A pair of rows in two halves, software-pipelined as in k_scan_w: issue() classifies, issues the
-    // LDS atomics and (GL) the lp loads from the global table; finish() turns the returned ranks and lp
+    // LDS atomics and the lp loads from the global table; finish() turns the returned ranks and lp
     // into D(r) - lp_k.  The loops issue pair j before they finish pair j - 2: a pair's atomics and its
     // L2 round trip for lp return under the next pair's work.
     struct PairSt { uint32_t ov[2], xs[2], kk[2]; double lp[2]; };
@@ -2067,14 +1990,14 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
         // (the global table, whose bin 0 is not zeroed: excluded SNPs read D's last entry, 0, instead --
         // an address select here, not a select of the loaded value in finish(), which the scheduler
         // hoisted next to the load and so waited for the gather on the spot)
-        if (GL) st.lp[q] = *(k2 ? LPl + k2 : Dt + (LNT - 1));
-        const uint32_t word = k2 ? (GL ? (k2 >> 2) : P16 ? (k2 >> 1) : k2) : trash;
-        // the byte / half's shift: the hardware reads shift operands' low five bits, so k2 << 3 (GL)
-        // or k2 << 4 serves without a mask (the bins word's low bits are k2's)
+        st.lp[q] = *(k2 ? LPl + k2 : Dt + (LNT - 1));
+        const uint32_t word = k2 ? (k2 >> 2) : trash;   // (u8 bins: four to a word)
+        // the byte's shift: the hardware reads shift operands' low five bits, so k2 << 3 serves
+        // without a mask (the bins word's low bits are k2's)
         const uint32_t wk = CNT ? k2 : w;
-        const uint32_t sh = GL ? (wk << 3) : P16 ? (wk << 4) : 0u;
+        const uint32_t sh = wk << 3;
         uint32_t one2 = 1u;
-        if (GL || P16) asm("v_lshlrev_b32 %0, %1, 1" : "=v"(one2) : "v"(sh));
+        asm("v_lshlrev_b32 %0, %1, 1" : "=v"(one2) : "v"(sh));
         st.ov[q] = atomicAdd(&W[word], k2 ? one2 : 0u);
         st.xs[q] = sh;
         st.kk[q] = k2;
@@ -2085,31 +2008,27 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
       }
       return st;
     };
-    // dlook(): the pair's D(r) look-ups, issued as soon as its ranks are in (GL: lane shuffles, before
+    // dlook(): the pair's D(r) look-ups, issued as soon as its ranks are in (lane shuffles, before
     // the next pair's atomics, so that waiting for them is not waiting for those too -- LDS operations
     // complete in order); finish(): D(r) - lp_k into the sum
     auto dlook = [&](const PairSt& st, double (&d)[2]) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        if (GL) {   // (the trash word's low byte counts 1D increments: excluded SNPs take rank 0)
-          const uint32_t r = __builtin_amdgcn_ubfe(st.ov[q], st.xs[q], 8);
-          const uint32_t rk = st.kk[q] ? r : 0u;
-          ovf |= (st.kk[q] != 0u) & (r == 255u);
-          // D(r) for r < 63 from the lanes' registers, lane 63 holding 0: ranks from 63 on add 0 here and
-          // the window's end adds F(x) - F(63) for each bin past 63 (a global read of D for them, even
-          // in a branch never taken, put a wait for every outstanding load -- the next pair's lp gathers
-          // and rows -- into every pair; config 4's bins never pass ~20 SNPs)
-          d[q] = __shfl(Dreg, (int)min(rk, 63u));
-          big |= rk >= 63u;
-        } else {
-          const uint32_t rk = P16 ? __builtin_amdgcn_ubfe(st.ov[q], st.xs[q], 16) : (st.kk[q] ? st.ov[q] : 0u);
-          d[q] = Dt[min(rk, (uint32_t)LNT - 1u)];   // D[LNT-1] = 0: ranks past the table add 0
-        }
+        // (the trash word's low byte counts 1D increments: excluded SNPs take rank 0)
+        const uint32_t r = __builtin_amdgcn_ubfe(st.ov[q], st.xs[q], 8);
+        const uint32_t rk = st.kk[q] ? r : 0u;
+        ovf |= (st.kk[q] != 0u) & (r == 255u);
+        // D(r) for r < 63 from the lanes' registers, lane 63 holding 0: ranks from 63 on add 0 here and
+        // the window's end adds F(x) - F(63) for each bin past 63 (a global read of D for them, even
+        // in a branch never taken, put a wait for every outstanding load -- the next pair's lp gathers
+        // and rows -- into every pair; config 4's bins never pass ~20 SNPs)
+        d[q] = __shfl(Dreg, (int)min(rk, 63u));
+        big |= rk >= 63u;
       }
     };
     auto finish = [&](const PairSt& st, const double (&d)[2]) {
 #pragma unroll
-      for (int q = 0; q < 2; ++q) acc2 += d[q] - (GL ? st.lp[q] : LPl[st.kk[q]]);
+      for (int q = 0; q < 2; ++q) acc2 += d[q] - st.lp[q];
     };
     // The pairs as a rolled loop, two per trip in fixed slots A / B (a pending pair carried through a
     // branch join is copied there, and a copy of registers with loads in flight waits for them: unrolled
@@ -2153,12 +2072,10 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
       }
     }
     if (!filt) nvar = nsnp;
-    // GL: the totals' x ln x from the global table, issued now (their latency under the 1D pass)
-    double fn2 = 0.0, fn1a = 0.0, fn1b = 0.0;
-    if (GL) { fn2 = xlnx(n2, Ft, lnx); fn1a = xlnx(n1a, Ft, lnx); fn1b = xlnx(n1b, Ft, lnx); }
+    // the totals' x ln x from the global table, issued now (their latency under the 1D pass)
+    const double fn2 = xlnx(n2, Ft, lnx), fn1a = xlnx(n1a, Ft, lnx), fn1b = xlnx(n1b, Ft, lnx);
     ulonglong2 fq = make_ulonglong2(0ull, 0ull);   // this window's Fst sums (k_prep), used at the end
     if (FST && lane == 0) fq = reinterpret_cast<const ulonglong2*>(fsum)[s];
-    const bool ov = !GL && nsnp > (uint32_t)(LNT - 1);   // some rank may have passed the D table (GL: ranks < 256)
     if (it == 0) STAMP(12);
     // next window: its slot record is in, issue its first steps now (the record made wave-uniform
     // here: its load, issued at the window's start, was otherwise waited for right there)
@@ -2169,7 +2086,7 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
     // 1D spectra: one lane per folded inner bin reads (and clears) its R1 replicas; with <= 32 inner
     // bins per population, lanes 0-31 take population 1 and lanes 32-63 population 2 (acca)
     double acca = 0.0, accb = 0.0;
-    constexpr uint32_t S1 = P16H ? 16u : 0u;
+    constexpr uint32_t S1 = 0u;   // (the 1D counts fill their words)
     if (half1d) {
       const bool pa = lane < 32;
       const int k = 1 + (lane & 31);
@@ -2190,9 +2107,9 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
         accb += x ? xlnx(x, Ft, lnx) - (double)x * LPl[P.t1b + k] : 0.0;
       }
     }
-    // GL: bins with x > 63 SNPs (u8: x <= 254, or the window is re-evaluated exactly below) add
+    // bins with x > 63 SNPs (u8: x <= 254, or the window is re-evaluated exactly below) add
     // F(x) - F(63) (read before the clear)
-    if (GL && __ballot(big) != 0ull) {
+    if (__ballot(big) != 0ull) {
       const double f63 = Ft[63];
       for (int k = lane; k < h2w; k += WAVE) {
         const uint32_t v = W[k];
@@ -2201,17 +2118,6 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
           const uint32_t x = (v >> (8 * b)) & 0xffu;
           if (x > 63u) acc2 += xlnx(x, Ft, lnx) - f63;
         }
-      }
-    }
-    // bins with x > LNT-1 SNPs: the ranks from LNT-1 on add F(x) - F(LNT-1) (read before the clear)
-    if (ov) {
-      constexpr uint32_t L1 = LNT - 1;
-      const double fl = Ft[L1];
-      for (int k = lane; k < h2w; k += WAVE) {
-        const uint32_t v = W[k];
-        const uint32_t xa = P16 ? (v & 0xffffu) : v, xb = P16 ? (v >> 16) : 0u;
-        if (xa > L1) acc2 += (double)xa * lnx_of(lnx, xa) - fl;
-        if (xb > L1) acc2 += (double)xb * lnx_of(lnx, xb) - fl;
       }
     }
     // clear the 2D words this window touched (<= 6 steps: all in kw, with trash words)
@@ -2231,19 +2137,15 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
     }
     WinOut w;
     w.snp_count = nvar; w.n2_all = n2 + nlast; w.n2 = n2; w.n1a = n1a; w.n1b = n1b;
-    w.t2d = 2.0 * (s2 - (GL ? fn2 : xlnx(n2, Ft, lnx)));
-    w.t1a = 2.0 * (sa - (GL ? fn1a : xlnx(n1a, Ft, lnx)));
-    w.t1b = 2.0 * (sb - (GL ? fn1b : xlnx(n1b, Ft, lnx)));
-    const bool wrapped = GL && __ballot(ovf) != 0ull;
+    w.t2d = 2.0 * (s2 - fn2);
+    w.t1a = 2.0 * (sa - fn1a);
+    w.t1b = 2.0 * (sb - fn1b);
+    const bool wrapped = __ballot(ovf) != 0ull;
     if (wrapped || cur.e - cur.b >= 65536u || suspect_zero(w.t2d, n2) || suspect_zero(w.t1a, n1a) ||
         suspect_zero(w.t1b, n1b)) {
       // rare: exact re-evaluation with the bin-by-bin proportionality test (histograms are clean)
       group_sync<WAVE>();
-      if (FUSED) {
-        w = eval_exact<WAVE, P16, RG, CNT>(P, bins, cur.b, cur.e,
-                                      TabFused{LPl, Rc, rs, P.nb2, P.n1, P.n2, P.n1p, P.h1a, P.h1b, P.t1a, P.t1b}, hb,
-                                      lnx, W, H1a, H1b, nullptr, nullptr);
-      } else if (GL) {
+      {
         // a u32 histogram in global memory: take a free slot (nscr >= resident waves)
         uint32_t* lock = gscr + (size_t)nscr * P.nb2;
         uint32_t slot = blockIdx.x % (uint32_t)nscr;
@@ -2257,9 +2159,6 @@ __device__ __forceinline__ void scan_w_body(double* ldsd, SCAN_W_ARGS) {
                                         gscr + (size_t)slot * P.nb2, H1a, H1b, nullptr, nullptr);
         __threadfence();   // the slot's words are clean again before it is released
         if (lane == 0) atomicExch(&lock[slot], 0u);
-      } else {
-        w = eval_exact<WAVE, P16, RG, CNT>(P, bins, cur.b, cur.e, TabLocal{tab + (size_t)bg * P.nt, LPl}, hb, lnx, W,
-                                      H1a, H1b, nullptr, nullptr);
       }
       if (lane == 0) atomicAdd(err_word + 1, 1u);   // statistics: windows that took the exact path
     } else {
@@ -3632,7 +3531,7 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) voi
 template <bool P16, bool FST, bool CNT>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(4))) void k_scan_gw(SCAN_W_ARGS) {
   extern __shared__ double ldsd[];
-  scan_w_body<P16, false, FST, true, CNT>(ldsd, SCAN_W_PASS);
+  scan_gw_body<P16, FST, CNT>(ldsd, SCAN_W_PASS);
 }
 
 // K3 for large grids: one workgroup per window, exact evaluation.
