@@ -1819,7 +1819,7 @@ __device__ __forceinline__ void fused_table(int nb2, int nh, int nt, int n1p, in
 // per-lane counters give every count, the 2D atomic returns the SNP's rank r in its bin and the
 // SNP adds D(r) - lp_k; the 1D atomics land in lane-&3 replicas; then one lane per 1D bin adds
 // x ln x - x lp; the touched 2D words are cleared; DPP sums; one record.
-// GL (k_scan_gw, grids too large for the table in LDS): one-wavefront workgroups whose LDS holds
+// k_scan_gw (grids too large for the table in LDS): one-wavefront workgroups whose LDS holds
 // only the wave's histograms; lp, D and F are read from the global tables (L2-resident: one
 // table per background, read by every window).  The 2D bins are u8-packed (101 x 101: 10 KB per
 // wave, 12 waves per CU instead of 7 with u16): a rank of 255 means the byte wrapped, and such a
