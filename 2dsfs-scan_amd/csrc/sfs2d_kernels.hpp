@@ -1865,32 +1865,27 @@ __device__ __forceinline__ void scan_gw_body(double* ldsd, SCAN_W_ARGS) {
   const uint32_t trash = (uint32_t)(h2w + h1w + h1wb + lane);   // word offset from W
   const uint32_t rep = lane & (RG - 1);
 
-  // the first window's slot record is fetched before the table work
-  auto bounds = [&](uint32_t s, uint2 sr, Win& w) {
+  // the first window's slot record is fetched before the table work.  The rows are loaded
+  // unconditionally, range-checked (a window that is not there -- live false, or an empty slot -- reads a
+  // 0-byte range: zeros, no memory access): no branch join around them for the wait counters to merge,
+  // which made later waits wait for them
+  auto bounds = [&](uint32_t s, uint2 sr, Win& w, bool live) {
     if (mode_bp) {
-      w.has = sr.x != 0u;
+      w.has = live && sr.x != 0u;
       w.b = sr.x - 1u;
       w.e = sr.y;
     } else {
-      w.has = true;
+      w.has = live;
       w.b = ch.cb + (ch.wid_lo + (s - ch.slot_lo)) * P.ws;
       w.e = w.b + P.ws;
     }
-    if (w.has) {   // the bins buffer has SCAN_PAD readable words past n (counts: buffer loads, 0 past n); masked in the last step
-      if (CNT) {
-        const __amdgpu_buffer_rsrc_t rr = window_rows(bins, w.b, w.e, P.nm1);
-        // (the lane's byte offset made opaque here: hoisted out of the window loop, the eight row offsets
-        // were kept live as eight VGPRs -- spilled elsewhere -- instead of one base + immediate offsets)
-        uint32_t lo = (uint32_t)lane * 4u;
-        asm volatile("" : "+v"(lo));
+    const __amdgpu_buffer_rsrc_t rr = window_rows(bins, w.has ? w.b : 0u, w.has ? w.e : 0u, P.nm1);
+    // (the lane's byte offset made opaque here: hoisted out of the window loop, the eight row offsets
+    // were kept live as eight VGPRs -- spilled elsewhere -- instead of one base + immediate offsets)
+    uint32_t lo = (uint32_t)lane * 4u;
+    asm volatile("" : "+v"(lo));
 #pragma unroll
-        for (int j = 0; j < 8; ++j) w.u[j] = __builtin_amdgcn_raw_buffer_load_b32(rr, (int)lo + 256 * j, 0, 0);
-      } else {
-        const uint32_t* q = bins + w.b + lane;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) w.u[j] = q[64 * j];
-      }
-    }
+    for (int j = 0; j < 8; ++j) w.u[j] = __builtin_amdgcn_raw_buffer_load_b32(rr, (int)lo + 256 * j, 0, 0);
   };
   // window schedule: one static window per wavefront, then the chromosome's pool counters (an
   // atomic is always one window ahead of its use, so its latency hides under a window's work)
@@ -1916,6 +1911,20 @@ __device__ __forceinline__ void scan_gw_body(double* ldsd, SCAN_W_ARGS) {
 
   if (!active) return;
   const double Dreg = lane < 63 ? dfg[lane] : 0.0;   // D(lane), lane 63: 0 (ranks from 63 on)
+  const double f63 = Ft[63];                          // F(63) (bins past 63 SNPs)
+  // the background's 1D terms of this lane's inner bins (the window's end: x ln x - x lp per bin)
+  const bool in1h = half1d && 1 + (lane & 31) <= (lane < 32 ? P.n1p : P.n2p) - 1;
+  double lp1a[2] = {0.0, 0.0}, lp1b[2] = {0.0, 0.0};
+  if (half1d) {
+    if (in1h) lp1a[0] = LPl[(lane < 32 ? P.t1a : P.t1b) + 1 + (lane & 31)];
+  } else {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = 1 + lane + WAVE * j;
+      if (k <= P.n1p - 1) lp1a[j] = LPl[P.t1a + k];
+      if (k <= P.n2p - 1) lp1b[j] = LPl[P.t1b + k];
+    }
+  }
   const uint32_t one1 = 1u;                         // 1D increment
   uint32_t* const H1a_l = H1a + rep;            // this lane's replica column of the 1D histograms
   uint32_t* const H1b_l = H1b + rep;
@@ -1926,7 +1935,7 @@ __device__ __forceinline__ void scan_gw_body(double* ldsd, SCAN_W_ARGS) {
   uint32_t atr = (uint32_t)(uintptr_t)((lds_u32*)T_l);
   asm volatile("" : "+v"(a1b), "+v"(a2b), "+v"(atr));
   Win cur;
-  bounds(s, sr0, cur);
+  bounds(s, sr0, cur, true);
   STAMP(11);
   int it = 0;
   uint32_t sn = ch.slot_hi;
@@ -1945,7 +1954,7 @@ __device__ __forceinline__ void scan_gw_body(double* ldsd, SCAN_W_ARGS) {
       if (FST && lane == 0) fst_out[s] = __builtin_nan("");
       Win nxt;
       nxt.has = false;
-      if (more) bounds(sn, make_uint2(__builtin_amdgcn_readfirstlane(srn.x), __builtin_amdgcn_readfirstlane(srn.y)), nxt);
+      bounds(sn, make_uint2(__builtin_amdgcn_readfirstlane(srn.x), __builtin_amdgcn_readfirstlane(srn.y)), nxt, more);
       cur = nxt;
       continue;
     }
@@ -2072,51 +2081,60 @@ __device__ __forceinline__ void scan_gw_body(double* ldsd, SCAN_W_ARGS) {
       }
     }
     if (!filt) nvar = nsnp;
-    // the totals' x ln x from the global table, issued now (their latency under the 1D pass)
-    const double fn2 = xlnx(n2, Ft, lnx), fn1a = xlnx(n1a, Ft, lnx), fn1b = xlnx(n1b, Ft, lnx);
+    // The window's end issues its global loads -- ln of the totals and of the 1D counts (F(x) = x * ln x,
+    // the F table's own values) -- before the next window's rows, unconditionally (no branch joins) and
+    // with the 1D background terms in registers, so that no wait here is a wait for those rows (loads
+    // complete in order; the rows then get the rest of this window's end to arrive)
+    auto lnld = [&](uint32_t x) { return lnx[min(x, (uint32_t)LNX_N - 1u)]; };
+    const double ln2 = lnld(n2), ln1a = lnld(n1a), ln1b = lnld(n1b);
     ulonglong2 fq = make_ulonglong2(0ull, 0ull);   // this window's Fst sums (k_prep), used at the end
     if (FST && lane == 0) fq = reinterpret_cast<const ulonglong2*>(fsum)[s];
     if (it == 0) STAMP(12);
-    // next window: its slot record is in, issue its first steps now (the record made wave-uniform
+    group_sync<WAVE>();
+    // 1D spectra: one lane per folded inner bin reads (and clears) its replicas; with <= 32 inner bins
+    // per population, lanes 0-31 take population 1 and lanes 32-63 population 2 (acca)
+    constexpr uint32_t S1 = 0u;   // (the 1D counts fill their words)
+    uint32_t xa[2] = {0u, 0u}, xb[2] = {0u, 0u};
+    if (half1d) {
+      if (in1h) xa[0] = take_replicas<RG>((lane < 32 ? H1a : H1b) + (1 + (lane & 31)) * RG, S1);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int k = 1 + lane + WAVE * j;
+        if (k <= P.n1p - 1) xa[j] = take_replicas<RG>(H1a + k * RG, S1);
+        if (k <= P.n2p - 1) xb[j] = take_replicas<RG>(H1b + k * RG, S1);
+      }
+    }
+    double la[2], lb[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) { la[j] = lnld(xa[j]); lb[j] = lnld(xb[j]); }
+    __builtin_amdgcn_sched_barrier(0);
+    // next window: its slot record is in, issue its first rows now (the record made wave-uniform
     // here: its load, issued at the window's start, was otherwise waited for right there)
     Win nxt;
     nxt.has = false;
-    if (more) bounds(sn, make_uint2(__builtin_amdgcn_readfirstlane(srn.x), __builtin_amdgcn_readfirstlane(srn.y)), nxt);
-    group_sync<WAVE>();
-    // 1D spectra: one lane per folded inner bin reads (and clears) its R1 replicas; with <= 32 inner
-    // bins per population, lanes 0-31 take population 1 and lanes 32-63 population 2 (acca)
+    bounds(sn, make_uint2(__builtin_amdgcn_readfirstlane(srn.x), __builtin_amdgcn_readfirstlane(srn.y)), nxt, more);
+    __builtin_amdgcn_sched_barrier(0);
+    const double fn2 = __dmul_rn((double)n2, ln2), fn1a = __dmul_rn((double)n1a, ln1a), fn1b = __dmul_rn((double)n1b, ln1b);
+    // x ln x - x lp per inner bin (x = 0: 0, whatever lp -- -inf for an empty background bin)
     double acca = 0.0, accb = 0.0;
-    constexpr uint32_t S1 = 0u;   // (the 1D counts fill their words)
-    if (half1d) {
-      const bool pa = lane < 32;
-      const int k = 1 + (lane & 31);
-      if (k <= (pa ? P.n1p : P.n2p) - 1) {
-        const uint32_t x = take_replicas<RG>((pa ? H1a : H1b) + k * RG, S1);
-        acca = x ? xlnx(x, Ft, lnx) - (double)x * LPl[(pa ? P.t1a : P.t1b) + k] : 0.0;
-      }
-    } else
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int k = 1 + lane + WAVE * j;
-      if (k <= P.n1p - 1) {
-        const uint32_t x = take_replicas<RG>(H1a + k * RG, S1);
-        acca += x ? xlnx(x, Ft, lnx) - (double)x * LPl[P.t1a + k] : 0.0;
-      }
-      if (k <= P.n2p - 1) {
-        const uint32_t x = take_replicas<RG>(H1b + k * RG, S1);
-        accb += x ? xlnx(x, Ft, lnx) - (double)x * LPl[P.t1b + k] : 0.0;
-      }
+    for (int j = 0; j < 2; ++j) {   // (half1d: j = 1 adds 0)
+      acca += xa[j] ? __dmul_rn((double)xa[j], la[j]) - (double)xa[j] * lp1a[j] : 0.0;
+      accb += xb[j] ? __dmul_rn((double)xb[j], lb[j]) - (double)xb[j] * lp1b[j] : 0.0;
     }
+    // (consumed here, before any branch: a load's register first used behind a branch join made the
+    // wait there conservative -- a wait for the rows just issued)
+    asm volatile("" ::"v"(acca), "v"(accb), "v"(fn2), "v"(fn1a), "v"(fn1b), "v"(fq.x), "v"(fq.y));
     // bins with x > 63 SNPs (u8: x <= 254, or the window is re-evaluated exactly below) add
-    // F(x) - F(63) (read before the clear)
+    // F(x) - F(63) (read before the clear; ln x computed, not loaded: no global load after the rows)
     if (__ballot(big) != 0ull) {
-      const double f63 = Ft[63];
       for (int k = lane; k < h2w; k += WAVE) {
         const uint32_t v = W[k];
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
           const uint32_t x = (v >> (8 * b)) & 0xffu;
-          if (x > 63u) acc2 += xlnx(x, Ft, lnx) - f63;
+          if (x > 63u) acc2 += __dmul_rn((double)x, log((double)x)) - f63;
         }
       }
     }
