@@ -2402,33 +2402,28 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   uint32_t* H1b = H1a + h1w;
   const uint32_t rep = lane & (R1 - 1);
 
-  auto bounds = [&](uint32_t s, uint2 sr, Win& w) {
+  // a window's first 8 rows, loaded unconditionally and range-checked (a window that is not there --
+  // live false, or an empty slot -- reads a 0-byte range: zeros, no memory access): issued behind a
+  // branch, the join made the wait counters merge conservatively, and the row loop waited for the next
+  // window's rows as well as this window's
+  auto bounds = [&](uint32_t s, uint2 sr, Win& w, bool live) {
     if (mode_bp) {
-      w.has = sr.x != 0u;
+      w.has = live && sr.x != 0u;
       w.b = sr.x - 1u;
       w.e = sr.y;
     } else {
-      w.has = true;
+      w.has = live;
       w.b = ch.cb + (ch.wid_lo + (s - ch.slot_lo)) * P.ws;
       w.e = w.b + P.ws;
     }
-    if (w.has) {   // the bins buffer has SCAN_PAD readable words past n; masked in the last step
-      // (uniform base + a 32-bit lane offset: no per-lane 64-bit pointer stays live, which the exact
-      // path's registers pushed to scratch -- 512 B of stores per wavefront)
-      const uint32_t* q = bins + w.b;
-      if (CNT) {   // counts, no padding past n: range-checked buffer loads (0 past n; masked later)
-        const __amdgpu_buffer_rsrc_t rr = window_rows(bins, w.b, w.e, P.nm1);
-        // (the lane's byte offset made opaque here: hoisted out of the window loop, the eight row offsets
-        // were kept live as eight VGPRs -- spilled elsewhere -- instead of one base + immediate offsets)
-        uint32_t lo = (uint32_t)lane * 4u;
-        asm volatile("" : "+v"(lo));
+    // (counts: 0 past the window's end; bins: masked in the row loop anyway)
+    const __amdgpu_buffer_rsrc_t rr = window_rows(bins, w.has ? w.b : 0u, w.has ? w.e : 0u, P.nm1);
+    // (the lane's byte offset made opaque here: hoisted out of the window loop, the eight row offsets
+    // were kept live as eight VGPRs -- spilled elsewhere -- instead of one base + immediate offsets)
+    uint32_t lo = (uint32_t)lane * 4u;
+    asm volatile("" : "+v"(lo));
 #pragma unroll
-        for (int j = 0; j < 8; ++j) w.u[j] = __builtin_amdgcn_raw_buffer_load_b32(rr, (int)lo + 256 * j, 0, 0);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) w.u[j] = q[(uint32_t)lane + 64u * j];
-      }
-    }
+    for (int j = 0; j < 8; ++j) w.u[j] = __builtin_amdgcn_raw_buffer_load_b32(rr, (int)lo + 256 * j, 0, 0);
   };
   // window schedule: one static window per wavefront, then the chromosome's pool counters (an
   // atomic is always one window ahead of its use, so its latency hides under a window's work)
@@ -2675,7 +2670,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     return dyn && dbase + npool * j < ch.slot_hi ? dbase + npool * j : ch.slot_hi;
   };
   Win cur;
-  bounds(s, sr0, cur);
+  bounds(s, sr0, cur, true);
   uint32_t s1 = pool_slot(gq1);
   uint2 sr1 = (mode_bp && s1 < ch.slot_hi) ? slots[s1] : make_uint2(0, 0);
   uint2 srs = make_uint2(0, 0);   // the slot record of window s, for the rows issued after a flush
@@ -2690,7 +2685,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     const uint2 sr1u = make_uint2(__builtin_amdgcn_readfirstlane(sr1.x), __builtin_amdgcn_readfirstlane(sr1.y));
     Win nxt;
     nxt.has = false;
-    if (more && fill) bounds(s1, sr1u, nxt);
+    bounds(s1, sr1u, nxt, more && fill);
     const uint32_t s2 = more ? pool_slot(gq) : ch.slot_hi;
     const uint2 sr2 = (mode_bp && s2 < ch.slot_hi) ? slots[s2] : make_uint2(0, 0);
     if (s2 < ch.slot_hi && lane == 0) gq = atomicAdd(myctr, 1u);
@@ -2995,7 +2990,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   }
   if (jb) flush();   // (a full batch, or the wavefront's last windows)
   if (s >= ch.slot_hi) break;
-  bounds(s, srs, cur);   // the next batch's first window
+  bounds(s, srs, cur, true);   // the next batch's first window
   }
   STAMP(15);
   WV_STAMP(it);
