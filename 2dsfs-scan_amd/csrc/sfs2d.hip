@@ -127,6 +127,12 @@ struct sfs2d_data {
   // some SNP has fewer than 2 called alleles in a population (unknown: true): Fst summed in the scan
   // must then drop such SNPs explicitly (k_scan_w<..., 3, ...>); without any, the unmasked terms are exact
   bool low_nc = true;
+  // sfs2d_data_synth_sims: the generator's window offsets (SNP index of window w's first SNP, nwin + 1
+  // entries; w = replicate * win_per_chrom + window), its window length and windows per replicate --
+  // fixed-bp plans of that window length take their slot table from them instead of k_prep's
+  // segmentation pass over the positions (the generator placed window w's SNPs in its own window)
+  unsigned long long* d_win_off = nullptr;
+  uint32_t win_bp = 0, win_per_chrom = 0;
 };
 
 struct sfs2d_plan {
@@ -136,6 +142,7 @@ struct sfs2d_plan {
   KParams K{};
   int nbg = 0;
   bool do_bg = false, do_seg = false, lds_hist = true, bg_ready = false;
+  bool seg_synth = false;   // fixed-bp slots from the generator's window offsets (synth_seg)
   bool fused = false;       // per-chromosome tables built inside k_scan_w (parity-alternating replicas)
   bool sliced = false;      // per-chromosome tables by k_bg_slice without its tail; k_scan_w combines
                             // the leaf sums (parity-alternating inner sums)
@@ -381,6 +388,21 @@ hipError_t launch_prep_cnt(sfs2d_plan* pl) {
   if (pl->do_seg) return launch_prep1<false, true, false, false>(pl);
   if (fs) return launch_prep1<false, false, false, false>(pl);
   return hipSuccess;
+}
+
+// whether a run takes its slot table from the generator's window offsets instead of k_prep (see
+// seg_synth; k_prep's Fst sums or an attached plan's use of its pass keep k_prep)
+bool synth_seg(const sfs2d_plan* pl) {
+  return pl->seg_synth && pl->attached.empty() && !(pl->fst && !pl->fst_win && !pl->fst_scan);
+}
+
+hipError_t launch_slots_synth(sfs2d_plan* pl) {
+  const unsigned long long nw = (unsigned long long)pl->nslots;
+  const unsigned grid = (unsigned)std::min<unsigned long long>(8192, (nw + 255) / 256);
+  if (nw)   // (the k_prep timing slot: this is the run's segmentation stage)
+    hipExtLaunchKernelGGL(k_slots_synth, dim3(grid), dim3(256), 0, CTX_STREAM(pl->ctx), pl->kev[0], pl->kev[1], 0,
+                          pl->data->d_win_off, nw, pl->d_slots);
+  return hipGetLastError();
 }
 
 // whether a plan run launches k_prep at all
@@ -699,12 +721,15 @@ int sfs2d_data_synth_sims(sfs2d_ctx* ctx, const sfs2d_synth_params* sp, const ui
     e = hipGetLastError();
   }
   if (e == hipSuccess) e = hipStreamSynchronize(CTX_STREAM(ctx));
-  hipFree(d_woff);
   hipFree(d_mt);
   if (e != hipSuccess) {
+    hipFree(d_woff);
     hipFree(d->counts); hipFree(d->pos); hipFree(d->ann); hipFree(d->d_chrom_off); delete d;
     return set_err(ctx, SFS2D_E_HIP, std::string("synthetic data: ") + hipGetErrorString(e));
   }
+  d->d_win_off = d_woff;   // the window offsets stay: fixed-bp plans of window_bp read their slots from them
+  d->win_bp = sp->window_bp;
+  d->win_per_chrom = sp->n_windows;
   d->last_pos.assign(sp->n_replicates, sp->n_windows * sp->window_bp);   // upper bound: trailing slots stay empty
   d->strict = true;
   d->max_nc1 = 2u * (uint32_t)sp->n1p;   // k_synth_sims: ref + alt + missing = 2 pop_size
@@ -729,6 +754,7 @@ int sfs2d_data_free(sfs2d_data* d) {
   if (d->owned) { hipFree(d->counts); hipFree(d->pos); }
   if (d->owned || d->ann_owned) hipFree(d->ann);
   hipFree(d->d_chrom_off);
+  hipFree(d->d_win_off);
   delete d;
   return 0;
 }
@@ -810,6 +836,18 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   if (pl->cnt && prm->bg_mode != SFS2D_BG_PER_CHROM &&
       !(data->max_nc1 <= (uint32_t)K.n1 && data->max_nc2 <= (uint32_t)K.n2))
     pl->cnt = false;
+  // generated replicates (sfs2d_data_synth_sims) scanned with the generator's window length: slot s of
+  // replicate c is the generator's window c * win_per_chrom + w, whose SNPs it placed in that window
+  // ((pos - 1) / ws == w), so the slot table is the window offsets (k_slots_synth) -- when every
+  // replicate holds SNPs (the slot numbering skips empty chromosomes) and the plan has no other k_prep
+  // work (a counts plan with a supplied background; see synth_seg).  SFS2D_SYNTH_SEG=0: k_prep instead.
+  if (bp && data->d_win_off && (uint32_t)prm->window == data->win_bp && pl->cnt && !pl->do_bg &&
+      pl->nslots == (int64_t)nc * (int64_t)data->win_per_chrom) {
+    bool all = true;
+    for (int c = 0; c < nc && all; ++c) all = data->chrom_off[c + 1] > data->chrom_off[c];
+    const char* ev = std::getenv("SFS2D_SYNTH_SEG");
+    pl->seg_synth = all && !(ev && ev[0] == '0');
+  }
   pl->K.nm1 = data->n > 0 ? (uint32_t)(data->n - 1) : 0u;
   pl->K.kmul = (uint32_t)(pl->K.n2 + 1) | (1u << 16);
   pl->K.n12 = (uint32_t)pl->K.n1 | ((uint32_t)pl->K.n2 << 16);
@@ -1271,8 +1309,13 @@ int sfs2d_plan_run_phase(sfs2d_plan* pl, int phase, sfs2d_window* out_dev) {
   };
   int rc = 0;
   if (phase == 0 || phase == 1) {
-    HIPCHK(ctx, launch_prep(pl, true));
-    if (!prep_runs(pl) && (rc = mark(0))) return rc;
+    if (synth_seg(pl)) {
+      HIPCHK(ctx, launch_slots_synth(pl));
+      if (pl->nslots == 0 && (rc = mark(0))) return rc;
+    } else {
+      HIPCHK(ctx, launch_prep(pl, true));
+      if (!prep_runs(pl) && (rc = mark(0))) return rc;
+    }
   } else if ((rc = mark(0))) {
     return rc;
   }
@@ -1567,7 +1610,7 @@ int sfs2d_plan_time(sfs2d_plan* pl, int iters, double* ms_run, double* ms_k1, do
   double t1 = 0, t2 = 0, t3 = 0, tall = 0;
   for (int it = 0; it < iters; ++it) {
     HIPCHK(ctx, hipEventRecord(pl->ev[0], st));
-    HIPCHK(ctx, launch_prep(pl, true));
+    HIPCHK(ctx, synth_seg(pl) ? launch_slots_synth(pl) : launch_prep(pl, true));
     HIPCHK(ctx, hipEventRecord(pl->ev[1], st));
     if (pl->do_bg && !pl->fused) HIPCHK(ctx, launch_bg_slices(pl));
     for (sfs2d_plan* a : pl->attached) HIPCHK(ctx, launch_attached(a));

@@ -3789,4 +3789,16 @@ __global__ __launch_bounds__(256) void k_synth_sims(SynthP S, const unsigned lon
   }
 }
 
+// the slot table of a fixed-bp plan over generated replicates from the generator's window offsets
+// (sfs2d_data_synth_sims placed window w's SNPs [woff[w], woff[w+1]) in window w): slot w = (first + 1,
+// last + 1) as k_prep's segmentation writes it, (0, 0) for a window without SNPs
+__global__ __launch_bounds__(256) void k_slots_synth(const unsigned long long* __restrict__ woff, unsigned long long nw,
+                                                     uint2* __restrict__ slots) {
+  for (unsigned long long w = (unsigned long long)blockIdx.x * 256 + threadIdx.x; w < nw;
+       w += (unsigned long long)gridDim.x * 256) {
+    const unsigned long long a = woff[w], b = woff[w + 1];
+    slots[w] = b > a ? make_uint2((uint32_t)a + 1u, (uint32_t)b) : make_uint2(0u, 0u);
+  }
+}
+
 }  // namespace sfs2dk

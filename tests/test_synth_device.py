@@ -56,3 +56,39 @@ def test_scan_of_generated_data_vs_oracle():
         got = post.sims_process_window(sub, q, ws, len(sub))
         ref = O.sims_process_window(q, o2, o1, o1b, ws, n, n)
         assert not gu.compare_results(got, ref)
+
+
+@pytest.mark.parametrize("ws", [20000, 10000])
+def test_generator_slots_equal_segmentation(monkeypatch, ws):
+    """A fixed-bp plan over generated replicates with the generator's window length takes its slot table
+    from the generator's window offsets (k_slots_synth) instead of k_prep's segmentation of the
+    positions: the records are byte-equal to the segmentation path's (SFS2D_SYNTH_SEG=0), including
+    windows without SNPs; another window length (10 kb) takes the segmentation path either way."""
+    from sfs2d import _lib as L
+    from sfs2d.engine import Engine, ScanConfig
+    from sfs2d.synth import miss_table, sims_window_counts
+    n, nwin, nrep = 25, 60, 5
+    seed, gen = 4242, 2
+    wc = sims_window_counts(seed, gen, nrep, nwin, mean=40.0)
+    wc[3] = 0                     # an empty window in replicate 0
+    wc[nwin + 7] = 1              # a one-SNP window in replicate 1
+    mt = miss_table(2 * n)
+    eng = Engine.get(0)
+    dev = eng.synth_sims(seed, gen, nrep, nwin, 20000, n, n, wc, mt, mt)
+    try:
+        h2, u1, u2 = eng.bg_hist(dev, ScanConfig(n1p=n, n2p=n, start_position=0, end_position=500000), -1)
+        bg = (h2.reshape(-1).astype(np.float64), u1[: n + 1].astype(np.float64), u2[: n + 1].astype(np.float64))
+        cfg = ScanConfig(n1p=n, n2p=n, window=ws, bg_mode=L.BG_SUPPLIED)
+        outs = []
+        for flag in ("1", "0"):
+            monkeypatch.setenv("SFS2D_SYNTH_SEG", flag)
+            pl = eng.plan(dev, cfg)
+            pl.set_background(*bg)
+            for _ in range(2):   # the scan clears the slot table after use: a second run rebuilds it
+                pl.run()
+                pl.check()
+            outs.append(pl.read().tobytes())
+            pl.close()
+    finally:
+        dev.close()
+    assert outs[0] == outs[1]
