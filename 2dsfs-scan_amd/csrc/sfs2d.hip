@@ -20,7 +20,6 @@
 #include <cstring>
 #include <string>
 #include <mutex>
-#include <thread>
 #include <vector>
 
 #include "sfs2d.h"
@@ -87,12 +86,8 @@ void div_magic(uint32_t d, uint32_t* m, int* s1, int* s2) {
 
 }  // namespace
 
-// the stream a host thread enqueues on: the ctx's, unless this thread runs one of
-// sfs2d_plan_run_streams' enqueue threads (each on its own stream)
-namespace {
-thread_local hipStream_t tl_stream = nullptr;
-}
-#define CTX_STREAM(c) (tl_stream ? tl_stream : (c)->stream)
+// the stream the library enqueues on: the ctx's current one (sfs2d_ctx_set_stream)
+#define CTX_STREAM(c) ((c)->stream)
 
 struct sfs2d_ctx {
   int device = 0;
@@ -100,7 +95,7 @@ struct sfs2d_ctx {
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   double* d_lnx = nullptr;
-  double* d_df = nullptr;   // D(r), F(x) (LNT each), then (1/k, 1/(k(k-1))) pairs (RCPN), then Fst (p, A) by (alt, ref) (FSTAR)
+  double* d_df = nullptr;   // D(r), F(x) (LNT each), then (1/k, 1/(k(k-1))) pairs (RCPN), then Fst (p, A) by (n, a) (PA_N, a triangle)
   std::string err;
   std::mutex err_mu;
 };
@@ -206,15 +201,15 @@ struct sfs2d_plan {
   uint32_t fst_m = 0;             // attached Fst: base windows per window (their sums add)
   bool fst_win = false;           // Fst by window kernels (fst_windows) instead of k_prep's sums
   bool fst_scan = false;          // Fst summed by k_scan_w itself (counts plans, small grids): k_prep has no Fst work
-  bool lite = false;              // k_scan_wl instead of k_scan_w (counts plans, small grids: six waves per SIMD)
-  bool fst_mask = true;           // Fst in the scan: the data set has SNPs with < 2 called alleles (k_scan_w FST 3)
+  bool fst_mask = true;           // Fst in the scan: the data set has SNPs with < 2 called alleles (k_scan_w FST 3 / 5)
+  bool w8 = false;                // k_scan_w8 (counts plans, small grids): u8 2D bins, Fst's (p, A) table in LDS
   int nfst = 0;                   // k_bg_slice's extra Fst workgroups
 };
 
 namespace {
 
 int set_err(sfs2d_ctx* ctx, int code, const std::string& m) {
-  if (ctx) {   // (the SFS2D_ENQ_THREADS enqueue threads may fail concurrently on one ctx)
+  if (ctx) {   // (callers may use several ctx objects from several threads)
     std::lock_guard<std::mutex> g(ctx->err_mu);
     ctx->err = m;
   }
@@ -277,6 +272,16 @@ void launch_scan_w(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
                      (int)(pl->runs & 1), pl->d_leafsum, pl->d_bg1d, pl->sliced ? 1 : 0, nullptr, 0);
 }
 
+template <bool FUSED, int FST>
+void launch_scan_w8(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
+  hipExtLaunchKernelGGL((k_scan_w8<FUSED, FST>), dim3((unsigned)pl->chunks.size()), dim3(SBLOCK), pl->scan_lds,
+                     CTX_STREAM(pl->ctx), pl->kev[4], pl->kev[5], 0, pl->K, scan_src(pl), pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
+                     per_chrom, pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, bp, pl->d_repl, pl->d_bcount,
+                     plan_par(pl), pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels,
+                     pl->extra_rec >= 0 ? (int)pl->last_chrom : -1, pl->d_fsum, pl->d_fst, pl->d_ctr,
+                     (int)(pl->runs & 1), pl->d_leafsum, pl->d_bg1d, pl->sliced ? 1 : 0, pl->d_gscr, pl->nscr);
+}
+
 template <bool P16, bool FST, bool CNT>
 void launch_scan_g(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
   hipExtLaunchKernelGGL((k_scan_g<P16, FST, CNT>), dim3((unsigned)pl->chunks.size()), dim3(BLOCK), pl->scan_lds,
@@ -293,27 +298,20 @@ void launch_scan_gw(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
                      pl->d_ctr, (int)(pl->runs & 1), pl->d_leafsum, pl->d_bg1d, 0, pl->d_gscr, pl->nscr);
 }
 
-template <bool FUSED, int FST>
-void launch_scan_wl(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
-  hipExtLaunchKernelGGL((k_scan_wl<FUSED, FST>), dim3((unsigned)pl->chunks.size()), dim3(SBLOCK), pl->scan_lds,
-                     CTX_STREAM(pl->ctx), pl->kev[4], pl->kev[5], 0, pl->K, scan_src(pl), pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
-                     per_chrom, pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, bp, pl->d_repl, pl->d_bcount,
-                     plan_par(pl), pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels,
-                     pl->extra_rec >= 0 ? (int)pl->last_chrom : -1, pl->d_fsum, pl->d_fst, pl->d_ctr,
-                     (int)(pl->runs & 1), pl->d_leafsum, pl->d_bg1d, pl->sliced ? 1 : 0, pl->d_gscr, pl->nscr);
-}
-
 template <bool P16, bool CNT>
 hipError_t launch_scan_c(sfs2d_plan* pl, sfs2d_window* out) {
   const int per_chrom = pl->prm.bg_mode == SFS2D_BG_PER_CHROM ? 1 : 0;
   const int bp = pl->prm.window_mode == SFS2D_WINDOW_BP ? 1 : 0;
-  if (CNT && pl->lite) {
+  if (CNT && pl->w8) {
+    const int f = !pl->fst ? 0 : pl->fst_mask ? 5 : 4;
     if (pl->fused) {
-      if (pl->fst) launch_scan_wl<true, 2>(pl, out, per_chrom, bp);
-      else launch_scan_wl<true, 0>(pl, out, per_chrom, bp);
+      if (f == 0) launch_scan_w8<true, 0>(pl, out, per_chrom, bp);
+      else if (f == 4) launch_scan_w8<true, 4>(pl, out, per_chrom, bp);
+      else launch_scan_w8<true, 5>(pl, out, per_chrom, bp);
     } else {
-      if (pl->fst) launch_scan_wl<false, 2>(pl, out, per_chrom, bp);
-      else launch_scan_wl<false, 0>(pl, out, per_chrom, bp);
+      if (f == 0) launch_scan_w8<false, 0>(pl, out, per_chrom, bp);
+      else if (f == 4) launch_scan_w8<false, 4>(pl, out, per_chrom, bp);
+      else launch_scan_w8<false, 5>(pl, out, per_chrom, bp);
     }
     return hipGetLastError();
   }
@@ -514,7 +512,7 @@ int sfs2d_ctx_create(int device, sfs2d_ctx** out) {
   c->stream = c->own;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) c->ncu = prop.multiProcessorCount;
-  if (dalloc(c, &c->d_lnx, LNX_N) || dalloc(c, &c->d_df, 2 * LNT + 2 * RCPN + 2 * FSTAR)) {
+  if (dalloc(c, &c->d_lnx, LNX_N) || dalloc(c, &c->d_df, 2 * LNT + 2 * RCPN + 2 * PA_N)) {
     hipFree(c->d_lnx); hipStreamDestroy(c->own); delete c; return SFS2D_E_NOMEM;
   }
   hipLaunchKernelGGL(k_init_lnx, dim3(LNX_N / 256), dim3(256), 0, c->stream, c->d_lnx, c->d_df, c->d_df + LNT,
@@ -537,9 +535,17 @@ int sfs2d_ctx_destroy(sfs2d_ctx* ctx) {
   return 0;
 }
 
+// NULL is the HIP null stream (ordered with the process's blocking streams), not the ctx's own: a
+// caller passing its default stream's handle (torch's is 0) gets the ordering it expects
 int sfs2d_ctx_set_stream(sfs2d_ctx* ctx, void* stream) {
   if (!ctx) return SFS2D_E_ARG;
-  ctx->stream = stream ? (hipStream_t)stream : ctx->own;
+  ctx->stream = (hipStream_t)stream;
+  return 0;
+}
+
+int sfs2d_ctx_use_own_stream(sfs2d_ctx* ctx) {
+  if (!ctx) return SFS2D_E_ARG;
+  ctx->stream = ctx->own;
   return 0;
 }
 
@@ -927,7 +933,6 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
       // otherwise k_scan_g (a workgroup per window).  SFS2D_GW=0/1 forces one.
       const int h2w = ((K.nb2 + 3) / 4 + 3) & ~3;   // u8-packed 2D bins
       size_t gw_lds = (size_t)(h2w + R1GW * (K.n1p + 1) + R1GW * (K.n2p + 1) + TRASH) * 4;
-      if (const char* ev = std::getenv("SFS2D_GW_PAD")) gw_lds += (size_t)std::atoll(ev);   // occupancy experiments
       int occ = 0;
       if (gw_lds <= 160 * 1024) {
         const hipFuncAttribute A = hipFuncAttributeMaxDynamicSharedMemorySize;
@@ -986,31 +991,29 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
       if (hipFuncGetAttributes(&fa, f) != hipSuccess || pl->scan_lds + fa.sharedSizeBytes > 160 * 1024) pl->fst_scan = false;
     }
   }
-  // k_scan_wl (six waves per SIMD: u8 2D bins, 2 1D replicas, three workgroups per CU) for counts plans on
-  // the small-grid path whose Fst, if any, is summed in the scan: opt-in (SFS2D_LITE=1, where it can run
-  // the plan).  Measured slower than k_scan_w on config 3 (206 vs 177 us per pass with Fst,
-  // profiles/r04b_exp_lite.log), so not the default.
   const PwTree pw = pw_plan(K.nb2 - 3);
-  {
-    const bool can = pl->cnt && pl->G == WAVE && !pl->gw;
-    int occ_l = 0;
-    const char* ev = std::getenv("SFS2D_LITE");
-    if (can && ev && ev[0] == '1') {
-      const size_t lds_l = wl_lds_bytes(K.nb2, K.n1p, K.n2p, K.nt, (int)pw.leaves.size(), (int)pw.nodes.size(),
-                                        pl->fused ? 1 : 0, pl->sliced ? 1 : 0, pl->K.rtn);
-      const void* fl = pl->fused ? (pl->fst ? (const void*)k_scan_wl<true, 2> : (const void*)k_scan_wl<true, 0>)
-                                 : (pl->fst ? (const void*)k_scan_wl<false, 2> : (const void*)k_scan_wl<false, 0>);
-      if (lds_l > 64 * 1024) hipFuncSetAttribute(fl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)std::min<size_t>(lds_l, 160 * 1024));
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_l, fl, SBLOCK, lds_l) != hipSuccess) occ_l = 0;
-      (void)hipGetLastError();
-      pl->lite = occ_l >= 1;
-      if (pl->lite) {
-        pl->scan_lds = lds_l;
-        pl->fst_scan = pl->fst;   // Fst summed in the scan
-      }
+  pl->fst_mask = data->low_nc;
+  // k_scan_w8 for counts plans on the small-grid path whose Fst, if any, is summed in the scan: u8 2D
+  // bins (wrapped bytes re-evaluated exactly) leave LDS for Fst's (p, A) table by (n, a) -- two 16-B
+  // reads per SNP and no conversions or products.  Needs the data's called counts < 128
+  // (the table's rows, and the refs' bit 7 clear) and the workgroup to fit twice per CU beside its
+  // static LDS.  SFS2D_W8=0: k_scan_w (u16 bins, reciprocal table).
+  pl->w8 = false;
+  if (pl->cnt && pl->G == WAVE && !pl->gw && (!pl->fst || pl->fst_scan) && pl->K.rtn <= 128) {
+    const int h2w8 = ((K.nb2 + 3) / 4 + 3) & ~3;
+    const int per8 = h2w8 + w8_h1_words(K.n1p, K.n2p);
+    const size_t hist8 = std::max<size_t>((size_t)(SBLOCK / WAVE) * per8, (size_t)FUSED_VCNT + K.nt + 16);
+    const size_t pa = pl->fst ? (size_t)pl->K.rtn * (pl->K.rtn + 1) : 0;   // doubles: rtn (rtn + 1) / 2 (p, A) pairs
+    const size_t lds8 = sizeof(double) * (size_t)(((K.nt + 1) & ~1) + LDT8 + LNF + pa) + hist8 * 4;
+    hipFuncAttributes fa{};
+    const void* f = pl->fst ? (const void*)k_scan_w8<true, 5> : (const void*)k_scan_w8<true, 0>;
+    const size_t stat = hipFuncGetAttributes(&fa, f) == hipSuccess ? fa.sharedSizeBytes : 8192;
+    const char* ev = std::getenv("SFS2D_W8");
+    if (lds8 + stat <= 80 * 1024 && !(ev && ev[0] == '0')) {
+      pl->w8 = true;
+      pl->scan_lds = lds8;
     }
   }
-  pl->fst_mask = data->low_nc;
   pl->fst_win = pl->sliced && bp && pl->fst && !pl->fst_scan;
   pl->nfst = pl->fst_win ? (int)std::min<int64_t>(1024, std::max<int64_t>(1, (pl->nslots + 7) / 8)) : 0;   // ~1 window per wave
   if (pl->scan_lds > 64 * 1024) {
@@ -1028,6 +1031,8 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
                           (const void*)k_scan_w<true, false, 2, true>, (const void*)k_scan_w<false, false, 2, true>,
                           (const void*)k_scan_w<true, true, 3, true>, (const void*)k_scan_w<false, true, 3, true>,
                           (const void*)k_scan_w<true, false, 3, true>, (const void*)k_scan_w<false, false, 3, true>,
+                          (const void*)k_scan_w8<true, 0>, (const void*)k_scan_w8<true, 4>, (const void*)k_scan_w8<true, 5>,
+                          (const void*)k_scan_w8<false, 0>, (const void*)k_scan_w8<false, 4>, (const void*)k_scan_w8<false, 5>,
                           (const void*)k_scan_g<true, false, false>, (const void*)k_scan_g<false, false, false>,
                           (const void*)k_scan_g<true, true, false>, (const void*)k_scan_g<false, true, false>,
                           (const void*)k_scan_g<true, false, true>, (const void*)k_scan_g<false, false, true>,
@@ -1049,9 +1054,9 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
     int occ = 0;
     // (the grid is one dispatch wave of resident workgroups: occupancy of the variant that runs)
     hipError_t oe;
-    if (pl->lite)
-      oe = pl->fused ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_wl<true, 2>, SBLOCK, pl->scan_lds)
-                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_wl<false, 2>, SBLOCK, pl->scan_lds);
+    if (pl->w8)
+      oe = pl->fused ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w8<true, 5>, SBLOCK, pl->scan_lds)
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w8<false, 5>, SBLOCK, pl->scan_lds);
     else if (pl->gw)
       oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<true, true, true>, WAVE, pl->scan_lds)
                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<false, true, true>, WAVE, pl->scan_lds);
@@ -1071,8 +1076,8 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
     if (prm->scan_wgs_per_cu > 0 && (int)prm->scan_wgs_per_cu < occ) occ = (int)prm->scan_wgs_per_cu;
     int64_t cap = (int64_t)occ * ctx->ncu;
     if (pl->gw) pl->nscr = (int)cap;   // one exact-path histogram per resident wavefront
-    // k_scan_wl: exact evaluations are rare (|T| ~ 0, a wrapped u8 bin): a few shared slots, taken by CAS
-    if (pl->lite) pl->nscr = (int)std::min<int64_t>(256, cap * (SBLOCK / WAVE));
+    // k_scan_w8: exact evaluations are rare (|T| ~ 0, a wrapped u8 bin): a few shared slots, taken by CAS
+    if (pl->w8) pl->nscr = (int)std::min<int64_t>(256, cap * (SBLOCK / WAVE));
     if (const char* ev = std::getenv("SFS2D_WGS")) cap = std::max<int64_t>(1, std::atoll(ev));   // tuning
     const double S = (double)std::max<unsigned long long>(1, slot_base[nc] - slot_base[0]);
     const uint32_t NW = pl->gw ? 1u : (uint32_t)(SBLOCK / WAVE);   // wavefronts per workgroup
@@ -1149,10 +1154,8 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   }
   // one LDS copy per histogram word: four interleaved copies (lane & 3, fewer same-address atomics)
   // cost more in zeroing and flushing than they saved (k_prep config 2 10.3 vs 10.9 us, config 3
-  // 183 vs 187 us); SFS2D_HR=4 restores them where they fit
+  // 183 vs 187 us)
   pl->hr = 1;
-  if (const char* ev = std::getenv("SFS2D_HR"))
-    if (ev[0] == '4' && (size_t)K.nh * 4 * 4 <= 64 * 1024) pl->hr = 4;
   pl->bg_lds = ((size_t)K.nh * pl->hr + WAVE) * 4;   // + 64 lane trash words
   {
     // the LDS histogram must fit beside the static LDS of the k_prep variant that will run: the Fst
@@ -1197,8 +1200,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   pl->nnodes = (int)pw.nodes.size();
   pl->nlevels = pw.nlevels;
   if (pl->nleaves > PW_MAX_LEAVES) { delete pl; return set_err(ctx, SFS2D_E_ARG, "grid too large for the pairwise plan"); }
-  int lps = LEAVES_PER_SLICE;
-  if (const char* ev = std::getenv("SFS2D_LPS")) lps = std::max(1, std::min(LEAVES_PER_SLICE, std::atoi(ev)));   // tuning
+  const int lps = LEAVES_PER_SLICE;   // (1 / 2 / 4 leaves per slice measure the same, tools/lps_probe.sh)
   for (int j = 0; j < pl->nleaves; j += lps) {
     const int jl = std::min(pl->nleaves, j + lps);
     const int kb = j == 0 ? 0 : 1 + pw.leaves[j].x;
@@ -1218,8 +1220,8 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   rc = rc ? rc : dalloc(ctx, &pl->d_done, (size_t)pl->nbg);
   const size_t nctr = (size_t)2 * std::max(1, nc) * CTR_POOLS * CTR_STRIDE;
   rc = rc ? rc : dalloc(ctx, &pl->d_ctr, nctr);
-  const size_t ngscr = (pl->gw || pl->lite) ? (size_t)pl->nscr * (K.nb2 + 1) : 0;
-  if (pl->gw || pl->lite) rc = rc ? rc : dalloc(ctx, &pl->d_gscr, ngscr);
+  const size_t ngscr = (pl->gw || pl->w8) ? (size_t)pl->nscr * (K.nb2 + 1) : 0;
+  if (pl->gw || pl->w8) rc = rc ? rc : dalloc(ctx, &pl->d_gscr, ngscr);
   rc = rc ? rc : dalloc(ctx, &pl->d_bgval, (size_t)pl->nbg * K.nt);
   rc = rc ? rc : dalloc(ctx, &pl->d_tab, (size_t)pl->nbg * K.nt);
   rc = rc ? rc : dalloc(ctx, &pl->d_lp, (size_t)pl->nbg * K.nt);
@@ -1249,7 +1251,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_bcount, 0, sizeof(uint32_t) * 2 * std::max(1, nc), st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_done, 0, sizeof(uint32_t) * pl->nbg, st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_ctr, 0, sizeof(uint32_t) * nctr, st);
-  if (e == hipSuccess && (pl->gw || pl->lite)) e = hipMemsetAsync(pl->d_gscr, 0, sizeof(uint32_t) * ngscr, st);
+  if (e == hipSuccess && (pl->gw || pl->w8)) e = hipMemsetAsync(pl->d_gscr, 0, sizeof(uint32_t) * ngscr, st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_err, 0, 4 * sizeof(uint32_t), st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_bins, 0, sizeof(uint32_t) * nbins, st);
   if (e == hipSuccess && pl->fst) e = hipMemsetAsync(pl->d_fsum, 0, sizeof(unsigned long long) * 2 * ((size_t)pl->nslots + 1), st);
@@ -1345,8 +1347,8 @@ int sfs2d_plan_grids(const sfs2d_plan* pl, int64_t* prep_threads, int64_t* scan_
 
 const char* sfs2d_plan_scan_kernel(const sfs2d_plan* pl) {
   if (!pl) return nullptr;
-  if (pl->lite) return "k_scan_wl";
   if (pl->gw) return "k_scan_gw";
+  if (pl->w8) return "k_scan_w8";
   return pl->G == WAVE ? "k_scan_w" : "k_scan_g";
 }
 
@@ -1416,36 +1418,15 @@ int sfs2d_plan_run_streams(sfs2d_plan* const* plans, void* const* streams, sfs2d
       if (plans[j] == plans[k]) return set_err(ctx, SFS2D_E_ARG, "a plan may appear once (its per-run state is not shareable)");
   }
   // run i: plan i % nplans on stream i % nplans.  The plans' per-run state (bins, replicas, slots,
-  // counters) is their own, so consecutive runs on different streams overlap.  SFS2D_ENQ_THREADS=1
-  // (distinct streams): each plan's runs are enqueued by a host thread of its own (tl_stream: that
-  // thread's stream).  Off by default: config 2 with 3 streams is not host-bound (enqueue 10.7 us per
-  // pass on one thread, 9.1 threaded, vs 14.5 us per pass on the GPU): +1.5% at 400 passes, and the
-  // thread starts cost more than that in 20-pass runs (profiles/r02i_enqueue_probe.txt)
-  bool distinct = nplans > 1;
-  for (int k = 0; k < nplans && distinct; ++k)
-    for (int j = 0; j < k; ++j)
-      if (streams[j] == streams[k]) distinct = false;
-  const char* ev = std::getenv("SFS2D_ENQ_THREADS");
-  if (distinct && ev && ev[0] == '1') {
-    std::vector<int> rcs((size_t)nplans, 0);
-    std::vector<std::thread> th;
-    for (int k = 0; k < nplans; ++k)
-      th.emplace_back([&, k]() {
-        tl_stream = streams[k] ? (hipStream_t)streams[k] : ctx->own;
-        for (int i = k; i < nruns && !rcs[(size_t)k]; i += nplans)
-          rcs[(size_t)k] = sfs2d_plan_run_phase(plans[k], 0, outs ? outs[k] : nullptr);
-        tl_stream = nullptr;
-      });
-    for (auto& t : th) t.join();
-    for (int r : rcs)
-      if (r) return r;
-    return 0;
-  }
+  // counters) is their own, so consecutive runs on different streams overlap.  (One host thread
+  // enqueues: config 2 with 3 streams is not host-bound -- 10.7 us of enqueue per pass vs 14.5 us on
+  // the GPU; a thread per stream gained 1.5% at 400 passes and lost its thread starts in 20-pass runs,
+  // profiles/r02i_enqueue_probe.txt)
   hipStream_t saved = CTX_STREAM(ctx);
   int rc = 0;
   for (int i = 0; i < nruns && !rc; ++i) {
     const int k = i % nplans;
-    ctx->stream = streams[k] ? (hipStream_t)streams[k] : ctx->own;
+    ctx->stream = (hipStream_t)streams[k];   // (NULL: the null stream, as sfs2d_ctx_set_stream)
     rc = sfs2d_plan_run_phase(plans[k], 0, outs ? outs[k] : nullptr);
   }
   ctx->stream = saved;
@@ -1670,8 +1651,7 @@ int sfs2d_plan_attach(sfs2d_plan* base, const sfs2d_params* prm, sfs2d_plan** ou
   sfs2d_plan* a = nullptr;
   int rc = plan_create(ctx, base->data, prm, base->sliced ? 1 : 0, &a);
   if (rc) return rc;
-  if (a->fused != base->fused || a->sliced != base->sliced || a->G != base->G || a->cnt != base->cnt ||
-      a->lite != base->lite) {
+  if (a->fused != base->fused || a->sliced != base->sliced || a->G != base->G || a->cnt != base->cnt || a->w8 != base->w8) {
     plan_free(a); delete a;
     return set_err(ctx, SFS2D_E_ARG, "attached plan would take a different kernel path than its base");
   }
@@ -1824,218 +1804,6 @@ int sfs2d_scan(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* param
   sfs2d_plan_destroy(pl);
   ctx->err = keep;
   return rc;
-}
-
-}  // extern "C"
-
-// ------------------------------------------------------------------------------------------ multi-GPU
-// RCCL from native code: the per-step loop (scan, event, all-gather on the comm stream) is enqueued
-// here, not from Python, so a step costs the GPU's ~30 us and not the interpreter's ~60.  RCCL is
-// opened with dlopen (the process's torch has usually loaded librccl.so.1 already: the same copy is
-// used); the library itself has no link-time dependency on it.
-#include <dlfcn.h>
-#include <rccl/rccl.h>
-
-namespace {
-struct RcclApi {
-  bool ok = false;
-  std::string err;
-  decltype(&ncclGetUniqueId) get_id = nullptr;
-  decltype(&ncclCommInitRank) init_rank = nullptr;
-  decltype(&ncclCommDestroy) destroy = nullptr;
-  decltype(&ncclAllGather) all_gather = nullptr;
-  decltype(&ncclGather) gather = nullptr;   // (optional: an RCCL extension)
-  decltype(&ncclGetErrorString) errstr = nullptr;
-};
-
-RcclApi& rccl() {
-  static RcclApi api = [] {
-    RcclApi a;
-    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
-    if (!h) h = dlopen("librccl.so.1", RTLD_NOW);
-    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW);
-    if (!h) { a.err = std::string("cannot load librccl.so.1: ") + dlerror(); return a; }
-    a.get_id = reinterpret_cast<decltype(a.get_id)>(dlsym(h, "ncclGetUniqueId"));
-    a.init_rank = reinterpret_cast<decltype(a.init_rank)>(dlsym(h, "ncclCommInitRank"));
-    a.destroy = reinterpret_cast<decltype(a.destroy)>(dlsym(h, "ncclCommDestroy"));
-    a.all_gather = reinterpret_cast<decltype(a.all_gather)>(dlsym(h, "ncclAllGather"));
-    a.gather = reinterpret_cast<decltype(a.gather)>(dlsym(h, "ncclGather"));
-    a.errstr = reinterpret_cast<decltype(a.errstr)>(dlsym(h, "ncclGetErrorString"));
-    a.ok = a.get_id && a.init_rank && a.destroy && a.all_gather && a.errstr;
-    if (!a.ok) a.err = "librccl.so.1 lacks the expected symbols";
-    return a;
-  }();
-  return api;
-}
-}  // namespace
-
-struct sfs2d_dist {
-  sfs2d_ctx* ctx = nullptr;
-  ncclComm_t comm = nullptr;
-  int rank = 0, world = 1;
-  bool to_root = false;   // ncclGather to rank 0 (else ncclAllGather)
-  hipEvent_t ev_scan[2] = {nullptr, nullptr}, ev_comm[2] = {nullptr, nullptr};
-  std::vector<hipEvent_t> ev_k;   // sfs2d_dist_scan_gather_streams: per-stream scan events, per-parity gather events
-  bool gath_rec[2] = {false, false};   // ... whether the parity's gather event has been recorded (by any call)
-};
-
-extern "C" {
-
-int sfs2d_dist_unique_id(uint8_t* id128) {
-  if (!id128) return SFS2D_E_ARG;
-  RcclApi& r = rccl();
-  if (!r.ok) return set_err(nullptr, SFS2D_E_HIP, r.err);
-  ncclUniqueId id;
-  const ncclResult_t e = r.get_id(&id);
-  if (e != ncclSuccess) return set_err(nullptr, SFS2D_E_HIP, std::string("ncclGetUniqueId: ") + r.errstr(e));
-  std::memcpy(id128, id.internal, NCCL_UNIQUE_ID_BYTES);
-  return 0;
-}
-
-int sfs2d_dist_create(sfs2d_ctx* ctx, const uint8_t* id128, int rank, int world, sfs2d_dist** out) {
-  if (!ctx || !id128 || !out || world < 1 || rank < 0 || rank >= world) return set_err(ctx, SFS2D_E_ARG, "bad argument");
-  *out = nullptr;
-  RcclApi& r = rccl();
-  if (!r.ok) return set_err(ctx, SFS2D_E_HIP, r.err);
-  HIPCHK(ctx, hipSetDevice(ctx->device));
-  ncclUniqueId id;
-  std::memcpy(id.internal, id128, NCCL_UNIQUE_ID_BYTES);
-  sfs2d_dist* d = new sfs2d_dist();
-  d->ctx = ctx; d->rank = rank; d->world = world;
-  d->to_root = false;   // all-gather by default; gather-to-root opt-in (sfs2d_dist_set_gather)
-  if (const char* ev = std::getenv("SFS2D_GATHER")) d->to_root = r.gather != nullptr && std::strcmp(ev, "root") == 0;
-  const ncclResult_t e = r.init_rank(&d->comm, world, id, rank);
-  if (e != ncclSuccess) { delete d; return set_err(ctx, SFS2D_E_HIP, std::string("ncclCommInitRank: ") + r.errstr(e)); }
-  for (int b = 0; b < 2; ++b) {
-    if (hipEventCreateWithFlags(&d->ev_scan[b], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&d->ev_comm[b], hipEventDisableTiming) != hipSuccess) {
-      sfs2d_dist_destroy(d);
-      return set_err(ctx, SFS2D_E_HIP, "event creation failed");
-    }
-  }
-  *out = d;
-  return 0;
-}
-
-int sfs2d_dist_scan_gather(sfs2d_dist* d, sfs2d_plan* pl, void* out0, void* out1, void* gathered0, void* gathered1,
-                           int64_t rows, int64_t first_step, int nsteps, void* comm_stream) {
-  if (!d || !pl || !out0 || !out1 || !gathered0 || !gathered1 || rows < pl->nrec || nsteps < 0 || first_step < 0)
-    return set_err(d ? d->ctx : nullptr, SFS2D_E_ARG, "bad argument (rows must cover the plan's records)");
-  sfs2d_ctx* ctx = d->ctx;
-  if (pl->ctx != ctx) return set_err(ctx, SFS2D_E_ARG, "plan belongs to another context");
-  RcclApi& r = rccl();
-  HIPCHK(ctx, hipSetDevice(ctx->device));
-  // overlapped: gathers on comm_stream, ordered by events; serial (comm_stream NULL or the library's
-  // stream): each gather follows its scan on one stream, no events (measured on one GPU: the two
-  // cross-stream dependencies per step cost ~12 us, the serial one-rank gather ~2 us)
-  hipStream_t cs = comm_stream ? (hipStream_t)comm_stream : CTX_STREAM(ctx);
-  const bool overlap = cs != CTX_STREAM(ctx);
-  void* outs[2] = {out0, out1};
-  void* gath[2] = {gathered0, gathered1};
-  for (int i = 0; i < nsteps; ++i) {
-    const int b = (int)((first_step + i) & 1);
-    if (overlap && first_step + i >= 2) HIPCHK(ctx, hipStreamWaitEvent(CTX_STREAM(ctx), d->ev_comm[b], 0));   // table b is free
-    const int rc = sfs2d_plan_run(pl, static_cast<sfs2d_window*>(outs[b]));
-    if (rc) return rc;
-    if (overlap) {
-      HIPCHK(ctx, hipEventRecord(d->ev_scan[b], CTX_STREAM(ctx)));
-      HIPCHK(ctx, hipStreamWaitEvent(cs, d->ev_scan[b], 0));
-    }
-    const size_t bytes = (size_t)rows * sizeof(sfs2d_window);
-    const ncclResult_t e = d->to_root ? r.gather(outs[b], gath[b], bytes, ncclUint8, 0, d->comm, cs)
-                                      : r.all_gather(outs[b], gath[b], bytes, ncclUint8, d->comm, cs);
-    if (e != ncclSuccess)
-      return set_err(ctx, SFS2D_E_HIP, std::string(d->to_root ? "ncclGather: " : "ncclAllGather: ") + r.errstr(e));
-    if (overlap) HIPCHK(ctx, hipEventRecord(d->ev_comm[b], cs));
-  }
-  return 0;
-}
-
-int sfs2d_dist_scan_gather_streams(sfs2d_dist* d, sfs2d_plan* const* plans, void* const* streams, int nplans,
-                                   void* outbuf, void* gathered0, void* gathered1, int64_t rows, int nsteps) {
-  if (!d || !plans || !streams || !outbuf || !gathered0 || !gathered1 || nplans < 1 || nplans > 16 || nsteps < 0)
-    return set_err(d ? d->ctx : nullptr, SFS2D_E_ARG, "bad argument");
-  sfs2d_ctx* ctx = d->ctx;
-  for (int k = 0; k < nplans; ++k) {
-    if (!plans[k] || plans[k]->ctx != ctx || rows < plans[k]->nrec)
-      return set_err(ctx, SFS2D_E_ARG, "bad argument (plans of this ctx; rows must cover every plan's records)");
-    for (int j = 0; j < k; ++j)
-      if (plans[j] == plans[k] || streams[j] == streams[k])
-        return set_err(ctx, SFS2D_E_ARG, "plans and streams must be distinct");
-  }
-  RcclApi& r = rccl();
-  HIPCHK(ctx, hipSetDevice(ctx->device));
-  if ((int)d->ev_k.size() != 2 * nplans) {   // (another plan count: fresh events, after the earlier calls' work)
-    HIPCHK(ctx, hipDeviceSynchronize());
-    for (hipEvent_t e : d->ev_k) hipEventDestroy(e);
-    d->ev_k.clear();
-    d->gath_rec[0] = d->gath_rec[1] = false;
-  }
-  while ((int)d->ev_k.size() < 2 * nplans) {
-    hipEvent_t e = nullptr;
-    HIPCHK(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    d->ev_k.push_back(e);
-  }
-  // Steps in groups of nplans: in group g, plan k scans on streams[k] into table (g & 1) * nplans + k
-  // of outbuf; streams[0] waits for the group's other scans and gathers the group's tables (one
-  // collective, m * rows records per rank) into gathered[g & 1]; a stream k > 0 waits for the gather
-  // of group g - 2 (which read the tables it is about to overwrite).  One communicator, one stream
-  // for its collectives; cross-stream waits: 2 (nplans - 1) per group.
-  auto st = [&](int k) { return streams[k] ? (hipStream_t)streams[k] : ctx->own; };
-  hipStream_t saved = CTX_STREAM(ctx);
-  const size_t rec = sizeof(sfs2d_window);
-  void* gath[2] = {gathered0, gathered1};
-  // (a lambda: the HIPCHK early returns leave through the ctx-stream restore below)
-  const int rc = [&]() -> int {
-  int rc = 0;
-  for (int64_t g = 0, done = 0; done < nsteps && !rc; ++g) {
-    const int m = (int)std::min<int64_t>(nplans, nsteps - done);
-    const int par = (int)(g & 1);
-    char* base = static_cast<char*>(outbuf) + (size_t)par * nplans * rows * rec;
-    for (int k = 0; k < m && !rc; ++k) {
-      ctx->stream = st(k);
-      // a stream k > 0 overwrites the tables the parity's last gather read (this call's group g - 2, or a
-      // previous call's: enqueued calls need no host synchronisation between them)
-      if (k > 0 && d->gath_rec[par]) HIPCHK(ctx, hipStreamWaitEvent(st(k), d->ev_k[nplans + par], 0));
-      if ((rc = sfs2d_plan_run(plans[k], reinterpret_cast<sfs2d_window*>(base + (size_t)k * rows * rec)))) break;
-      if (k > 0) HIPCHK(ctx, hipEventRecord(d->ev_k[k], st(k)));
-    }
-    if (rc) break;
-    for (int k = 1; k < m; ++k) HIPCHK(ctx, hipStreamWaitEvent(st(0), d->ev_k[k], 0));
-    const size_t bytes = (size_t)m * rows * rec;
-    const ncclResult_t e = d->to_root ? r.gather(base, gath[par], bytes, ncclUint8, 0, d->comm, st(0))
-                                      : r.all_gather(base, gath[par], bytes, ncclUint8, d->comm, st(0));
-    if (e != ncclSuccess) {
-      rc = set_err(ctx, SFS2D_E_HIP, std::string(d->to_root ? "ncclGather: " : "ncclAllGather: ") + r.errstr(e));
-      break;
-    }
-    HIPCHK(ctx, hipEventRecord(d->ev_k[nplans + par], st(0)));
-    d->gath_rec[par] = true;
-    done += m;
-  }
-  return rc;
-  }();
-  ctx->stream = saved;
-  return rc;
-}
-
-int sfs2d_dist_set_gather(sfs2d_dist* d, int to_root) {
-  if (!d) return SFS2D_E_ARG;
-  if (to_root && !rccl().gather) return set_err(d->ctx, SFS2D_E_ARG, "the loaded RCCL has no ncclGather");
-  d->to_root = to_root != 0;
-  return 0;
-}
-
-int sfs2d_dist_destroy(sfs2d_dist* d) {
-  if (!d) return 0;
-  for (int b = 0; b < 2; ++b) {
-    if (d->ev_scan[b]) hipEventDestroy(d->ev_scan[b]);
-    if (d->ev_comm[b]) hipEventDestroy(d->ev_comm[b]);
-  }
-  for (hipEvent_t e : d->ev_k) hipEventDestroy(e);
-  if (d->comm) rccl().destroy(d->comm);
-  delete d;
-  return 0;
 }
 
 }  // extern "C"

@@ -57,11 +57,22 @@ constexpr int KBLOCK = 512;       // k_bg_slice workgroup
 constexpr int LNX_N = 1 << 20;    // ln(k) table for k < LNX_N (bin counts / window totals)
 constexpr int LNT = 512;          // D(r) and x ln x tables staged in LDS by k_scan_w
 constexpr int LNF = 256;          // k_scan_w: x ln x entries in LDS (x < LNF; the 1D pass and the flush, per window)
-// Fst's reciprocals (1/n, 1/(n(n-1))) in LDS (k_scan_w, k_scan_wl) for n <= 2 max(n1p, n2p): an even
+// Fst's reciprocals (1/n, 1/(n(n-1))) in LDS (k_scan_w) for n <= 2 max(n1p, n2p): an even
 // count of double2
 __host__ __device__ inline int wl_rtn(int n1p, int n2p) { return 2 * (n1p > n2p ? n1p : n2p) + 2; }
 constexpr int RCPN = 512;         // (1/k, 1/(k(k-1))) for k < 512 (Fst: called allele counts ref + alt <= 510), after the LNT tables
-constexpr int FSTAR = 65536;      // Fst per population and SNP: (p, A) by (alt, ref) = one u16 half of the counts word, after RCPN
+constexpr int PA_ROWS = 256;      // Fst per population and SNP: (p, A) = (a / n, a (a-1) / (n (n-1))) by (n, a), a <= n < PA_ROWS,
+constexpr int PA_N = PA_ROWS * (PA_ROWS + 1) / 2;   // row n at n (n + 1) / 2 (a triangle), after RCPN; (0, 0) for n < 2
+constexpr int LDT8 = 256;         // k_scan_w8: D(r) for u8 ranks r < 255 in LDS; D(255) = NaN marks a wrapped byte
+#ifndef SFS2D_W8_U1
+#define SFS2D_W8_U1 0
+#endif
+// k_scan_w8's per-wave 1D histogram words: (SFS2D_W8_U1) the UNFOLDED spectra, bins 0..2 pop_size in
+// two lane-&-1 replicas (an SNP's bin is its raw alt count: two operations per population; folded at
+// the window's end), else the folded bins 0..pop_size in R1 replicas
+__host__ __device__ inline int w8_h1_words(int n1p, int n2p) {
+  return SFS2D_W8_U1 ? 2 * (2 * n1p + 1) + 2 * (2 * n2p + 1) : 4 * (n1p + 1) + 4 * (n2p + 1);
+}
 constexpr int REPL = 4;           // replicas of the per-chromosome background histograms
 constexpr int PW_MAX_LEAVES = 1024;  // numpy pairwise leaves (64-128 values each): grids up to 255 x 255 (u8 counts)
 constexpr int LEAVES_PER_SLICE = 4;
@@ -131,7 +142,7 @@ struct KParams {
   uint32_t nm1;          // the data set's last SNP index (counts-reading scans clamp their row loads to it)
   uint32_t kmul;         // bytes (n2+1, 0, 1, 0): the 2D key x1*(n2+1) + x2 as one byte dot product
   uint32_t n12, lim12;   // u16 pairs (n1, n2), (n1p-1, n2p-1): both folded 1D bins in packed 16-bit ops
-  int rtn;               // Fst's (1/n, 1/(n(n-1))) entries in LDS (k_scan_w, k_scan_wl): n up to the data's
+  int rtn;               // Fst's (1/n, 1/(n(n-1))) entries in LDS (k_scan_w): n up to the data's
                          // largest called count (even; >= wl_rtn(n1p, n2p))
 };
 
@@ -504,19 +515,21 @@ __device__ __forceinline__ uint32_t bin_g2(uint32_t w) { return (w >> 23) & 0x7f
 
 // ln k for k < LNX_N; F(x) = x ln x for x < LNT; D(r) = F(r+1) - F(r) for r < LNT-1 and
 // D(LNT-1) = 0 (k_scan_w adds the ranks from LNT-1 on per bin, as F(x) - F(LNT-1))
-__global__ void k_init_lnx(double* lnx, double* dtab, double* ftab, double* rtab, double* artab) {
+__global__ void k_init_lnx(double* lnx, double* dtab, double* ftab, double* rtab, double* patab) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < LNX_N) lnx[i] = i ? log((double)i) : 0.0;
   if (i < RCPN) {   // Fst: (1/n, 1/(n(n-1))) per called allele count n; 0 below n = 2 (not in the set)
     rtab[2 * i] = i >= 2 ? 1.0 / (double)i : 0.0;
     rtab[2 * i + 1] = i >= 2 ? 1.0 / ((double)i * (double)(i - 1)) : 0.0;
   }
-  if (i < FSTAR) {   // Fst: one population's (p, A) = (a / n, a(a-1) / (n(n-1))) by i = a << 8 | r (n = r + a),
-                     // both 0 below n = 2 -- fst_snp's p and A, from the same reciprocals
-    const uint32_t a = (uint32_t)i >> 8, n = a + ((uint32_t)i & 0xffu);
-    const double r1 = n >= 2u ? 1.0 / (double)n : 0.0, r2 = n >= 2u ? 1.0 / ((double)n * (double)(n - 1u)) : 0.0;
-    artab[2 * i] = (double)a * r1;
-    artab[2 * i + 1] = (double)(a * (a - 1u)) * r2;
+  if (i < PA_N) {   // Fst: one population's (p, A) by the triangle index n (n + 1) / 2 + a (k_scan_w8 stages
+                    // rows n < P.rtn in LDS): both correctly rounded quotients of exact integers
+    uint32_t n = (uint32_t)((sqrt(8.0 * (double)i + 1.0) - 1.0) * 0.5);
+    while (n * (n + 1u) / 2u > (uint32_t)i) --n;
+    while ((n + 1u) * (n + 2u) / 2u <= (uint32_t)i) ++n;
+    const uint32_t a = (uint32_t)i - n * (n + 1u) / 2u;
+    patab[2 * i] = n >= 2u ? (double)a / (double)n : 0.0;
+    patab[2 * i + 1] = n >= 2u ? (double)(a * (a - 1u)) / (double)(n * (n - 1u)) : 0.0;
   }
   if (i < LNT) {
     const double a = i ? (double)i * log((double)i) : 0.0;
@@ -668,10 +681,6 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
     const unsigned long long qn = fst_fixed(num, P.fst_scale), qd = fst_fixed(den, P.fst_scale);
     if ((qn | qd) == 0ull) return;
     const uint32_t j = wid - wlo;
-#ifdef SFS2D_EXP_NOATOM
-    if (qn == 0x123456789ull && qd == 7ull) sh_fst[j & 7] = qn;   // experiment: no atomics
-    return;
-#endif
     if (j < (uint32_t)FST_LDS) {
       atomicAdd(&sh_fst[2 * (j * FST_R + frep)], qn);
       atomicAdd(&sh_fst[2 * (j * FST_R + frep) + 1], qd);
@@ -835,11 +844,7 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         double nk, dk;
-#ifdef SFS2D_EXP_FSTCONST
-        nk = (double)(cc[k] & 1u); dk = fm[k] ? 1.0 : 0.0;   // experiment: no term arithmetic
-#else
         fst_snp(cc[k], fm[k], sh_rcp, nk, dk);
-#endif
         if (k && fw[k] != wc) {
           fst_add(wc, sn, sd);
           sn = 0.0; sd = 0.0; wc = fw[k];
@@ -1640,7 +1645,7 @@ __device__ __forceinline__ void fused_table(int nb2, int nh, int nt, int n1p, in
   double* p1b = scr + 392;           // 128
   double* acc8 = scr + 512;          // 8 per leaf (<= 128 leaves)
   // lsum: leaf sums and tree nodes (nleaves + nnodes); vcnt: the table's counts (2D, then folded 1D),
-  // nt words -- both in HB past acc8 (k_scan_w: fixed offsets; k_scan_wl: packed after this grid's leaves)
+  // nt words -- both in HB past acc8 (fixed offsets)
   const double B2 = (double)bcount[(size_t)par * nchrom + chrom];
   const int4 my_node = tid < nnodes ? nodes[tid] : make_int4(0, 0, -1, 0);
   const int2 my_leaf = tid < nleaves ? leaves[tid] : make_int2(0, 0);   // this thread's leaf to combine
@@ -2367,11 +2372,22 @@ __device__ __forceinline__ void lds_copy_d(double* dst, const double* __restrict
 // membership = an inner 2D bin; the unfolded last bin in the rare pass), fp64 lane sums in a fixed order
 // and two wave sums per window: k_prep then runs without the Fst work (DESIGN.md "Fst placement");
 // 3: as 2, for data sets where some SNP has < 2 called alleles in a population (those SNPs masked out)
-template <bool P16, bool FUSED, int FST, bool CNT>
+// P8 (k_scan_w8, counts plans): the 2D bins u8-packed (a quarter of u32 bins: 652 words at 51 x 51
+// instead of u16's 1,304), which frees the LDS for FST 4 / 5: Hudson's per-population (p, A) read from
+// an LDS table by (n, a) -- one 16-B read per population and SNP, no conversions or products -- instead
+// of (1/n, 1/(n(n-1))) times a and a (a-1).  A 2D atomic returning rank 255 means the byte wrapped (the
+// bin's 256th SNP of the window; the carry corrupts a neighbour): D(255) is NaN, so the window's 2D sum
+// is NaN and the flush re-evaluates it exactly on a u32 histogram in global memory (gscr, as k_scan_gw).
+// Ranks never pass 254 otherwise, so no window needs the clamped D pass of the u16 bins.
+template <bool P16, bool FUSED, int FST, bool CNT, bool P8 = false>
 __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   constexpr bool FSTIN = FST >= 2;
-  constexpr bool FMASK = FST == 3;
+  constexpr bool FMASK = FST == 3 || FST == 5;
+  constexpr bool PA = FST >= 4;
   static_assert(!FSTIN || CNT, "Fst in the scan reads the counts");
+  static_assert(!P8 || (CNT && !P16), "u8-packed 2D bins: counts plans");
+  static_assert(!PA || P8, "the (p, A) table takes the LDS the u8 bins free");
+  constexpr int DT = P8 ? LDT8 : LNT;   // D(r) entries in LDS
   constexpr int NWV = SBLOCK / WAVE;
   constexpr int SB = 8;    // windows per batch (see flush; LDS-limited: the 2 KB of the retired trash words)
   __shared__ BgHead sh_hb;
@@ -2389,18 +2405,21 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   // LDS: lp table (nt, rounded up to even: the histograms are 16-B aligned) | D (LNT) | F (LNF) |
   // FSTIN: Fst's (1/n, 1/(n(n-1))) for n < P.rtn | histograms
   double* LPl = ldsd;
-  double* Dt = LPl + ((P.nt + 1) & ~1);   // LNT
-  double* Ft = Dt + LNT;                  // LNF
+  double* Dt = LPl + ((P.nt + 1) & ~1);   // DT
+  double* Ft = Dt + DT;                   // LNF
   double2* RT = reinterpret_cast<double2*>(Ft + LNF);
-  const int rtn = FSTIN ? P.rtn : 0;
+  // FSTIN: rtn (1/n, 1/(n(n-1))) pairs, or (PA) the (p, A) triangle of rows n < P.rtn
+  const int rtn = FSTIN ? (PA ? P.rtn * (P.rtn + 1) / 2 : P.rtn) : 0;
   uint32_t* HB = reinterpret_cast<uint32_t*>(RT + rtn);
-  const int h2w = P16 ? ((P.nb2 + 1) / 2 + 3) & ~3 : (P.nb2 + 3) & ~3;
-  const int h1w = R1 * (P.n1p + 1), h1wb = R1 * (P.n2p + 1);
+  const int h2w = P8 ? ((P.nb2 + 3) / 4 + 3) & ~3 : P16 ? ((P.nb2 + 1) / 2 + 3) & ~3 : (P.nb2 + 3) & ~3;
+  constexpr bool U1 = P8 && SFS2D_W8_U1;   // unfolded 1D spectra (w8_h1_words)
+  constexpr int R1U = U1 ? 2 : R1;         // 1D replicas per bin
+  const int h1w = U1 ? 2 * (P.n1 + 1) : R1 * (P.n1p + 1), h1wb = U1 ? 2 * (P.n2 + 1) : R1 * (P.n2p + 1);
   const int per = h2w + h1w + h1wb;   // (no trash words: SNPs outside the 2D SFS skip the atomic)
   uint32_t* W = HB + wv * per;
   uint32_t* H1a = W + h2w;
   uint32_t* H1b = H1a + h1w;
-  const uint32_t rep = lane & (R1 - 1);
+  const uint32_t rep = lane & (R1U - 1);
 
   // a window's first 8 rows, loaded unconditionally and range-checked (a window that is not there --
   // live false, or an empty slot -- reads a 0-byte range: zeros, no memory access): issued behind a
@@ -2448,8 +2467,12 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   // of config 2's ~4 us prologue): the D / F tables (two doubles per thread), and for sliced plans the
   // leaf sums, the tree nodes and the head's inputs, then the lp table
   static_assert(LNT == SBLOCK && LNF <= SBLOCK, "one D and at most one F double per thread");
-  const double dfv0 = dfg[tid], dfv1 = tid < LNF ? dfg[LNT + tid] : 0.0;
-  const double2 rtv = (FSTIN && tid < rtn) ? reinterpret_cast<const double2*>(dfg + 2 * LNT)[tid] : make_double2(0.0, 0.0);
+  const double dfv0 = P8 && tid == LDT8 - 1 ? __builtin_nan("") : dfg[tid], dfv1 = tid < LNF ? dfg[LNT + tid] : 0.0;
+  const double2 rtv = (FSTIN && !PA && tid < rtn) ? reinterpret_cast<const double2*>(dfg + 2 * LNT)[tid] : make_double2(0.0, 0.0);
+  auto stage_fst = [&]() {   // Fst's LDS table
+    if (PA) lds_copy_d(reinterpret_cast<double*>(RT), dfg + 2 * LNT + 2 * RCPN, 2 * rtn);
+    else if (FSTIN && tid < rtn) RT[tid] = rtv;
+  };
   BgHead hb;
   const size_t rs = (size_t)P.nchrom * P.nh;     // replica stride
   const uint32_t* Rc = repl + (size_t)par * REPL * rs + (size_t)ch.chrom * P.nh;
@@ -2464,9 +2487,9 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       if (tid == 0) { bc = bcount[(size_t)par * P.nchrom + bg]; o = bg1d[bg]; }
     }
     lds_copy_d(LPl, LPg + (size_t)bg * P.nt, P.nt);
-    Dt[tid] = dfv0;
+    if (tid < DT) Dt[tid] = dfv0;
     if (tid < LNF) Ft[tid] = dfv1;
-    if (FSTIN && tid < rtn) RT[tid] = rtv;
+    stage_fst();
     if (sliced) {
       // this run's per-chromosome table from k_bg_slice (proportions, logs, 1D part final) and its
       // leaf sums: numpy's tree over the leaves, then scipy's p[-1] rule on the 2D table -- the
@@ -2509,9 +2532,9 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       hb = head[bg];
     }
   } else {
-    Dt[tid] = dfv0;
+    if (tid < DT) Dt[tid] = dfv0;
     if (tid < LNF) Ft[tid] = dfv1;
-    if (FSTIN && tid < rtn) RT[tid] = rtv;
+    stage_fst();
     fused_table(P.nb2, P.nh, P.nt, P.n1p, P.n2p, P.n1, P.n2, P.t1a, P.t1b, P.nchrom, ch.chrom,
                 ch.first == 0 && (int)ch.chrom == write_chrom, bg,
                 Rc, rs, repl, bcount, par, tab, LPg, head, LPl, HB, leaves, nleaves, nodes, nnodes, nlevels, lnx,
@@ -2574,10 +2597,11 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     w.t2d = 2.0 * (B2 - xlnx<LNF>(w.n2, Ft, lnx));
     w.t1a = 2.0 * (Ba - xlnx<LNF>(w.n1a, Ft, lnx));
     w.t1b = 2.0 * (Bb - xlnx<LNF>(w.n1b, Ft, lnx));
-    // |T| this small may be an exactly proportional window: the exact evaluation below
+    // |T| this small may be an exactly proportional window: the exact evaluation below (P8: also a
+    // window whose 2D sum is NaN -- a u8 bin wrapped -- unless the background makes T2D NaN anyway)
     const bool exact = mine && !empty &&
-                       (nsnp == 0xffffu || suspect_zero(w.t2d, w.n2) || suspect_zero(w.t1a, w.n1a) ||
-                        suspect_zero(w.t1b, w.n1b));
+                       (nsnp == 0xffffu || (P8 && !nan2 && B2 != B2) || suspect_zero(w.t2d, w.n2) ||
+                        suspect_zero(w.t1a, w.n1a) || suspect_zero(w.t1b, w.n1b));
     if (nan2) w.t2d = __builtin_nan("");
     if (nan1a) w.t1a = __builtin_nan("");
     if (nan1b) w.t1b = __builtin_nan("");
@@ -2609,13 +2633,35 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       const uint32_t xn = __builtin_amdgcn_readlane(Bnv, l) & 0xffffu;
       const uint32_t xe = xn != 0xffffu ? xb + xn : (mode_bp ? slots[xs].y : xb + P.ws);
       WinOut x;
-      if (FUSED)
+      if (P8) {
+        // a u32 histogram in global memory: a gscr slot taken by CAS (nscr slots of nb2 words, then nscr
+        // lock words), left clean by the take-and-clear evaluation
+        uint32_t* lock = gscr + (size_t)nscr * P.nb2;
+        uint32_t sl = (uint32_t)(blockIdx.x * NWV + wv) % (uint32_t)nscr;
+        for (;;) {
+          uint32_t got = 1u;
+          if (lane == 0) got = atomicCAS(&lock[sl], 0u, 1u);
+          if (__builtin_amdgcn_readfirstlane(got) == 0u) break;
+          sl = sl + 1u == (uint32_t)nscr ? 0u : sl + 1u;
+        }
+        uint32_t* H2g = gscr + (size_t)sl * P.nb2;
+        if (FUSED)
+          x = eval_exact<WAVE, false, R1U, CNT>(P, bins, xb, xe,
+                                               TabFused{LPl, Rc, rs, P.nb2, P.n1, P.n2, P.n1p, P.h1a, P.h1b, P.t1a, P.t1b},
+                                               hb, lnx, H2g, H1a, H1b, nullptr, nullptr);
+        else
+          x = eval_exact<WAVE, false, R1U, CNT>(P, bins, xb, xe, TabLocal{tab + (size_t)bg * P.nt, LPl}, hb, lnx, H2g,
+                                               H1a, H1b, nullptr, nullptr);
+        __threadfence();   // the slot's words are clean again before it is released
+        if (lane == 0) atomicExch(&lock[sl], 0u);
+      } else if (FUSED) {
         x = eval_exact<WAVE, P16, R1, CNT>(P, bins, xb, xe,
                                       TabFused{LPl, Rc, rs, P.nb2, P.n1, P.n2, P.n1p, P.h1a, P.h1b, P.t1a, P.t1b}, hb,
                                       lnx, W, H1a, H1b, nullptr, nullptr);
-      else
+      } else {
         x = eval_exact<WAVE, P16, R1, CNT>(P, bins, xb, xe, TabLocal{tab + (size_t)bg * P.nt, LPl}, hb, lnx, W, H1a, H1b,
                                       nullptr, nullptr);
+      }
       if (lane == 0) {
         write_rec(out + xs, ch.chrom, ch.wid_lo + (xs - ch.slot_lo), xb, xe, x, zflags);
         atomicAdd(err_word + 1, 1u);   // statistics: windows that took the exact path
@@ -2708,7 +2754,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     // trash word: 2 KB of LDS per workgroup, now the batch's).  n2 is a wave-uniform ballot count.
     const uint32_t nsnp = cur.e - cur.b;
     const int lim = (int)nsnp - lane;
-    const bool clampd = nsnp > (uint32_t)(LNT - 1);   // some rank may pass the D table
+    const bool clampd = !P8 && nsnp > (uint32_t)(LNT - 1);   // some rank may pass the D table (u8: NaN at 255 instead)
     double acc2 = 0.0;
     // FSTIN: this lane's sums of A1 + A2, p1 + p2 and p1 p2 (fst_snp's num = A1 + A2 - 2 p1 p2,
     // den = p1 + p2 - 2 p1 p2, summed per part).  Every SNP takes part: those outside the 2D SFS --
@@ -2729,6 +2775,26 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           const uint32_t w = ww[q];
+          if (PA) {
+            // entry n (n + 1) / 2 + a of the triangle: byte offset 8 (n (n + 1) + 2 a), n (n + 1) by one
+            // 24-bit multiply-add of the two byte dot products (n, n + 1); 2 a straight from the word (the
+            // refs' bit 7 is 0: called counts < 128 on this path)
+            const uint32_t n1c = __builtin_amdgcn_udot4(w, 0x00000101u, 0u, false);
+            const uint32_t n1d = __builtin_amdgcn_udot4(w, 0x00000101u, 1u, false);
+            const uint32_t n2c = __builtin_amdgcn_udot4(w, 0x01010000u, 0u, false);
+            const uint32_t n2d = __builtin_amdgcn_udot4(w, 0x01010000u, 1u, false);
+            uint32_t t1 = __builtin_amdgcn_ubfe(w, 7, 9), t2 = w >> 23;
+            if (FMASK) {
+              const bool ok = min(n1c, n2c) >= 2u;
+              t1 = ok ? t1 : 0u;
+              t2 = ok ? t2 : 0u;
+            }
+            const d2v e1 = *(const lds_d2*)(uintptr_t)(rtb + 8u * (__umul24(n1c, n1d) + t1));
+            const d2v e2 = *(const lds_d2*)(uintptr_t)(rtb + 8u * (__umul24(n2c, n2d) + t2));
+            fq[2 * q] = make_double2(e1.x, e1.y);
+            fq[2 * q + 1] = make_double2(e2.x, e2.y);
+            continue;
+          }
           const uint32_t n1c = __builtin_amdgcn_udot4(w, 0x00000101u, 0u, false);
           const uint32_t n2c = __builtin_amdgcn_udot4(w, 0x01010000u, 0u, false);
           uint32_t a1 = __builtin_amdgcn_ubfe(w, 8, 8), a2 = w >> 24;
@@ -2739,22 +2805,8 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
           }
           // (a and a (a - 1) converted here: an LDS table of them, two more LDS reads per SNP, made the
           // pass slower -- 143 -> 158 us on config 3: the loop's LDS pipe is the busier one)
-#ifdef SFS2D_FST_VALU_RCP   // experiment: the reciprocals by v_rcp_f64 + one Newton step, no LDS reads
-          auto rcp2 = [](uint32_t n) {
-            const double nd = (double)max(n, 2u), md = fma(nd, nd, -nd);   // n (n - 1), exact
-            double x = __builtin_amdgcn_rcp(nd), y = __builtin_amdgcn_rcp(md);
-            x = fma(x, fma(-nd, x, 1.0), x);
-            y = fma(y, fma(-md, y, 1.0), y);
-            d2v r;
-            r.x = x;
-            r.y = y;
-            return r;
-          };
-          const d2v r1 = rcp2(n1c), r2 = rcp2(n2c);
-#else
           const d2v r1 = *(const lds_d2*)(uintptr_t)(rtb + 16u * n1c);
           const d2v r2 = *(const lds_d2*)(uintptr_t)(rtb + 16u * n2c);
-#endif
           fq[2 * q] = make_double2((double)a1 * r1.x, (double)__umul24(a1, a1 - 1u) * r1.y);
           fq[2 * q + 1] = make_double2((double)a2 * r2.x, (double)__umul24(a2, a2 - 1u) * r2.y);
         }
@@ -2774,11 +2826,12 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
         else { k2 = bin_k2(w); gp = (bin_g1(w) | (bin_g2(w) << 16)) * (4u * R1); }
         in2[q] = k2 != 0u;   // (one compare: the ballot, the atomic's exec mask, the rank's select)
         n2 += __popcll(__ballot(in2[q]));
-        const uint32_t x = (CNT ? k2 : w) << 4;   // low five bits: (k2 & 1) << 4, the u16 half's shift
-        const uint32_t word = P16 ? (k2 >> 1) : k2;   // (k2 = 0: word 0, cleared after the window anyway)
+        // low five bits: (k2 & 1) << 4, the u16 half's shift (P8: (k2 & 3) << 3, the byte's)
+        const uint32_t x = (CNT ? k2 : w) << (P8 ? 3 : 4);
+        const uint32_t word = P8 ? (k2 >> 2) : P16 ? (k2 >> 1) : k2;   // (k2 = 0: word 0, cleared after the window anyway)
         // (v_lshlrev_b32 / v_bfe_u32 read the shift's low five bits: no mask; C's << would need one)
         uint32_t one2 = 1u;
-        if (P16) asm("v_lshlrev_b32 %0, %1, 1" : "=v"(one2) : "v"(x));
+        if (P16 || P8) asm("v_lshlrev_b32 %0, %1, 1" : "=v"(one2) : "v"(x));
         // an SNP outside the 2D SFS skips the atomic (exec mask; its rank is 0 below): no trash word,
         // fewer lanes in the LDS atomic.  (The address before the branch: one v_lshl_add.)
         const uint32_t wa = awb + word * 4u;
@@ -2791,7 +2844,9 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
         if (keep) kw[(j + q) & 7] = word;
         // every SNP slot adds to one bin of each folded 1D spectrum (no range test, no trash select: the
         // window's end drops bins 0 and n_p and counts n1a / n1b from them)
-        const uint32_t u1 = a1b + (gp & 0xffffu), u2 = a2b + (gp >> 16);
+        // (U1: the raw alt counts' bins, 8 B apart: two operations per population)
+        const uint32_t u1 = U1 ? a1b + (__builtin_amdgcn_ubfe(w, 8, 8) << 3) : a1b + (gp & 0xffffu);
+        const uint32_t u2 = U1 ? a2b + ((w >> 24) << 3) : a2b + (gp >> 16);
         __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u1, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u2, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -2816,13 +2871,14 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       // the ranks once both SNPs' atomics are issued (extracted right after its own atomic, each rank's
       // wait held the other SNP's work back: two LDS round trips per pair instead of one)
 #pragma unroll
-      for (int q = 0; q < 2; ++q) rk[q] = in2[q] ? (P16 ? __builtin_amdgcn_ubfe(ov[q], xs[q], 16) : ov[q]) : 0u;
+      for (int q = 0; q < 2; ++q)
+        rk[q] = in2[q] ? (P8 ? __builtin_amdgcn_ubfe(ov[q], xs[q], 8) : P16 ? __builtin_amdgcn_ubfe(ov[q], xs[q], 16) : ov[q]) : 0u;
       double d[2], lp[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         // D[LNT-1] = 0: ranks past the table add 0 (clampd windows); elsewhere rank < nsnp <= LNT-1 and
-        // the min is a no-op, cheaper than selecting it per window
-        d[q] = Dt[min(rk[q], (uint32_t)LNT - 1u)];
+        // the min is a no-op, cheaper than selecting it per window (P8: ranks <= 255, D(255) = NaN)
+        d[q] = P8 ? Dt[rk[q]] : Dt[min(rk[q], (uint32_t)LNT - 1u)];
         lp[q] = LPl[kk[q]];
       }
       const double t = (d[0] - lp[0]) + (d[1] - lp[1]);
@@ -2915,15 +2971,33 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     // (counting only the live slots -- a partial row's live lanes, no row past the end -- measured 1%
     // slower: its uniform tests cost more than the same-address atomics of the padding)
     const uint32_t slots = 128u * ((nsnp + 127u) / 128u);
+    // folded bin k (<= n_p) of a population's spectrum, its replicas read and cleared (U1: fold_1d_sfs's
+    // u[k] + u[n - k], k < n_p, from the unfolded bins)
+    auto take1 = [&](uint32_t* H, int k, int np, int n) -> uint32_t {
+      if (U1) {
+        uint2* q = reinterpret_cast<uint2*>(H + 2 * k);
+        const uint2 v = *q;
+        *q = make_uint2(0u, 0u);
+        uint32_t x = v.x + v.y;
+        if (k < np) {
+          uint2* r = reinterpret_cast<uint2*>(H + 2 * (n - k));
+          const uint2 u = *r;
+          *r = make_uint2(0u, 0u);
+          x += u.x + u.y;
+        }
+        return x;
+      }
+      uint4* q = reinterpret_cast<uint4*>(H + k * R1);
+      const uint4 v = *q;
+      *q = make_uint4(0, 0, 0, 0);
+      return (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
+    };
     if (half1d) {
       const bool pa = lane < 32;
       const int k = lane & 31, np = pa ? P.n1p : P.n2p;
       uint32_t x = 0;
       if (k <= np) {
-        uint4* q = reinterpret_cast<uint4*>((pa ? H1a : H1b) + k * R1);
-        const uint4 v = *q;
-        *q = make_uint4(0, 0, 0, 0);
-        x = (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
+        x = take1(pa ? H1a : H1b, k, np, pa ? P.n1 : P.n2);
         if (k >= 1 && k < np && x) acca = xlnx<LNF>(x, Ft, lnx) - (double)x * LPl[(pa ? P.t1a : P.t1b) + k];
       }
       n1a = slots - (uint32_t)__builtin_amdgcn_readlane((int)x, 0) - (uint32_t)__builtin_amdgcn_readlane((int)x, P.n1p);
@@ -2935,18 +3009,12 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       for (int j = 0; j < 2; ++j) {
         const int k = lane + WAVE * j;
         if (k <= P.n1p) {
-          uint4* q = reinterpret_cast<uint4*>(H1a + k * R1);
-          const uint4 v = *q;
-          *q = make_uint4(0, 0, 0, 0);
-          const uint32_t x = (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
+          const uint32_t x = take1(H1a, k, P.n1p, P.n1);
           xa[j] = x;
           if (k >= 1 && k < P.n1p && x) acca += xlnx<LNF>(x, Ft, lnx) - (double)x * LPl[P.t1a + k];
         }
         if (k <= P.n2p) {
-          uint4* q = reinterpret_cast<uint4*>(H1b + k * R1);
-          const uint4 v = *q;
-          *q = make_uint4(0, 0, 0, 0);
-          const uint32_t x = (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
+          const uint32_t x = take1(H1b, k, P.n2p, P.n2);
           xb[j] = x;
           if (k >= 1 && k < P.n2p && x) accb += xlnx<LNF>(x, Ft, lnx) - (double)x * LPl[P.t1b + k];
         }
@@ -3000,544 +3068,18 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   BLK_STAMP(1, 1);
 }
 
-// ------------------------------------------------------------------------------------------ K3, lite
-// k_scan_wl: the window scan of counts plans on small grids (no filter: the scan classifies the
-// counts it streams; Fst summed in the scan or off), laid out for SIX wavefronts per SIMD -- three
-// 512-thread workgroups per CU and <= 80 VGPRs -- where k_scan_w (two workgroups, 128 VGPRs) runs
-// four: that kernel waits on memory / LDS for ~55% of its wave cycles on config 3
-// (profiles/r03x_pmc_config3_fst.csv).  Per workgroup: the background's lp table, D(r) for r < 256,
-// and per wavefront its 2D histogram with u8-packed bins (a quarter of u32 bins: 652 words at 51 x 51)
-// and two lane-&-1 replicas of each folded 1D spectrum.  A rank of 255 returned by a 2D atomic means
-// the byte wrapped (>= 256 SNPs of the window in one bin): the window is re-evaluated exactly, on a
-// u32 histogram in global memory (gscr, as k_scan_gw), like windows of >= 65535 SNPs and windows whose
-// |T| is ~0 (the exact-zero rule).  Window schedule three deep: at window i's start the rows of window
-// i+1 are issued (its slot record arrived during window i-1), the slot record of window i+2 is loaded
-// (its pool index arrived during window i-1) and the pool atomic for window i+3 issued, so a window's
-// rows have a whole window's time to arrive from HBM.  The window loop, the batched finish (8 windows
-// per flush, evaluated per lane) and the numerics are k_scan_w's.
-constexpr int LDT = 256;   // D(r) in LDS: u8 ranks (255 = the byte wrapped)
-constexpr int R1L = 2;     // folded 1D replicas per bin (lane & 1)
-
-__host__ __device__ inline int wl_h2w(int nb2) { return ((nb2 + 3) / 4 + 3) & ~3; }   // u8-packed 2D words, 16-B rows
-__host__ __device__ inline int wl_per(int nb2, int n1p, int n2p) {                     // words per wavefront
-  return (wl_h2w(nb2) + R1L * (n1p + 1) + R1L * (n2p + 1) + 3) & ~3;
-}
-// fused prologue scratch in the histogram area (fused_table): u1 words [0, 512) | p1a, p1b (doubles
-// 264.., 392..) | acc8 (double 512, 8 per leaf) | lsum (leaves + nodes) | vcnt (nt words)
-__host__ __device__ inline int wl_lsum_off(int nleaves) { return 512 + 8 * nleaves; }   // doubles
-__host__ __device__ inline int wl_vcnt_off(int nleaves, int nnodes) {                  // words (16-B aligned)
-  return (2 * (wl_lsum_off(nleaves) + nleaves + nnodes) + 3) & ~3;
-}
-// words of a workgroup's histogram area: the 8 wavefronts', or the prologue's scratch if larger
-__host__ __device__ inline int wl_hb_words(int nb2, int n1p, int n2p, int nt, int nleaves, int nnodes, int fused,
-                                           int sliced) {
-  int w = (SBLOCK / WAVE) * wl_per(nb2, n1p, n2p);
-  if (fused) w = w > wl_vcnt_off(nleaves, nnodes) + nt + 16 ? w : wl_vcnt_off(nleaves, nnodes) + nt + 16;
-  if (sliced) w = w > 2 * (nleaves + nnodes) ? w : 2 * (nleaves + nnodes);
-  return w;
-}
-// LDS bytes of a k_scan_wl workgroup besides its static arrays: lp | D | Fst reciprocals | histogram area
-__host__ __device__ inline size_t wl_lds_bytes(int nb2, int n1p, int n2p, int nt, int nleaves, int nnodes, int fused,
-                                               int sliced, int rtn) {
-  return sizeof(double) * (size_t)(((nt + 1) & ~1) + LDT + 2 * rtn) +
-         4 * (size_t)wl_hb_words(nb2, n1p, n2p, nt, nleaves, nnodes, fused, sliced);
-}
-
-// what only the batch finish and the exact path read, parked in LDS for the window loop's duration (read
-// back behind a compiler barrier): kept in scalar registers, these values and the kernel arguments they
-// come from spilled the loop's own to VGPR lanes (v_readlane / v_writelane inside the loop)
-struct WlCold {
-  KParams P;
-  sfs2d_window* out;
-  double* fst_out;
-  uint32_t* err_word;
-  uint32_t* gscr;
-  const PL* tab;          // this chromosome's background table (global)
-  const uint32_t* Rc;     // this chromosome's replicas (fused plans)
-  unsigned long long rs;  // replica stride
-  BgHead hb;
-  uint32_t chrom, wid_lo, slot_lo, nscr, zflags, nanf;
-};
-
-// k_scan_wl's exact re-evaluation of one window (rare), out of line: its register needs stay out of the
-// window loop's allocation (live values are saved around the call only when it runs).  A u32 histogram in
-// global memory (a gscr slot taken by CAS, as k_scan_gw), the folded 1D spectra in the wave's LDS replicas
-// (stride R1L, clean before and after); the record written by lane 0.
-template <bool FUSED>
-__device__ __noinline__ void wl_exact(const WlCold* Cp, const double* LPl, const uint32_t* __restrict__ bins,
-                                      uint32_t* H1a, uint32_t* H1b, const double* __restrict__ lnx, uint32_t xs,
-                                      uint32_t xb, uint32_t xe, uint32_t sl) {
-  const WlCold& C = *Cp;
-  const KParams PC = C.P;
-  const uint32_t nscr_ = C.nscr;
-  uint32_t* gs = C.gscr;
-  uint32_t* lock = gs + (size_t)nscr_ * PC.nb2;
-  const int lane = threadIdx.x & (WAVE - 1);
-  sl %= nscr_;
-  for (;;) {
-    uint32_t got = 1u;
-    if (lane == 0) got = atomicCAS(&lock[sl], 0u, 1u);
-    if (__builtin_amdgcn_readfirstlane(got) == 0u) break;
-    sl = sl + 1u == nscr_ ? 0u : sl + 1u;
-  }
-  const BgHead hbc = C.hb;
-  WinOut x;
-  if (FUSED)
-    x = eval_exact<WAVE, false, R1L, true>(PC, bins, xb, xe,
-                                           TabFused{LPl, C.Rc, (size_t)C.rs, PC.nb2, PC.n1, PC.n2, PC.n1p, PC.h1a, PC.h1b,
-                                                    PC.t1a, PC.t1b},
-                                           hbc, lnx, gs + (size_t)sl * PC.nb2, H1a, H1b, nullptr, nullptr);
-  else
-    x = eval_exact<WAVE, false, R1L, true>(PC, bins, xb, xe, TabLocal{C.tab, LPl}, hbc, lnx, gs + (size_t)sl * PC.nb2,
-                                           H1a, H1b, nullptr, nullptr);
-  __threadfence();   // the slot's words are clean again before it is released
-  if (lane == 0) {
-    atomicExch(&lock[sl], 0u);
-    write_rec(C.out + xs, C.chrom, C.wid_lo + (xs - C.slot_lo), xb, xe, x, C.zflags);
-    atomicAdd(C.err_word + 1, 1u);   // statistics: windows that took the exact path
-  }
-}
-
-template <bool FUSED, int FST>
-__device__ __forceinline__ void scan_wl(double* ldsd, SCAN_W_ARGS) {
-  constexpr bool FSTIN = FST == 2;
-  static_assert(FST == 0 || FST == 2, "k_scan_wl: Fst summed in the scan, or none");
-  constexpr int NWV = SBLOCK / WAVE;
-  constexpr int SB = 8;   // windows per batch
-  __shared__ BgHead sh_hb;
-  __shared__ double sh_bd[NWV][3][SB];      // batch: the three sums of window j
-  __shared__ uint32_t sh_bu[NWV][6][SB];    // batch: slot, begin, end, n2 | n2_all, n1a | n1b, nvar | exact << 31
-  __shared__ double sh_bf[NWV][FSTIN ? 2 : 1][SB];   // batch (FSTIN): the two Fst sums
-  __shared__ WlCold sh_c;
-  STAMP(10);
-  BLK_STAMP(1, 0);
-  const int tid = threadIdx.x;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & (WAVE - 1);
-  const Chunk ch = chunks[blockIdx.x];
-  const int bg = bg_per_chrom ? (int)ch.chrom : 0;
-  const double2* rtg = reinterpret_cast<const double2*>(dfg + 2 * LNT);   // Fst (1/n, 1/(n(n-1))) by n
-  const int rtn = P.rtn;
-  double* LPl = ldsd;
-  double* Dt = LPl + ((P.nt + 1) & ~1);
-  double2* RT = reinterpret_cast<double2*>(Dt + LDT);
-  uint32_t* HB = reinterpret_cast<uint32_t*>(RT + rtn);
-  const int h2w = wl_h2w(P.nb2);
-  const int h1w = R1L * (P.n1p + 1);
-  const int per = wl_per(P.nb2, P.n1p, P.n2p);
-  uint32_t* W = HB + wv * per;
-  uint32_t* H1a = W + h2w;
-  uint32_t* H1b = H1a + h1w;
-  const uint32_t rep = lane & (R1L - 1);
-
-  // ---- schedule: static first window, then the pool; two pool atomics in flight from the start
-  const uint32_t npool = ch.pool & 0xffffu, pool = ch.pool >> 16;
-  const bool dyn = ch.slot_lo + ch.nstatic < ch.slot_hi;
-  const uint32_t dbase = ch.slot_lo + ch.nstatic + pool;
-  uint32_t* myctr = ctr + (((size_t)cpar * P.nchrom + ch.chrom) * CTR_POOLS + pool) * CTR_STRIDE;
-  uint32_t s = ch.slot_lo + ch.first + wv;
-  const bool active = s < ch.slot_hi;
-  uint32_t gq1 = 0, gq2 = 0;
-  if (active && dyn && lane == 0) {
-    gq1 = atomicAdd(myctr, 1u);
-    gq2 = atomicAdd(myctr, 1u);
-  }
-  const uint2 sr0 = (active && mode_bp) ? slots[s] : make_uint2(0, 0);   // in flight during the table work
-  if (blockIdx.x == 0)   // the other parity's counters, for the next run
-    for (int k = tid; k < P.nchrom * CTR_POOLS; k += SBLOCK) ctr[((size_t)(1 - cpar) * P.nchrom * CTR_POOLS + k) * CTR_STRIDE] = 0u;
-
-  // ---- prologue: the chromosome's table in LDS (k_scan_w's three sources), D(r)
-  const double dv = tid < LDT ? dfg[tid] : 0.0;
-  if (FSTIN && tid < rtn) RT[tid] = rtg[tid];
-  BgHead hb;
-  const size_t rs = (size_t)P.nchrom * P.nh;
-  const uint32_t* Rc = repl + (size_t)par * REPL * rs + (size_t)ch.chrom * P.nh;
-  if (!FUSED) {
-    double lsv = 0.0;
-    int4 my_node = make_int4(0, 0, -1, 0);
-    uint32_t bc = 0u;
-    Bg1D o{};
-    if (sliced) {
-      if (tid < nleaves) lsv = leafsum[(size_t)bg * nleaves + tid];
-      if (tid < nnodes) my_node = nodes[tid];
-      if (tid == 0) { bc = bcount[(size_t)par * P.nchrom + bg]; o = bg1d[bg]; }
-    }
-    lds_copy_d(LPl, LPg + (size_t)bg * P.nt, P.nt);
-    if (tid < LDT) Dt[tid] = dv;
-    if (sliced) {
-      const bool writer = ch.first == 0 && (int)ch.chrom == write_chrom;
-      double* lsum = reinterpret_cast<double*>(HB);
-      if (tid < nleaves) lsum[tid] = lsv;
-      __syncthreads();
-      for (int l = 0; l < nlevels; ++l) {
-        if (my_node.z == l) lsum[nleaves + tid] = lsum[my_node.x] + lsum[my_node.y];
-        __syncthreads();
-      }
-      if (tid == 0) {
-        const double B2 = (double)bc;
-        uint32_t flags = o.flags;
-        if (B2 == 0.0) flags |= BGF_B2_ZERO;
-        const int M2 = P.nb2 - 2;
-        if (M2 >= 1 && B2 != 0.0) {
-          const double S = (nleaves + nnodes) ? lsum[nleaves + nnodes - 1] : 0.0;
-          const double padj = 1.0 - S;
-          if (padj < -1e-15) {
-            flags |= BGF_NAN2;
-          } else if (fabs(padj) > 1e-15) {
-            const double l2 = log(padj);
-            LPl[M2] = l2;
-            if (writer) { tab[(size_t)bg * P.nt + M2].lp = l2; LPg[(size_t)bg * P.nt + M2] = l2; }
-          }
-        }
-        BgHead h;
-        h.B2 = B2; h.B1a = o.B1a; h.B1b = o.B1b; h.flags = flags; h.pad = 0;
-        sh_hb = h;
-        if (writer) head[bg] = h;
-      }
-      if (blockIdx.x == 0)
-        for (int c = tid; c < P.nchrom; c += SBLOCK) bcount[(size_t)(1 - par) * P.nchrom + c] = 0u;
-      __syncthreads();
-      hb = sh_hb;
-    } else {
-      hb = head[bg];
-    }
-  } else {
-    if (tid < LDT) Dt[tid] = dv;
-    fused_table(P.nb2, P.nh, P.nt, P.n1p, P.n2p, P.n1, P.n2, P.t1a, P.t1b, P.nchrom, ch.chrom,
-                ch.first == 0 && (int)ch.chrom == write_chrom, bg,
-                Rc, rs, repl, bcount, par, tab, LPg, head, LPl, HB, leaves, nleaves, nodes, nnodes, nlevels, lnx,
-                &sh_hb, reinterpret_cast<double*>(HB) + wl_lsum_off(nleaves), HB + wl_vcnt_off(nleaves, nnodes));
-    hb = sh_hb;
-  }
-  for (int k = lane; k < per / 4; k += WAVE) reinterpret_cast<uint4*>(W)[k] = make_uint4(0, 0, 0, 0);
-  if (tid == 0) {
-    LPl[0] = 0.0;   // bin 0 ((0,0), never counted): SNPs outside the 2D SFS read it and add 0
-    WlCold c;
-    c.P = P; c.out = out; c.fst_out = fst_out; c.err_word = err_word; c.gscr = gscr; c.tab = tab + (size_t)bg * P.nt;
-    c.Rc = Rc; c.rs = rs; c.hb = hb; c.chrom = ch.chrom; c.wid_lo = ch.wid_lo; c.slot_lo = ch.slot_lo;
-    c.nscr = (uint32_t)nscr; c.zflags = bg_zero_flags(hb); c.nanf = hb.flags;
-    sh_c = c;
-  }
-  __syncthreads();
-  if (FUSED) {   // the other parity's replicas and inner sums, zeroed for the next run (a slice per workgroup)
-    uint32_t* Ro = repl + (size_t)(1 - par) * REPL * rs;
-    const size_t tot = (size_t)REPL * rs, share = (tot + gridDim.x - 1) / gridDim.x;
-    const size_t lo = (size_t)blockIdx.x * share, hi = lo + share < tot ? lo + share : tot;
-    for (size_t k = lo + tid; k < hi; k += SBLOCK) Ro[k] = 0u;
-    if (blockIdx.x == 0)
-      for (int c = tid; c < P.nchrom; c += SBLOCK) bcount[(size_t)(1 - par) * P.nchrom + c] = 0u;
-  }
-  if (!active) return;
-  const bool half1d = P.n1p <= 31 && P.n2p <= 31;
-  typedef __attribute__((address_space(3))) uint32_t lds_u32;
-  typedef __attribute__((address_space(3))) double lds_f64;
-  uint32_t a1b = (uint32_t)(uintptr_t)((lds_u32*)(H1a + rep)), a2b = (uint32_t)(uintptr_t)((lds_u32*)(H1b + rep));
-  asm volatile("" : "+v"(a1b), "+v"(a2b));
-  uint32_t awb = (uint32_t)(uintptr_t)((lds_u32*)W);
-  asm volatile("" : "+s"(awb));
-  const uint32_t dtb = (uint32_t)(uintptr_t)((lds_f64*)Dt), lpb = (uint32_t)(uintptr_t)((lds_f64*)LPl);
-  const uint32_t rtb = (uint32_t)(uintptr_t)((lds_f64*)RT), rtm = (uint32_t)rtn - 1u;
-
-  // ---- batched finish (k_scan_w's flush, with the window's end stored and an explicit exact flag)
-  uint32_t jb = 0;
-  auto flush = [&]() {
-    MARK(44);
-    asm volatile("" ::: "memory");   // (sh_c read back from LDS, not kept in registers across the loop)
-    const WlCold& C = sh_c;
-    uint32_t ln = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    asm volatile("" : "+v"(ln));
-    const bool mine = ln < jb;
-    const int jl = ln & (SB - 1);
-    const double B2 = sh_bd[wv][0][jl], Ba = sh_bd[wv][1][jl], Bb = sh_bd[wv][2][jl];
-    const uint32_t Bs = sh_bu[wv][0][jl], Bsb = sh_bu[wv][1][jl], Bse = sh_bu[wv][2][jl], Bn2 = sh_bu[wv][3][jl],
-                   Bn1 = sh_bu[wv][4][jl], Bnv = sh_bu[wv][5][jl];
-    const bool empty = Bse == Bsb;
-    const uint32_t wid = C.wid_lo + (Bs - C.slot_lo);
-    WinOut w;
-    w.snp_count = Bnv & 0x7fffffffu; w.n2 = Bn2 & 0xffffu; w.n2_all = Bn2 >> 16; w.n1a = Bn1 & 0xffffu; w.n1b = Bn1 >> 16;
-    w.t2d = 2.0 * (B2 - (double)w.n2 * lnx[w.n2]);
-    w.t1a = 2.0 * (Ba - (double)w.n1a * lnx[w.n1a]);
-    w.t1b = 2.0 * (Bb - (double)w.n1b * lnx[w.n1b]);
-    const bool exact = mine && !empty &&
-                       ((Bnv >> 31) != 0u || suspect_zero(w.t2d, w.n2) || suspect_zero(w.t1a, w.n1a) ||
-                        suspect_zero(w.t1b, w.n1b));
-    const uint32_t nanf = C.nanf, zflags = C.zflags;
-    if (nanf & BGF_NAN2) w.t2d = __builtin_nan("");
-    if (nanf & BGF_NAN1A) w.t1a = __builtin_nan("");
-    if (nanf & BGF_NAN1B) w.t1b = __builtin_nan("");
-    if (empty) { w.t2d = 0.0; w.t1a = 0.0; w.t1b = 0.0; }
-    if (mine && !exact)
-      write_rec(C.out + Bs, C.chrom, wid, empty ? 0u : Bsb, empty ? 0u : Bse, w, empty ? SFS2D_W_EMPTY : zflags);
-    if (mine) {
-      if (FSTIN) {
-        const double fx = sh_bf[wv][0][jl], fy = sh_bf[wv][FSTIN ? 1 : 0][jl];
-        C.fst_out[Bs] = fy != 0.0 ? fx / fy : __builtin_nan("");
-      }
-      if (mode_bp) {
-        uint32_t z = 0u;
-        asm volatile("" : "+v"(z));
-        slots[Bs] = make_uint2(z, z);
-      }
-    }
-    MARK(45);
-    // rare: exact re-evaluation on a u32 histogram in global memory (a scratch slot taken by CAS)
-    for (unsigned long long m = __ballot(exact); m; m &= m - 1) {
-      const int l = __builtin_ctzll(m);
-      const uint32_t xs = __builtin_amdgcn_readlane(Bs, l), xb = __builtin_amdgcn_readlane(Bsb, l),
-                     xe = __builtin_amdgcn_readlane(Bse, l);
-      wl_exact<FUSED>(&sh_c, LPl, bins, H1a, H1b, lnx, xs, xb, xe, blockIdx.x * NWV + wv);
-      group_sync<WAVE>();
-    }
-    jb = 0;
-  };
-  constexpr unsigned long long OWN5 = 1ull | (1ull << 33) | (1ull << 48) | (FSTIN ? (1ull << 16) | (1ull << 32) : 0ull);
-  uint32_t sdst;
-  {
-    double* d = lane == 0 ? &sh_bd[wv][0][0] : lane == 33 ? &sh_bd[wv][1][0] : lane == 48 ? &sh_bd[wv][2][0]
-              : lane == 16 ? &sh_bf[wv][0][0] : &sh_bf[wv][FSTIN ? 1 : 0][0];
-    sdst = (uint32_t)(uintptr_t)((lds_f64*)d);
-  }
-  asm volatile("" : "+v"(sdst));
-
-  // ---- the window loop.  Every VMEM load is waited for in issue order (vmcnt): the next window's rows,
-  // its slot record and the pool atomic are issued right after the row loop (the rest of the window --
-  // 1D pass, sums, batch -- is their cover, with the other five waves of the SIMD), behind any streamed
-  // row load of this window they would otherwise hold back.
-  auto window_of = [&](uint32_t sl, uint2 sr, uint32_t& b, uint32_t& e) {
-    if (mode_bp) {   // slot record: first + 1, last + 1 (0: no SNP in the slot -> b == e)
-      b = sr.x ? sr.x - 1u : 0u;
-      e = sr.x ? sr.y : 0u;
-    } else {
-      b = ch.cb + (ch.wid_lo + (sl - ch.slot_lo)) * P.ws;
-      e = b + P.ws;
-    }
-  };
-  uint32_t u[8];
-  auto issue_rows = [&](uint32_t b, uint32_t e) {
-    const __amdgpu_buffer_rsrc_t rr = window_rows(bins, b, e, P.nm1);
-    // (the lane's byte offset made opaque here: hoisted out of the loop, the eight row offsets were kept
-    // as eight VGPRs -- spilled -- instead of one base + the loads' immediate offsets)
-    uint32_t lo = (uint32_t)lane * 4u;
-    asm volatile("" : "+v"(lo));
-#pragma unroll
-    for (int j = 0; j < 8; ++j) u[j] = __builtin_amdgcn_raw_buffer_load_b32(rr, (int)lo + 256 * j, 0, 0);
-  };
-  auto pool_slot = [&](uint32_t g) -> uint32_t {
-    const uint32_t j = __builtin_amdgcn_readfirstlane(g);
-    return dyn && dbase + npool * j < ch.slot_hi ? dbase + npool * j : ch.slot_hi;
-  };
-  uint32_t b = 0, e = 0;
-  window_of(s, make_uint2(__builtin_amdgcn_readfirstlane(sr0.x), __builtin_amdgcn_readfirstlane(sr0.y)), b, e);
-  issue_rows(b, e);
-  uint32_t s1 = pool_slot(gq1);
-  uint2 sr1 = (mode_bp && s1 < ch.slot_hi) ? slots[s1] : make_uint2(0, 0);
-  STAMP(11);
-  int it = 0;
-  while (true) {
-    MARK(40);
-    const uint32_t nsnp = e - b;
-    double acc2 = 0.0, fN = 0.0, fD = 0.0;
-    uint32_t n2 = 0;
-    bool wrap = false;
-    // one row of 64 SNPs: per SNP the 2D atomic (u8 bins) returns the SNP's rank r in its bin and the SNP
-    // adds D(r) - lp_k; both folded 1D bins counted (lane & 1 replicas; bins 0 and n_p dropped at the end);
-    // FSTIN: fst_snp's (num, den) from the counts and the LDS reciprocals (0 unless both populations have
-    // >= 2 called alleles; SNPs outside the 2D SFS have num = den = 0).  Rows past e load as 0.
-    auto row = [&](uint32_t w) {
-      uint32_t k2, gp;
-      cls_k2g<4 * R1L>(P, w, k2, gp);
-      const bool in2 = k2 != 0u;
-      n2 += __popcll(__ballot(in2));
-      const uint32_t x = k2 << 3;   // the byte's shift: the hardware reads the low five bits
-      uint32_t one2;
-      asm("v_lshlrev_b32 %0, %1, 1" : "=v"(one2) : "v"(x));
-      const uint32_t wa = awb + (k2 & ~3u);
-      uint32_t o = one2;
-      if (in2)
-        o = __hip_atomic_fetch_add((lds_u32*)(uintptr_t)wa, one2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      __hip_atomic_fetch_add((lds_u32*)(uintptr_t)(a1b + (gp & 0xffffu)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      __hip_atomic_fetch_add((lds_u32*)(uintptr_t)(a2b + (gp >> 16)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#ifdef SFS2D_WL_FSTTAB   // experiment: the (alt, ref) table in global memory, as k_scan_w
-      if (FSTIN) {
-        const bool ok = (__builtin_amdgcn_udot4(w, 0x00000101u, 0u, false) >= 2u) &
-                        (__builtin_amdgcn_udot4(w, 0x01010000u, 0u, false) >= 2u);
-        const double2* artg = reinterpret_cast<const double2*>(dfg + 2 * LNT + 2 * RCPN);
-        const double2 fa = artg[ok ? w & 0xffffu : 0u], fb = artg[ok ? w >> 16 : 0u];
-        const double m = fa.x * fb.x;
-        fN += fma(-2.0, m, fa.y + fb.y);
-        fD += fma(-2.0, m, fa.x + fb.x);
-      }
-#else
-      if (FSTIN) {
-        const uint32_t n1c = __builtin_amdgcn_udot4(w, 0x00000101u, 0u, false);
-        const uint32_t n2c = __builtin_amdgcn_udot4(w, 0x01010000u, 0u, false);
-        const bool ok = (n1c >= 2u) & (n2c >= 2u);
-        const uint32_t f1 = ok ? (w >> 8) & 0xffu : 0u, f2 = ok ? w >> 24 : 0u;
-        const uint32_t q1a = rtb + 16u * min(n1c, rtm), q2a = rtb + 16u * min(n2c, rtm);
-        const double r1x = ((lds_f64*)(uintptr_t)q1a)[0], r1y = ((lds_f64*)(uintptr_t)q1a)[1];
-        const double r2x = ((lds_f64*)(uintptr_t)q2a)[0], r2y = ((lds_f64*)(uintptr_t)q2a)[1];
-        const double p1 = (double)f1 * r1x, p2 = (double)f2 * r2x;
-        const double A1 = (double)__umul24(f1, f1 - 1u) * r1y, A2 = (double)__umul24(f2, f2 - 1u) * r2y;
-        const double m = p1 * p2;
-        fN += fma(-2.0, m, A1 + A2);
-        fD += fma(-2.0, m, p1 + p2);
-      }
-#endif
-      const uint32_t r = in2 ? __builtin_amdgcn_ubfe(o, x, 8) : 0u;
-      wrap |= r == 255u;
-      const double d = ((lds_f64*)(uintptr_t)(dtb + 8u * r))[0];
-      const double lp = ((lds_f64*)(uintptr_t)(lpb + 8u * k2))[0];
-      acc2 += d - lp;
-    };
-    if (nsnp) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (64 * j < (int)nsnp) row(u[j]);
-      if (nsnp > 8 * WAVE) {   // rows 8 on, streamed one row ahead (buffer loads: 0 past the window's end)
-        const __amdgpu_buffer_rsrc_t rr = window_rows(bins, b, e, P.nm1);
-        uint32_t ln = (uint32_t)lane * 4u;
-        asm volatile("" : "+v"(ln));
-        int vo = (int)ln + 256 * 8;
-        uint32_t x0 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo, 0, 0);
-        for (int j = 8; 64 * j < (int)nsnp; ++j) {
-          const uint32_t w0 = x0;
-          vo += 256;
-          x0 = __builtin_amdgcn_raw_buffer_load_b32(rr, vo, 0, 0);
-          row(w0);
-        }
-        asm volatile("" ::"v"(x0));   // (the last prefetch consumed on this path: see k_scan_w)
-      }
-    }
-    MARK(41);
-    // the pipeline: window s1's rows (its slot record arrived during this window), window s2's slot record
-    // (its pool index arrived during this window), the pool atomic for the window after it
-    // (the batch's last window issues them after the flush instead: no row registers live across it)
-    const bool more = s1 < ch.slot_hi;
-    const bool fill = jb + 1u < (uint32_t)SB;
-    uint32_t b1 = 0, e1 = 0;
-    if (more) {
-      window_of(s1, make_uint2(__builtin_amdgcn_readfirstlane(sr1.x), __builtin_amdgcn_readfirstlane(sr1.y)), b1, e1);
-      if (fill) issue_rows(b1, e1);
-    }
-    const uint32_t s2 = more ? pool_slot(gq2) : ch.slot_hi;
-    const uint2 sr2 = (mode_bp && s2 < ch.slot_hi) ? slots[s2] : make_uint2(0, 0);
-    if (s2 < ch.slot_hi && lane == 0) gq2 = atomicAdd(myctr, 1u);
-    if (nsnp == 0u) {   // an empty slot
-      if (lane == 0) {
-        sh_bu[wv][0][jb] = s; sh_bu[wv][1][jb] = 0u; sh_bu[wv][2][jb] = 0u;
-        sh_bu[wv][3][jb] = 0u; sh_bu[wv][4][jb] = 0u; sh_bu[wv][5][jb] = 0u;
-        sh_bd[wv][0][jb] = 0.0; sh_bd[wv][1][jb] = 0.0; sh_bd[wv][2][jb] = 0.0;
-        if (FSTIN) { sh_bf[wv][0][jb] = 0.0; sh_bf[wv][FSTIN ? 1 : 0][jb] = 0.0; }
-      }
-    } else {
-      uint32_t nlast = 0;
-      if (!P.fold) {   // unfolded: SNPs in the excluded last 2D bin count in n2_all
-        for (uint32_t i0 = b; i0 < e; i0 += WAVE) {
-          const uint32_t w = i0 + lane < e ? cls_word(P, bins[i0 + lane]) : 0u;
-          nlast += __popcll(__ballot((w & B_LAST) != 0u));
-        }
-      }
-      group_sync<WAVE>();
-      // 1D spectra: one lane per folded bin reads and clears its R1L replicas (lanes 0-31 population 1,
-      // 32-63 population 2 when both have <= 31 bins); every SNP slot of the rows counted in one bin of
-      // each spectrum: n1a / n1b = slots - bin 0 - bin n_p
-      double acca = 0.0;
-      uint32_t n1a, n1b;
-      const uint32_t slots128 = 64u * ((nsnp + 63u) / 64u);
-      // (the lane id made opaque: hoisted out of the window loop, the lane predicates and LDS addresses
-      // below were kept in registers across it -- and spilled)
-      uint32_t ln1 = (uint32_t)lane, z1 = 0u;   // (z1: the replicas' clearing zeros, likewise)
-      asm volatile("" : "+v"(ln1), "+v"(z1));
-      if (half1d) {
-        const bool pa = ln1 < 32u;
-        const int k = (int)(ln1 & 31u), np = pa ? P.n1p : P.n2p;
-        uint32_t x = 0;
-        if (k <= np) {
-          uint2* q = reinterpret_cast<uint2*>((pa ? H1a : H1b) + k * R1L);
-          const uint2 v = *q;
-          *q = make_uint2(z1, z1);
-          x = v.x + v.y;
-          if (k >= 1 && k < np && x) acca = (double)x * lnx[x] - (double)x * LPl[(pa ? P.t1a : P.t1b) + k];
-        }
-        n1a = slots128 - (uint32_t)__builtin_amdgcn_readlane((int)x, 0) - (uint32_t)__builtin_amdgcn_readlane((int)x, P.n1p);
-        n1b = slots128 - (uint32_t)__builtin_amdgcn_readlane((int)x, 32) - (uint32_t)__builtin_amdgcn_readlane((int)x, 32 + P.n2p);
-      } else {
-        double accb = 0.0;
-        uint32_t xa[2] = {0u, 0u}, xb[2] = {0u, 0u};
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int k = (int)ln1 + WAVE * j;
-          if (k <= P.n1p) {
-            uint2* q = reinterpret_cast<uint2*>(H1a + k * R1L);
-            const uint2 v = *q;
-            *q = make_uint2(z1, z1);
-            xa[j] = v.x + v.y;
-            if (k >= 1 && k < P.n1p && xa[j]) acca += (double)xa[j] * lnx[xa[j]] - (double)xa[j] * LPl[P.t1a + k];
-          }
-          if (k <= P.n2p) {
-            uint2* q = reinterpret_cast<uint2*>(H1b + k * R1L);
-            const uint2 v = *q;
-            *q = make_uint2(z1, z1);
-            xb[j] = v.x + v.y;
-            if (k >= 1 && k < P.n2p && xb[j]) accb += (double)xb[j] * lnx[xb[j]] - (double)xb[j] * LPl[P.t1b + k];
-          }
-        }
-        const uint32_t ea = P.n1p >= WAVE ? (uint32_t)__builtin_amdgcn_readlane((int)xa[1], P.n1p - WAVE)
-                                          : (uint32_t)__builtin_amdgcn_readlane((int)xa[0], P.n1p);
-        const uint32_t eb = P.n2p >= WAVE ? (uint32_t)__builtin_amdgcn_readlane((int)xb[1], P.n2p - WAVE)
-                                          : (uint32_t)__builtin_amdgcn_readlane((int)xb[0], P.n2p);
-        n1a = slots128 - (uint32_t)__builtin_amdgcn_readlane((int)xa[0], 0) - ea;
-        n1b = slots128 - (uint32_t)__builtin_amdgcn_readlane((int)xb[0], 0) - eb;
-        // (wave_sum5 sums its h operand over each lane half: population 1's total in lane 0, 2's in 32)
-        const double sa = wave_sum_all(acca), sb = wave_sum_all(accb);
-        acca = lane == 0 ? sa : (lane == 32 ? sb : 0.0);
-      }
-      MARK(42);
-      {   // clear the 2D histogram (u8 words: three 16-B stores per lane at 51 x 51)
-        uint4* q = reinterpret_cast<uint4*>(W);
-        for (int k = lane; k < h2w / 4; k += WAVE) q[k] = make_uint4(0, 0, 0, 0);
-      }
-      const double v = wave_sum5(acc2, acca, FSTIN ? fN : 0.0, FSTIN ? fD : 0.0, (uint32_t)lane);
-      if ((OWN5 >> lane) & 1ull) ((lds_f64*)(uintptr_t)(sdst + 8u * jb))[0] = v;
-      const bool ex = __ballot(wrap) != 0ull || nsnp >= 65535u;
-      if (lane == 0) {
-        sh_bu[wv][0][jb] = s;
-        sh_bu[wv][1][jb] = b;
-        sh_bu[wv][2][jb] = e;
-        sh_bu[wv][3][jb] = min(n2, 0xffffu) | (min(n2 + nlast, 0xffffu) << 16);
-        sh_bu[wv][4][jb] = min(n1a, 0xffffu) | (min(n1b, 0xffffu) << 16);
-        sh_bu[wv][5][jb] = nsnp | (ex ? 0x80000000u : 0u);
-      }
-    }
-    ++jb;
-    ++it;
-    group_sync<WAVE>();
-    MARK(43);
-    if (!fill) {
-      flush();
-      if (more) issue_rows(b1, e1);
-    }
-    if (!more) break;
-    s = s1; b = b1; e = e1;   // window s1 (its rows in u) becomes the current one
-    s1 = s2; sr1 = sr2;
-  }
-  if (jb) flush();
-  STAMP(15);
-  WV_STAMP(it);
-  BLK_STAMP(1, 1);
-}
-
-template <bool FUSED, int FST>
-__global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(6))) void k_scan_wl(SCAN_W_ARGS) {
-  extern __shared__ double ldsd[];
-  scan_wl<FUSED, FST>(ldsd, SCAN_W_PASS);
-}
-
 // CNT: `bins` is the counts array (counts plans): every scan classifies the counts it streams
 template <bool P16, bool FUSED, int FST, bool CNT>
 __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_scan_w(SCAN_W_ARGS) {
   extern __shared__ double ldsd[];
   scan_w_small<P16, FUSED, FST, CNT>(ldsd, SCAN_W_PASS);
+}
+
+// k_scan_w's window loop with u8-packed 2D bins and (FST 4 / 5) the Fst (p, A) table in LDS (see scan_w_small)
+template <bool FUSED, int FST>
+__global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_scan_w8(SCAN_W_ARGS) {
+  extern __shared__ double ldsd[];
+  scan_w_small<false, FUSED, FST, true, true>(ldsd, SCAN_W_PASS);
 }
 
 // K3 for large grids, one wavefront per window (LDS: the wave's histograms only)

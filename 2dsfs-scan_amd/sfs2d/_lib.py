@@ -40,9 +40,7 @@ EXPORTS = [
     "sfs2d_plan_bg_buffer", "sfs2d_plan_bg_words", "sfs2d_plan_bg_exchange", "sfs2d_plan_run_phase", "sfs2d_plan_check", "sfs2d_plan_time",
     "sfs2d_plan_destroy", "sfs2d_scan", "sfs2d_plan_set_timing", "sfs2d_plan_timing_read",
     "sfs2d_plan_stats", "sfs2d_plan_grids", "sfs2d_plan_scan_kernel", "sfs2d_plan_attach", "sfs2d_data_synth_sims",
-    "sfs2d_data_read", "sfs2d_dist_unique_id", "sfs2d_dist_create", "sfs2d_dist_scan_gather",
-    "sfs2d_dist_destroy", "sfs2d_dist_set_gather", "sfs2d_plan_run_streams",
-    "sfs2d_dist_scan_gather_streams", "sfs2d_bg_hist_dev", "sfs2d_plan_bg_rows_dev", "sfs2d_plan_bg_rows_set_dev",
+    "sfs2d_data_read", "sfs2d_plan_run_streams", "sfs2d_ctx_use_own_stream", "sfs2d_bg_hist_dev", "sfs2d_plan_bg_rows_dev", "sfs2d_plan_bg_rows_set_dev",
 ]
 
 
@@ -133,12 +131,7 @@ def lib():
     L.sfs2d_plan_attach.argtypes = [vp, C.POINTER(Params), C.POINTER(vp)]
     L.sfs2d_data_synth_sims.argtypes = [vp, C.POINTER(SynthParams), vp, vp, i32, vp, i32, C.POINTER(vp)]
     L.sfs2d_data_read.argtypes = [vp, vp, vp, i64]
-    L.sfs2d_dist_unique_id.argtypes = [vp]
-    L.sfs2d_dist_create.argtypes = [vp, vp, i32, i32, C.POINTER(vp)]
-    L.sfs2d_dist_scan_gather.argtypes = [vp, vp, vp, vp, vp, vp, i64, i64, C.c_int, vp]
-    L.sfs2d_dist_destroy.argtypes = [vp]
-    L.sfs2d_dist_scan_gather_streams.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, i64, C.c_int]
-    L.sfs2d_dist_set_gather.argtypes = [vp, C.c_int]
+    L.sfs2d_ctx_use_own_stream.argtypes = [vp]
     L.sfs2d_plan_timing_read.argtypes = [vp, C.POINTER(C.c_int)] + [C.POINTER(C.c_double)] * 3
     L.sfs2d_scan.argtypes = [vp, vp, C.POINTER(Params), vp, vp, vp, vp, i64, C.POINTER(i64)]
     _lib = L

@@ -252,20 +252,21 @@ def _all_gather_dev(out, world):
 @contextlib.contextmanager
 def _one_stream(eng, dev):
     """torch's ops on the exchange buffers, the collectives and the library's kernels ordered on ONE
-    stream: a fresh (non-null) torch stream made current and handed to the library.  (Handing it torch's
-    default stream does not work: its handle is 0, and NULL selects the library's own non-blocking
-    stream, which nothing orders against the default stream -- the kernels could read an exchange buffer
-    before its zero fill or its all-reduced copy had landed.)"""
+    stream: a fresh torch stream made current and handed to the library; the engine's previous stream
+    is restored on exit (the engine is shared per device: a caller that had handed it its own stream,
+    as bench.py does, keeps it).  (Round 4 found the 2-rank test reading a NaN background once in
+    several runs: the C API then took a NULL handle -- torch's default stream -- as the library's own
+    non-blocking stream, unordered with the buffers' fill.  NULL is now the HIP null stream.)"""
     import torch
     s = torch.cuda.Stream(device=dev)
     s.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(s):
-        eng.set_stream(s.cuda_stream)
+        prev = eng.set_stream(s.cuda_stream)
         try:
             yield s
         finally:
             s.synchronize()
-            eng.set_stream(None)
+            eng.set_stream(prev)
 
 
 def _split_device(p, cfg, bg, split_scan, device, cuts, c0s, sub, c0, rank, world, last):
@@ -323,7 +324,10 @@ def _split_device(p, cfg, bg, split_scan, device, cuts, c0s, sub, c0, rank, worl
 
 
 def _rows_on_device(split_scan) -> bool:
-    if not getattr(split_scan, "device_rows", False):
+    """Whether the jobs of ``split_scan`` exchange background rows in HBM: engine.SplitJob factories
+    (``split_scan.device_rows``, or a factory whose jobs are SplitJob instances: ``split_scan.job_type``)."""
+    from .engine import SplitJob
+    if not (getattr(split_scan, "device_rows", False) or getattr(split_scan, "job_type", None) is SplitJob):
         return False
     try:
         import torch
@@ -420,26 +424,32 @@ def sharded_bg_hist(p, cfg, device: int = 0, chrom: int = -1):
     on_dev = torch.cuda.is_available()
     dev = torch.device(f"cuda:{device}") if on_dev else torch.device("cpu")
     buf = torch.zeros(W + world, dtype=torch.int64, device=dev)
-    code = 0
+    code, err = 0, None
     if b > a:
-        sub, _ = p.slice_snps(a, b)
         eng = Engine.get(device)
-        with _one_stream(eng, dev):   # the histogram kernels ordered after buf's zero fill
-            d = eng.upload(sub)
-            try:
-                eng.bg_hist_dev(d, cfg, -1, buf.data_ptr())
-            except KeyError:
-                code = 1
-            except L.Sfs2dError as e:
-                if e.code != L.E_GRID:
-                    raise
-                code = 2
-            finally:
-                d.close()
+        try:
+            with _one_stream(eng, dev):   # the histogram kernels ordered after buf's zero fill
+                sub, _ = p.slice_snps(a, b)
+                d = eng.upload(sub)
+                try:
+                    eng.bg_hist_dev(d, cfg, -1, buf.data_ptr())
+                finally:
+                    d.close()
+        except KeyError:
+            code = 1
+        except L.Sfs2dError as e:
+            code, err = (2, None) if e.code == L.E_GRID else (4, e)
+        except Exception as e:  # noqa: BLE001  (every rank must reach the all-reduce: no RCCL hang)
+            code, err = 4, e
     buf[W + rank] = code
     _all_reduce_dev(buf)
     h = buf.cpu().numpy()
     bits = int(np.bitwise_or.reduce(h[W:].astype(np.int64))) if world else 0
+    if bits & 4:   # a failure other than the reference's count errors, on this rank or another
+        if err is not None:
+            raise err
+        bad = [r for r in range(world) if int(h[W + r]) & 4]
+        raise L.Sfs2dError(L.E_HIP, f"sharded background histogram failed on rank(s) {bad}")
     if bits & 1:
         raise KeyError("allele count above 2*pop_size (reference: KeyError in calculate_1d_sfs)")
     if bits & 2:

@@ -58,6 +58,7 @@ class Engine:
         if rc != 0:
             raise L.Sfs2dError(rc, f"cannot create a HIP context on device {device} (no MI355X visible?)")
         self.h = h
+        self.stream = None   # the ctx's own stream (set_stream)
 
     @classmethod
     def get(cls, device: int = 0) -> "Engine":
@@ -75,25 +76,20 @@ class Engine:
             raise L.Sfs2dError(rc, msg)
 
     def set_stream(self, stream_handle: Optional[int]):
-        """Enqueue the library's work on the HIP stream ``stream_handle`` (None: the ctx's own stream).
-        Handle 0 -- torch's default stream -- is refused: the C API reads NULL as the ctx's own
-        non-blocking stream, which would silently not be ordered with the caller's work (share a
-        ``torch.cuda.Stream`` instead)."""
-        if stream_handle is not None and int(stream_handle) == 0:
-            raise ValueError("stream handle 0 (the default stream) cannot be shared; pass a torch.cuda.Stream's handle")
-        self.check(self.lib.sfs2d_ctx_set_stream(self.h, C.c_void_p(stream_handle) if stream_handle else None))
+        """Enqueue the library's work on the HIP stream ``stream_handle``: any handle, 0 included (the
+        HIP null stream -- torch's default stream -- ordered with the process's blocking streams);
+        None: the ctx's own non-blocking stream (sfs2d_ctx_use_own_stream), which nothing orders
+        against the caller's streams.  Returns the previous setting (for restore)."""
+        prev = self.stream
+        if stream_handle is None:
+            self.check(self.lib.sfs2d_ctx_use_own_stream(self.h))
+        else:
+            self.check(self.lib.sfs2d_ctx_set_stream(self.h, C.c_void_p(int(stream_handle)) if int(stream_handle) else None))
+        self.stream = stream_handle
+        return prev
 
     def upload(self, p: PackedSNPs) -> "DeviceData":
         return DeviceData(self, p)
-
-    def dist_unique_id(self) -> bytes:
-        """RCCL communicator id (rank 0 makes it, the caller broadcasts it): sfs2d_dist_unique_id."""
-        buf = (C.c_uint8 * 128)()
-        self.check(self.lib.sfs2d_dist_unique_id(buf))
-        return bytes(buf)
-
-    def dist(self, uid: bytes, rank: int, world: int) -> "Dist":
-        return Dist(self, uid, rank, world)
 
     def wrap_device(self, d_counts: int, d_pos: int, d_ann: Optional[int], n: int, chrom_off: np.ndarray,
                     chrom_last_pos: np.ndarray) -> "DeviceData":
@@ -369,52 +365,3 @@ class SplitJob:
             self.dev.close()
             self.dev = None
 
-
-class Dist:
-    """One rank's RCCL communicator in the native library (sfs2d_dist_*): back-to-back scans of a
-    plan, each gathering the fixed-stride window tables of every rank to rank 0 (ncclGather; or
-    all-gathering them into every rank, set_gather(False)), enqueued from C so that
-    the host loop is not the bottleneck."""
-
-    def __init__(self, eng: Engine, uid: bytes, rank: int, world: int):
-        if len(uid) != 128:
-            raise ValueError("RCCL unique id must be 128 bytes")
-        self.eng = eng
-        h = C.c_void_p()
-        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
-        eng.check(eng.lib.sfs2d_dist_create(eng.h, buf, rank, world, C.byref(h)))
-        self.h = h
-
-    def scan_gather(self, plan: "Plan", outs, gathered, rows: int, first_step: int, nsteps: int,
-                    comm_stream: Optional[int]):
-        """outs / gathered: two device pointers each (rows x 64 B per rank / world x rows x 64 B);
-        comm_stream None: gathers serial on the library's stream."""
-        self.eng.check(self.eng.lib.sfs2d_dist_scan_gather(
-            self.h, plan.h, C.c_void_p(outs[0]), C.c_void_p(outs[1]), C.c_void_p(gathered[0]),
-            C.c_void_p(gathered[1]), rows, first_step, nsteps, C.c_void_p(comm_stream) if comm_stream else None))
-
-    def scan_gather_streams(self, plans, streams, outbuf: int, gathered, rows: int, nsteps: int):
-        """Steps in groups of k = len(plans): plan j scans on streams[j] into table
-        (group & 1) * k + j of outbuf (2 k rows records), then one gather of the group's tables into
-        gathered[group & 1] (world * k * rows records) on streams[0] (sfs2d_dist_scan_gather_streams)."""
-        k = len(plans)
-        ph = (C.c_void_p * k)(*[p.h.value for p in plans])
-        sh = (C.c_void_p * k)(*[x or None for x in streams])
-        self.eng.check(self.eng.lib.sfs2d_dist_scan_gather_streams(self.h, ph, sh, k, C.c_void_p(outbuf),
-                                                                   C.c_void_p(gathered[0]), C.c_void_p(gathered[1]),
-                                                                   int(rows), int(nsteps)))
-
-    def set_gather(self, to_root: bool):
-        """True: ncclGather to rank 0 (the default where RCCL has it); False: ncclAllGather."""
-        self.eng.check(self.eng.lib.sfs2d_dist_set_gather(self.h, 1 if to_root else 0))
-
-    def close(self):
-        if self.h:
-            self.eng.lib.sfs2d_dist_destroy(self.h)
-            self.h = None
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass

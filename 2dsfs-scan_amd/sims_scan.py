@@ -185,6 +185,9 @@ def _split_scan(p, cfg, bg):
     return SplitJob(Engine.get(DEVICE), p, cfg, bg)
 
 
+_split_scan.device_rows = True   # its jobs exchange background rows in HBM (sfs2d.dist._split_device)
+
+
 def process_windows_batch(replicates, bg_2d_sfs, bg_p1_sfs, bg_p2_sfs, window_size, pop1, pop2, pop1_size,
                           pop2_size, start_position=None, end_position=None, variant_type=None, distributed=False):
     """``process_window`` (sims_scan.py:451-590) over many replicate data sets in ONE scan launch:

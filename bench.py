@@ -407,15 +407,44 @@ def config3_strong(cx, args):
     one = single_pass_ms(cx, plans[0]) if cx.rank == 0 else None
     extra = {}
     if cx.world == 1 and not args.no_variants:
-        # the same loop without Fst (the reference's statistics): what Hudson's Fst costs the pass
+        # what Hudson's Fst costs the pass: the same loop without Fst (the reference's statistics) and
+        # with it, interleaved three times each (box-to-box clock drift moves both alike); medians
         cfg2 = ScanConfig(n1p=POP, n2p=POP, window=WS, fst=False, scan_wgs_per_cu=1)
         q = [cx.eng.plan(dev, cfg2) for _ in range(ns)]
-        rr = run_loop(cx, q, args.steps, args.warmup, "config 3 without Fst")
-        extra["t2d_t1d_only"] = {"ms_per_step": rr["dt"] / args.steps * 1e3,
-                                 "windows_per_s": n_windows(rr["gathered"]) * args.steps / rr["dt"],
-                                 "note": "the same loop, T2D + T1D only (Hudson Fst not computed)"}
+        ms_f, ms_n = [], []
+        for _ in range(3):
+            rr = run_loop(cx, q, args.steps, args.warmup, "config 3 without Fst")
+            ms_n.append(rr["dt"] / args.steps * 1e3)
+            rf = run_loop(cx, plans, args.steps, args.warmup, "config 3 (Fst, repeat)")
+            ms_f.append(rf["dt"] / args.steps * 1e3)
         for x in q:
             x.close()
+        mf, mn = float(np.median(ms_f)), float(np.median(ms_n))
+        extra["t2d_t1d_only"] = {"ms_per_step": mn, "windows_per_s": n_windows(rr["gathered"]) / (mn * 1e-3),
+                                 "ms_per_step_runs": ms_n, "with_fst_ms_per_step_runs": ms_f,
+                                 "note": "the same loop, T2D + T1D only (Hudson Fst not computed); three loops "
+                                         "interleaved with three more of the Fst loop, medians"}
+        extra["fst_cost_interleaved"] = mf / mn - 1.0
+        # BASELINE configs[2] names 20 kb AND 500 kb windows: both from one k_prep pass (sfs2d_plan_attach:
+        # the 500 kb plan scanned from the 20 kb base's pass), T2D + T1D + Fst on both
+        bases = [cx.eng.plan(dev, cfg) for _ in range(ns)]
+        att = [b.attach(ScanConfig(n1p=POP, n2p=POP, window=500_000, fst=True, scan_wgs_per_cu=1)) for b in bases]
+        rm = run_loop(cx, bases, args.steps, args.warmup, "config 3, 20 kb + 500 kb")
+        w20 = n_windows(rm["gathered"])
+        a0 = att[(args.steps - 1) % ns].read()
+        w500 = int(((a0["flags"] & 0x80000000) == 0).sum())
+        ms = rm["dt"] / args.steps * 1e3
+        bpm = algorithmic_bytes(p.n, 0, w20 + w500, "pipeline")
+        extra["config3_20kb_500kb"] = {
+            "ms_per_step": ms, "windows_20kb": w20, "windows_500kb": w500,
+            "windows_per_s": (w20 + w500) / (ms * 1e-3),
+            "roofline_pipeline": {"achieved": bpm / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": bpm / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+            "note": "BASELINE configs[2]'s two window sizes per step: one k_prep pass, the 500 kb plan attached to "
+                    "the 20 kb base (its slots by binary search on the resident positions), both scans with "
+                    "Fst; 2 plans on 2 streams as the headline loop"}
+        for b in bases:
+            b.close()
     nrec, grids, kname = plans[0].nrec, plans[0].grids(), plans[0].scan_kernel()
     for x in plans:
         x.close()
@@ -557,7 +586,9 @@ def main():
         }
         if "t2d_t1d_only" in c3:
             line["t2d_t1d_only"] = c3["t2d_t1d_only"]
-            line["fst_cost"] = c3["ms_per_step"] / c3["t2d_t1d_only"]["ms_per_step"] - 1.0
+            line["fst_cost"] = c3["fst_cost_interleaved"]
+        if "config3_20kb_500kb" in c3:
+            line["config3_20kb_500kb"] = c3["config3_20kb_500kb"]
         if c2 is not None:
             line["config2_weak"] = c2
         if not args.no_cpu_baseline and world == 1:

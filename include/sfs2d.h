@@ -103,7 +103,14 @@ typedef struct {
 int sfs2d_ctx_create(int device, sfs2d_ctx** out);
 int sfs2d_ctx_destroy(sfs2d_ctx* ctx);
 const char* sfs2d_last_error(const sfs2d_ctx* ctx);
-int sfs2d_ctx_set_stream(sfs2d_ctx* ctx, void* hip_stream);   /* NULL = the ctx's own stream */
+/* Stream the ctx enqueues on.  sfs2d_ctx_set_stream(ctx, s): the caller's HIP stream s; NULL is the
+ * HIP null stream (the legacy default stream: ordered with every blocking stream of the process, e.g.
+ * torch's default stream), never a private one.  sfs2d_ctx_use_own_stream: the ctx's own non-blocking
+ * stream (the state after sfs2d_ctx_create), which NOTHING orders against the caller's streams --
+ * synchronise before handing buffers across.  The class state these replace is the reference object's
+ * (twoDSFS_class.py:21-33): one ctx per GPU, calls serialised by the caller. */
+int sfs2d_ctx_set_stream(sfs2d_ctx* ctx, void* hip_stream);
+int sfs2d_ctx_use_own_stream(sfs2d_ctx* ctx);
 int sfs2d_abi_version(void);
 
 /* data set: packed SNPs in scan order (sorted by chromosome string, then position) */
@@ -163,10 +170,9 @@ int sfs2d_plan_run(sfs2d_plan* plan, sfs2d_window* out_dev);
 /* enqueue `nruns` back-to-back runs (no host work in between; benchmarks and batch replays) */
 int sfs2d_plan_run_many(sfs2d_plan* plan, int nruns, sfs2d_window* out_dev);
 /* enqueue `nruns` runs round-robin over `nplans` distinct plans of one ctx: run i is plans[i % nplans]
- * on streams[i % nplans] (NULL = the ctx's own stream) into outs[i % nplans] (outs NULL or an entry
- * NULL = plan-owned).  Independent scans (replicates, data sets, repeated passes) overlap across the
- * streams; each plan's own runs stay ordered on its stream.  SFS2D_ENQ_THREADS=1 (distinct
- * streams): every plan's runs are enqueued by a host thread of its own, joined before return.  The
+ * on streams[i % nplans] (NULL = the HIP null stream, as sfs2d_ctx_set_stream) into outs[i % nplans]
+ * (outs NULL or an entry NULL = plan-owned).  Independent scans (replicates, data sets, repeated
+ * passes) overlap across the streams; each plan's own runs stay ordered on its stream.  The
  * ctx stream is unchanged after.  The runs are only enqueued: synchronise the passed streams before
  * sfs2d_plan_read / _check / _fst_read / _destroy of these plans (those synchronise the ctx stream
  * only). */
@@ -213,7 +219,7 @@ int sfs2d_plan_attach(sfs2d_plan* base, const sfs2d_params* params, sfs2d_plan**
 /* launch geometry (threads per grid) of k_prep and of the scan kernel: matches the Grid_Size column
  * of rocprofv3 kernel traces, so profiles can be joined to a plan */
 int sfs2d_plan_grids(const sfs2d_plan* plan, int64_t* prep_threads, int64_t* scan_threads);
-/* name of the scan kernel the plan launches ("k_scan_wl", "k_scan_w", "k_scan_gw", "k_scan_g"; the
+/* name of the scan kernel the plan launches ("k_scan_w", "k_scan_gw", "k_scan_g"; the
  * prefix of its rocprofv3 kernel name), NULL for a null plan */
 const char* sfs2d_plan_scan_kernel(const sfs2d_plan* plan);
 /* cumulative number of windows re-evaluated on the exact path (|T| ~ 0: proportionality test) */
@@ -237,39 +243,6 @@ int sfs2d_plan_timing_read(sfs2d_plan* plan, int* nruns, double* ms_k1, double* 
 /* standalone timing loop: average device time per kernel over `iters` runs */
 int sfs2d_plan_time(sfs2d_plan* plan, int iters, double* ms_per_run, double* ms_k1, double* ms_k2, double* ms_k3);
 int sfs2d_plan_destroy(sfs2d_plan* plan);
-
-/* ---- multi-GPU, native step loop: one process per GPU, each rank scanning its own data set (the
- * drivers' split at window boundaries lives in sfs2d/dist.py), one RCCL
- * all-gather of the fixed-stride window tables per scan (replaces the reference's
- * single-process loop over every window, twoDSFS_class.py:787-991).  RCCL is loaded at the first
- * call (dlopen librccl.so.1: the copy torch already loaded, else the ROCm one).
- * sfs2d_dist_unique_id: rank 0 makes the 128-byte communicator id the caller broadcasts;
- * sfs2d_dist_create: every rank joins (blocks until all `world` ranks have called it);
- * sfs2d_dist_scan_gather: `nsteps` back-to-back scans of `plan`, step s writing its records into
- * outs[s & 1] on the library stream, then all-gathering `rows` 64-B records from every rank into
- * gathered[s & 1] on `comm_stream` while the next step scans (the scan of step s + 2 waits for the
- * gather of step s); comm_stream NULL: each gather follows its scan on the library's stream (no
- * cross-stream events).  Steps are numbered from `first_step`.  Enqueue only: synchronise the
- * streams to wait; synchronise before switching between the two modes.
- * sfs2d_dist_set_gather: 0 (the default) = ncclAllGather into every rank's buffers; 1 = one
- * ncclGather to rank 0 per step (the reference's results have one consumer; only rank 0's `gathered`
- * buffers are written, the other ranks' are left alone).  SFS2D_E_ARG for 1 when the loaded RCCL
- * lacks ncclGather.  SFS2D_GATHER=root makes 1 the create-time default. */
-typedef struct sfs2d_dist sfs2d_dist;
-int sfs2d_dist_unique_id(uint8_t* id128);
-int sfs2d_dist_create(sfs2d_ctx* ctx, const uint8_t* id128, int rank, int world, sfs2d_dist** out);
-int sfs2d_dist_scan_gather(sfs2d_dist* d, sfs2d_plan* plan, void* out0, void* out1, void* gathered0,
-                           void* gathered1, int64_t rows, int64_t first_step, int nsteps, void* comm_stream);
-/* sfs2d_dist_scan_gather_streams: the same loop with consecutive steps spread over `nplans`
- * distinct plans on their own streams: steps go in groups of nplans, plan k of a group scanning on
- * streams[k] into table (group & 1) * nplans + k of `outbuf` (2 * nplans * rows records); then ONE
- * gather (or all-gather) of the group's tables (nplans * rows records per rank, rank-major) into
- * gathered[group & 1] (world * nplans * rows records each) on streams[0].  A last partial group
- * gathers its m < nplans tables.  One communicator; scans of a group overlap across the streams. */
-int sfs2d_dist_scan_gather_streams(sfs2d_dist* d, sfs2d_plan* const* plans, void* const* streams, int nplans,
-                                   void* outbuf, void* gathered0, void* gathered1, int64_t rows, int nsteps);
-int sfs2d_dist_set_gather(sfs2d_dist* d, int to_root);
-int sfs2d_dist_destroy(sfs2d_dist* d);
 
 /* one-shot convenience: plan + run + read (+ supplied background when bg2d != NULL) */
 int sfs2d_scan(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_params* params, const double* bg2d,

@@ -12,6 +12,10 @@ pytestmark = pytest.mark.gpu
 def test_sharded_drivers_two_ranks_on_gpu(golden, tmp_path):
     got = run_dist_workers("gpu", 2, str(tmp_path / "out.json"), extra=("all",), timeout=360)
     assert check_dist_results(got, golden) >= 45
+    # most calls (the sims batch included: its factory exchanges in HBM) ran split, not by the
+    # whole-chromosome fallback (which only the error cases take)
+    st = got["_stats"]
+    assert st["split"] >= 30 and st["allreduce"] >= 10 and st["fallback"] <= 12, st
 
 
 @pytest.mark.timeout(300)

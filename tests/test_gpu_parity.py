@@ -640,11 +640,12 @@ def test_wrapped_u8_bins_take_the_exact_path():
     _records_vs_oracle(q, ScanConfig(n1p=25, n2p=25, window=200000), ocfg, O.bp_windows(q, 200000), lambda k: bgs[k])
 
 
-@pytest.mark.parametrize("lite", ["0", "1"])
-def test_scan_kernels_agree(monkeypatch, lite):
-    """k_scan_wl (six waves per SIMD, opt-in for counts plans on small grids: SFS2D_LITE=1) and k_scan_w
-    (SFS2D_LITE=0): both against the oracle on fixed-bp and SNP-count windows, with Fst."""
-    monkeypatch.setenv("SFS2D_LITE", lite)
+@pytest.mark.parametrize("env", ["SFS2D_FUSED=1", "SFS2D_FUSED=0"])
+def test_scan_kernels_agree(monkeypatch, env):
+    """k_scan_w with its table built in the prologue (fused) and from k_bg_slice's (sliced): both against
+    the oracle on fixed-bp and SNP-count windows, with Fst."""
+    k, v = env.split("=")
+    monkeypatch.setenv(k, v)
     from sfs2d import _lib as L
     from sfs2d.engine import Engine, ScanConfig
     from sfs2d.synth import synth_genome
@@ -672,12 +673,11 @@ def test_scan_kernels_agree(monkeypatch, lite):
     dev.close()
 
 
-@pytest.mark.parametrize("env", ["SFS2D_LITE=1", "SFS2D_LITE=0", "SFS2D_FST_SCAN=0"])
+@pytest.mark.parametrize("env", ["SFS2D_FUSED=1", "SFS2D_FUSED=0", "SFS2D_FST_SCAN=0"])
 def test_fst_low_called_counts(monkeypatch, env):
     """SNPs with fewer than 2 called alleles in ONE population leave Hudson's Fst sums (oracle.window_fst
-    keeps SNPs with >= 2 in both): the scan kernels' per-SNP terms (k_scan_wl from the LDS reciprocals,
-    k_scan_w from the (alt, ref) table, k_prep's fixed-point sums) must drop them whatever the other
-    population holds."""
+    keeps SNPs with >= 2 in both): the scan kernels' per-SNP terms (k_scan_w's, fused and sliced, k_prep's
+    fixed-point sums) must drop them whatever the other population holds."""
     k, v = env.split("=")
     monkeypatch.setenv(k, v)
     from sfs2d import _lib as L

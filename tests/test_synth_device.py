@@ -92,3 +92,64 @@ def test_generator_slots_equal_segmentation(monkeypatch, ws):
     finally:
         dev.close()
     assert outs[0] == outs[1]
+
+
+@pytest.mark.timeout(600)
+def test_config4_shape_generator_slots_vs_oracle():
+    """BASELINE config 4's own path at its own shape: pop_size 50 / 50 (101 x 101 grid -> k_scan_gw),
+    2,000 windows of 20 kb per replicate, Poisson(358.5) SNPs per window, replicates generated in HBM,
+    the slot table from the generator's window offsets (k_slots_synth, the default for this plan), the
+    generation's background = every replicate's SNPs at pos <= 500,000 (sims_scan.py:615-617, 1D
+    spectra UNFOLDED, quirk Q7).  The device background equals the oracle's on the host twin's arrays
+    bit for bit; a sample of windows of three replicates (first / middle / last) equals the oracle's
+    restatement of process_window's per-window statistics (sims_scan.py:451-590: T2D, T1D of both
+    populations against the unfolded 1D background, snp_count, the inner totals)."""
+    from oracle import sfs_oracle as O
+    from sfs2d import _lib as L
+    from sfs2d.engine import Engine, ScanConfig
+    from sfs2d.synth import miss_table, sims_host, sims_window_counts
+    n, nwin, nrep, ws = 50, 2000, 20, 20000
+    seed, gen = 0xC0F4, 2
+    wc = sims_window_counts(seed, gen, nrep, nwin)
+    assert wc.min() > 0
+    mt = miss_table(2 * n)
+    host = sims_host(seed, gen, nwin, ws, n, n, wc, range(nrep), mt, mt)
+    o2, o1, o1b = O.sims_backgrounds(host, n, n)
+    eng = Engine.get(0)
+    dev = eng.synth_sims(seed, gen, nrep, nwin, ws, n, n, wc, mt, mt)
+    try:
+        h2, u1, u2 = eng.bg_hist(dev, ScanConfig(n1p=n, n2p=n, start_position=0, end_position=500000), -1)
+        assert np.array_equal(h2.reshape(o2.shape), o2)
+        assert np.array_equal(u1, o1) and np.array_equal(u2, o1b)
+        bg = (h2.reshape(-1).astype(np.float64), u1[: n + 1].astype(np.float64), u2[: n + 1].astype(np.float64))
+        pl = eng.plan(dev, ScanConfig(n1p=n, n2p=n, window=ws, bg_mode=L.BG_SUPPLIED))
+        assert pl.scan_kernel() == "k_scan_gw"
+        pl.set_background(*bg)
+        pl.run()
+        pl.check()
+        recs = pl.read()
+        pl.close()
+    finally:
+        dev.close()
+    assert len(recs) == nrep * nwin
+    assert np.array_equal(recs["chrom"], np.repeat(np.arange(nrep), nwin))
+    assert np.array_equal(recs["end"] - recs["begin"], wc.astype(np.uint32))
+    cfg = O.Cfg(n, n)
+    rng = np.random.default_rng(11)
+    checked = 0
+    for r in (0, nrep // 2, nrep - 1):
+        for w in np.sort(rng.choice(nwin, size=40, replace=False)):
+            x = recs[r * nwin + w]
+            b, e = int(x["begin"]), int(x["end"])
+            idx = np.arange(b, e)
+            assert host.chrom_off[r] <= b and e <= host.chrom_off[r + 1]
+            g = O.sfs2d(host, idx, cfg)
+            f1, f2 = O.fold1d(O.sfs1d(host, idx, 1, cfg)), O.fold1d(O.sfs1d(host, idx, 2, cfg))
+            assert int(x["snp_count"]) == e - b
+            assert int(x["n2"]) == int(g.ravel()[1:-1].sum())
+            assert int(x["n1a"]) == int(f1[1:-1].sum()) and int(x["n1b"]) == int(f2[1:-1].sum())
+            for f, want in (("t2d", O.clr2d(g, o2, guards=False)), ("t1d_p1", O.clr1d(f1, o1, guards=False)),
+                            ("t1d_p2", O.clr1d(f2, o1b, guards=False))):
+                assert gu.close(float(x[f]), want), (r, w, f, float(x[f]), want)
+            checked += 1
+    assert checked == 120
