@@ -64,15 +64,11 @@ constexpr int RCPN = 512;         // (1/k, 1/(k(k-1))) for k < 512 (Fst: called 
 constexpr int PA_ROWS = 256;      // Fst per population and SNP: (p, A) = (a / n, a (a-1) / (n (n-1))) by (n, a), a <= n < PA_ROWS,
 constexpr int PA_N = PA_ROWS * (PA_ROWS + 1) / 2;   // row n at n (n + 1) / 2 (a triangle), after RCPN; (0, 0) for n < 2
 constexpr int LDT8 = 256;         // k_scan_w8: D(r) for u8 ranks r < 255 in LDS; D(255) = NaN marks a wrapped byte
-#ifndef SFS2D_W8_U1
-#define SFS2D_W8_U1 0
+// k_scan_w8's per-wave 1D histogram words: the folded bins 0..pop_size in R1 replicas
+__host__ __device__ inline int w8_h1_words(int n1p, int n2p) { return 4 * (n1p + 1) + 4 * (n2p + 1); }
+#ifndef SFS2D_ABL   // ablation builds (timing only, results wrong): bit 0 no 2D atomic, 1 no 1D atomics, 2 no D / lp
+#define SFS2D_ABL 0  // reads, 3 no record stores, 4 no Fst table reads, 5 no 1D end pass
 #endif
-// k_scan_w8's per-wave 1D histogram words: (SFS2D_W8_U1) the UNFOLDED spectra, bins 0..2 pop_size in
-// two lane-&-1 replicas (an SNP's bin is its raw alt count: two operations per population; folded at
-// the window's end), else the folded bins 0..pop_size in R1 replicas
-__host__ __device__ inline int w8_h1_words(int n1p, int n2p) {
-  return SFS2D_W8_U1 ? 2 * (2 * n1p + 1) + 2 * (2 * n2p + 1) : 4 * (n1p + 1) + 4 * (n2p + 1);
-}
 constexpr int REPL = 4;           // replicas of the per-chromosome background histograms
 constexpr int PW_MAX_LEAVES = 1024;  // numpy pairwise leaves (64-128 values each): grids up to 255 x 255 (u8 counts)
 constexpr int LEAVES_PER_SLICE = 4;
@@ -107,7 +103,8 @@ __device__ __forceinline__ uint32_t take_replicas(uint32_t* p, uint32_t shift) {
 }
 constexpr int FUSED_VCNT = 2 * (1536 + 256) + 16;   // k_scan_w fused prologue: word offset of the counts
 
-enum : uint32_t { ERR_KEY = 1u, ERR_GRID = 2u, ERR_OVF = 4u };   // OVF: summed background rows >= 2^32
+// OVF: summed background rows >= 2^32; WAIT: a k_pass scan item gave up waiting for its chromosome's table
+enum : uint32_t { ERR_KEY = 1u, ERR_GRID = 2u, ERR_OVF = 4u, ERR_WAIT = 8u };
 enum : uint32_t {
   BGF_B2_ZERO = 1u, BGF_B1A_ZERO = 2u, BGF_B1B_ZERO = 4u, BGF_NAN2 = 8u, BGF_NAN1A = 16u, BGF_NAN1B = 32u,
   BGF_FLOATV = 64u
@@ -636,17 +633,17 @@ __device__ __forceinline__ unsigned long long fst_fixed(double x, double scale) 
   return (unsigned long long)(__double_as_longlong(y) - 0x4338000000000000ll);
 }
 
+// k_prep's work on one tile t (work item ti: its replica is ti % REPL), by a 512-thread workgroup whose
+// dynamic LDS starts at sh_hist (k_prep, and k_pass's prep items)
 template <bool DO_BG, bool DO_SEG, bool LDS_HIST, bool DO_BINS, bool FILT, bool FST>
-__global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __restrict__ counts,
-                                                 const uint32_t* __restrict__ pos, const uint16_t* __restrict__ ann,
-                                                 const Tile* __restrict__ tiles, uint32_t* __restrict__ repl,
-                                                 uint2* __restrict__ slots, uint32_t* __restrict__ bins,
-                                                 uint32_t* __restrict__ bcount, uint32_t* __restrict__ err_word,
-                                                 int hr, const double2* __restrict__ rcp_g,
-                                                 unsigned long long* __restrict__ fsum) {
+__device__ __forceinline__ void prep_tile(const KParams& P, const Tile t, uint32_t ti, uint32_t* sh_hist,
+                                          const uint32_t* __restrict__ counts, const uint32_t* __restrict__ pos,
+                                          const uint16_t* __restrict__ ann, uint32_t* __restrict__ repl,
+                                          uint2* __restrict__ slots, uint32_t* __restrict__ bins,
+                                          uint32_t* __restrict__ bcount, uint32_t* __restrict__ err_word, int hr,
+                                          const double2* __restrict__ rcp_g, unsigned long long* __restrict__ fsum) {
   // repl / bcount: this run's parity buffers.  LDS histogram: hr interleaved copies of every word
   // (lane & (hr-1) picks one), which spreads the many same-bin atomics of a wavefront over banks.
-  extern __shared__ uint32_t sh_hist[];
   __shared__ uint32_t sh_b2;
   // FST: per-window sums of the Fst terms, int64 fixed point (num, den) for the tile's first
   // FST_LDS windows (FST_R copies each), the rest straight to the global per-slot sums
@@ -657,8 +654,7 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
   __shared__ uint32_t sh_wlo;
   STAMP(20);
   BLK_STAMP(0, 0);
-  const Tile t = tiles[blockIdx.x];
-  uint32_t* gh = repl + ((size_t)(blockIdx.x % REPL) * P.nchrom + t.chrom) * (size_t)P.nh;
+  uint32_t* gh = repl + ((size_t)(ti % REPL) * P.nchrom + t.chrom) * (size_t)P.nh;
   const int lane0 = threadIdx.x & (WAVE - 1);
   const int hsh = LDS_HIST ? (hr == 4 ? 2 : 0) : 0;
   const int rep = lane0 & (hr - 1);
@@ -878,13 +874,21 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
     uint2 a;
     uint32_t xp, xn;
   };
+  // counts / positions through buffer resources covering the tile's vectors [ab, alast + 4): a load past
+  // them (the last step's lanes beyond the tile, the unconditional reload of the step after the last)
+  // returns 0 with no memory access -- clamped to the last vector instead, those re-reads cost small
+  // tiles (config 2: 4,096 SNPs, two steps) half as many bytes again in fetches
+  const uint32_t tbytes = (alast + 4u - ab) * 4u;
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(counts + ab), (short)0, (int)tbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(pos + ab), (short)0, (int)tbytes, 0x00020000);
+  typedef int v4i __attribute__((ext_vector_type(4)));
   auto load_step = [&](uint32_t base) {
     StepIn x;
     const uint32_t ia = base + 4 * threadIdx.x;
-    const uint32_t il = min(ia, alast);
-    x.c = NEED_C ? *reinterpret_cast<const uint4*>(counts + il) : make_uint4(0, 0, 0, 0);
-    x.p = need_pos ? *reinterpret_cast<const uint4*>(pos + il) : make_uint4(0, 0, 0, 0);
-    x.a = filt ? *reinterpret_cast<const uint2*>(ann + il) : make_uint2(0, 0);
+    const int off = (int)((ia - ab) * 4u);
+    x.c = NEED_C ? __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(crs, off, 0, 0)) : make_uint4(0, 0, 0, 0);
+    x.p = need_pos ? __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(prs, off, 0, 0)) : make_uint4(0, 0, 0, 0);
+    x.a = filt ? *reinterpret_cast<const uint2*>(ann + min(ia, alast)) : make_uint2(0, 0);
     x.xp = 0;
     x.xn = 0;
     if (DO_SEG) {   // neighbour positions at the wave edges and past the tile end
@@ -1001,6 +1005,19 @@ __global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __re
   }
   STAMP(23);
   BLK_STAMP(0, 1);
+}
+
+template <bool DO_BG, bool DO_SEG, bool LDS_HIST, bool DO_BINS, bool FILT, bool FST>
+__global__ __launch_bounds__(BLOCK1) void k_prep(KParams P, const uint32_t* __restrict__ counts,
+                                                 const uint32_t* __restrict__ pos, const uint16_t* __restrict__ ann,
+                                                 const Tile* __restrict__ tiles, uint32_t* __restrict__ repl,
+                                                 uint2* __restrict__ slots, uint32_t* __restrict__ bins,
+                                                 uint32_t* __restrict__ bcount, uint32_t* __restrict__ err_word,
+                                                 int hr, const double2* __restrict__ rcp_g,
+                                                 unsigned long long* __restrict__ fsum) {
+  extern __shared__ uint32_t sh_hist[];
+  prep_tile<DO_BG, DO_SEG, LDS_HIST, DO_BINS, FILT, FST>(P, tiles[blockIdx.x], blockIdx.x, sh_hist, counts, pos, ann,
+                                                         repl, slots, bins, bcount, err_word, hr, rcp_g, fsum);
 }
 
 
@@ -2380,7 +2397,8 @@ __device__ __forceinline__ void lds_copy_d(double* dst, const double* __restrict
 // is NaN and the flush re-evaluates it exactly on a u32 histogram in global memory (gscr, as k_scan_gw).
 // Ranks never pass 254 otherwise, so no window needs the clamped D pass of the u16 bins.
 template <bool P16, bool FUSED, int FST, bool CNT, bool P8 = false>
-__device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
+// (wgi: the work item -- chunks[wgi] -- and nwg the items of the launch: k_scan_w's block index and grid)
+__device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_t nwg, SCAN_W_ARGS) {
   constexpr bool FSTIN = FST >= 2;
   constexpr bool FMASK = FST == 3 || FST == 5;
   constexpr bool PA = FST >= 4;
@@ -2388,6 +2406,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   static_assert(!P8 || (CNT && !P16), "u8-packed 2D bins: counts plans");
   static_assert(!PA || P8, "the (p, A) table takes the LDS the u8 bins free");
   constexpr int DT = P8 ? LDT8 : LNT;   // D(r) entries in LDS
+  constexpr int R1U = R1;
   constexpr int NWV = SBLOCK / WAVE;
   constexpr int SB = 8;    // windows per batch (see flush; LDS-limited: the 2 KB of the retired trash words)
   __shared__ BgHead sh_hb;
@@ -2399,7 +2418,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   const int tid = threadIdx.x;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & (WAVE - 1);
-  const Chunk ch = chunks[blockIdx.x];
+  const Chunk ch = chunks[wgi];
   const int bg = bg_per_chrom ? (int)ch.chrom : 0;
 
   // LDS: lp table (nt, rounded up to even: the histograms are 16-B aligned) | D (LNT) | F (LNF) |
@@ -2412,9 +2431,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
   const int rtn = FSTIN ? (PA ? P.rtn * (P.rtn + 1) / 2 : P.rtn) : 0;
   uint32_t* HB = reinterpret_cast<uint32_t*>(RT + rtn);
   const int h2w = P8 ? ((P.nb2 + 3) / 4 + 3) & ~3 : P16 ? ((P.nb2 + 1) / 2 + 3) & ~3 : (P.nb2 + 3) & ~3;
-  constexpr bool U1 = P8 && SFS2D_W8_U1;   // unfolded 1D spectra (w8_h1_words)
-  constexpr int R1U = U1 ? 2 : R1;         // 1D replicas per bin
-  const int h1w = U1 ? 2 * (P.n1 + 1) : R1 * (P.n1p + 1), h1wb = U1 ? 2 * (P.n2 + 1) : R1 * (P.n2p + 1);
+  const int h1w = R1 * (P.n1p + 1), h1wb = R1 * (P.n2p + 1);
   const int per = h2w + h1w + h1wb;   // (no trash words: SNPs outside the 2D SFS skip the atomic)
   uint32_t* W = HB + wv * per;
   uint32_t* H1a = W + h2w;
@@ -2458,7 +2475,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     gq1 = atomicAdd(myctr, 1u);
     gq = atomicAdd(myctr, 1u);
   }
-  if (blockIdx.x == 0)   // the other parity's counters, for the next run
+  if (wgi == 0)   // the other parity's counters, for the next run
     for (int k = tid; k < P.nchrom * CTR_POOLS; k += SBLOCK) ctr[((size_t)(1 - cpar) * P.nchrom * CTR_POOLS + k) * CTR_STRIDE] = 0u;
 
   // table copies with every load of a thread in flight at once (a load-wait-store loop paid one
@@ -2524,7 +2541,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
         sh_hb = h;
         if (writer) head[bg] = h;
       }
-      if (blockIdx.x == 0)   // the other parity's inner sums, for the next run
+      if (wgi == 0)   // the other parity's inner sums, for the next run
         for (int c = tid; c < P.nchrom; c += SBLOCK) bcount[(size_t)(1 - par) * P.nchrom + c] = 0u;
       __syncthreads();
       hb = sh_hb;
@@ -2548,10 +2565,10 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     // the other parity's replicas and inner sums: zeroed for the next run, a slice per workgroup
     // (after the last barrier: nothing waits for these stores)
     uint32_t* Ro = repl + (size_t)(1 - par) * REPL * rs;
-    const size_t tot = (size_t)REPL * rs, share = (tot + gridDim.x - 1) / gridDim.x;
-    const size_t lo = (size_t)blockIdx.x * share, hi = lo + share < tot ? lo + share : tot;
+    const size_t tot = (size_t)REPL * rs, share = (tot + nwg - 1) / nwg;
+    const size_t lo = (size_t)wgi * share, hi = lo + share < tot ? lo + share : tot;
     for (size_t k = lo + tid; k < hi; k += SBLOCK) Ro[k] = 0u;
-    if (blockIdx.x == 0)
+    if (wgi == 0)
       for (int c = tid; c < P.nchrom; c += SBLOCK) bcount[(size_t)(1 - par) * P.nchrom + c] = 0u;
   }
   if (!active) return;
@@ -2607,7 +2624,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     if (nan1b) w.t1b = __builtin_nan("");
     if (empty) { w.t2d = 0.0; w.t1a = 0.0; w.t1b = 0.0; }   // (counts 0: write_empty's record)
     if (mine && !exact)
-      write_rec(out + Bs, ch.chrom, wid, empty ? 0u : Bsb, empty ? 0u : Bse, w, empty ? SFS2D_W_EMPTY : zflags);
+      if (!(SFS2D_ABL & 8)) write_rec(out + Bs, ch.chrom, wid, empty ? 0u : Bsb, empty ? 0u : Bse, w, empty ? SFS2D_W_EMPTY : zflags);
     if (mine) {
       if (FSTIN) {   // the window's own sums
         const double fx = __longlong_as_double((long long)sh_bf[wv][0][jl]);
@@ -2637,7 +2654,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
         // a u32 histogram in global memory: a gscr slot taken by CAS (nscr slots of nb2 words, then nscr
         // lock words), left clean by the take-and-clear evaluation
         uint32_t* lock = gscr + (size_t)nscr * P.nb2;
-        uint32_t sl = (uint32_t)(blockIdx.x * NWV + wv) % (uint32_t)nscr;
+        uint32_t sl = (uint32_t)(wgi * NWV + wv) % (uint32_t)nscr;
         for (;;) {
           uint32_t got = 1u;
           if (lane == 0) got = atomicCAS(&lock[sl], 0u, 1u);
@@ -2805,8 +2822,13 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
           }
           // (a and a (a - 1) converted here: an LDS table of them, two more LDS reads per SNP, made the
           // pass slower -- 143 -> 158 us on config 3: the loop's LDS pipe is the busier one)
-          const d2v r1 = *(const lds_d2*)(uintptr_t)(rtb + 16u * n1c);
-          const d2v r2 = *(const lds_d2*)(uintptr_t)(rtb + 16u * n2c);
+          d2v r1, r2;
+          if (SFS2D_ABL & 16) {
+            r1.x = (double)n1c; r1.y = (double)n1c; r2.x = (double)n2c; r2.y = (double)n2c;
+          } else {
+            r1 = *(const lds_d2*)(uintptr_t)(rtb + 16u * n1c);
+            r2 = *(const lds_d2*)(uintptr_t)(rtb + 16u * n2c);
+          }
           fq[2 * q] = make_double2((double)a1 * r1.x, (double)__umul24(a1, a1 - 1u) * r1.y);
           fq[2 * q + 1] = make_double2((double)a2 * r2.x, (double)__umul24(a2, a2 - 1u) * r2.y);
         }
@@ -2836,7 +2858,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
         // fewer lanes in the LDS atomic.  (The address before the branch: one v_lshl_add.)
         const uint32_t wa = awb + word * 4u;
         uint32_t o = one2;   // (any value: lanes outside take rank 0; one2's register, dead after the atomic)
-        if (in2[q])
+        if (in2[q] && !(SFS2D_ABL & 1))
           o = __hip_atomic_fetch_add((lds_u32*)(uintptr_t)wa, one2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         ov[q] = o;
         xs[q] = x;
@@ -2844,11 +2866,11 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
         if (keep) kw[(j + q) & 7] = word;
         // every SNP slot adds to one bin of each folded 1D spectrum (no range test, no trash select: the
         // window's end drops bins 0 and n_p and counts n1a / n1b from them)
-        // (U1: the raw alt counts' bins, 8 B apart: two operations per population)
-        const uint32_t u1 = U1 ? a1b + (__builtin_amdgcn_ubfe(w, 8, 8) << 3) : a1b + (gp & 0xffffu);
-        const uint32_t u2 = U1 ? a2b + ((w >> 24) << 3) : a2b + (gp >> 16);
-        __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u1, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u2, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t u1 = a1b + (gp & 0xffffu), u2 = a2b + (gp >> 16);
+        if (!(SFS2D_ABL & 2)) {
+          __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u1, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u2, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
       }
       if (FSTIN) {   // (SNPs past e: counts 0, no called allele, terms 0)
         // five fp64 operations per SNP on the table's (p, A) (computed from (1/n, 1/(n(n-1))) they took
@@ -2878,8 +2900,8 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       for (int q = 0; q < 2; ++q) {
         // D[LNT-1] = 0: ranks past the table add 0 (clampd windows); elsewhere rank < nsnp <= LNT-1 and
         // the min is a no-op, cheaper than selecting it per window (P8: ranks <= 255, D(255) = NaN)
-        d[q] = P8 ? Dt[rk[q]] : Dt[min(rk[q], (uint32_t)LNT - 1u)];
-        lp[q] = LPl[kk[q]];
+        d[q] = (SFS2D_ABL & 4) ? (double)rk[q] : P8 ? Dt[rk[q]] : Dt[min(rk[q], (uint32_t)LNT - 1u)];
+        lp[q] = (SFS2D_ABL & 4) ? (double)kk[q] : LPl[kk[q]];
       }
       const double t = (d[0] - lp[0]) + (d[1] - lp[1]);
       acc2 = j == 0 ? t : acc2 + t;
@@ -2971,22 +2993,9 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
     // (counting only the live slots -- a partial row's live lanes, no row past the end -- measured 1%
     // slower: its uniform tests cost more than the same-address atomics of the padding)
     const uint32_t slots = 128u * ((nsnp + 127u) / 128u);
-    // folded bin k (<= n_p) of a population's spectrum, its replicas read and cleared (U1: fold_1d_sfs's
-    // u[k] + u[n - k], k < n_p, from the unfolded bins)
-    auto take1 = [&](uint32_t* H, int k, int np, int n) -> uint32_t {
-      if (U1) {
-        uint2* q = reinterpret_cast<uint2*>(H + 2 * k);
-        const uint2 v = *q;
-        *q = make_uint2(0u, 0u);
-        uint32_t x = v.x + v.y;
-        if (k < np) {
-          uint2* r = reinterpret_cast<uint2*>(H + 2 * (n - k));
-          const uint2 u = *r;
-          *r = make_uint2(0u, 0u);
-          x += u.x + u.y;
-        }
-        return x;
-      }
+    // folded bin k (<= n_p) of a population's spectrum, its replicas read and cleared
+    auto take1 = [&](uint32_t* H, int k) -> uint32_t {
+      if (SFS2D_ABL & 32) return (uint32_t)k;
       uint4* q = reinterpret_cast<uint4*>(H + k * R1);
       const uint4 v = *q;
       *q = make_uint4(0, 0, 0, 0);
@@ -2997,7 +3006,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       const int k = lane & 31, np = pa ? P.n1p : P.n2p;
       uint32_t x = 0;
       if (k <= np) {
-        x = take1(pa ? H1a : H1b, k, np, pa ? P.n1 : P.n2);
+        x = take1(pa ? H1a : H1b, k);
         if (k >= 1 && k < np && x) acca = xlnx<LNF>(x, Ft, lnx) - (double)x * LPl[(pa ? P.t1a : P.t1b) + k];
       }
       n1a = slots - (uint32_t)__builtin_amdgcn_readlane((int)x, 0) - (uint32_t)__builtin_amdgcn_readlane((int)x, P.n1p);
@@ -3009,12 +3018,12 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
       for (int j = 0; j < 2; ++j) {
         const int k = lane + WAVE * j;
         if (k <= P.n1p) {
-          const uint32_t x = take1(H1a, k, P.n1p, P.n1);
+          const uint32_t x = take1(H1a, k);
           xa[j] = x;
           if (k >= 1 && k < P.n1p && x) acca += xlnx<LNF>(x, Ft, lnx) - (double)x * LPl[P.t1a + k];
         }
         if (k <= P.n2p) {
-          const uint32_t x = take1(H1b, k, P.n2p, P.n2);
+          const uint32_t x = take1(H1b, k);
           xb[j] = x;
           if (k >= 1 && k < P.n2p && x) accb += xlnx<LNF>(x, Ft, lnx) - (double)x * LPl[P.t1b + k];
         }
@@ -3072,14 +3081,97 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, SCAN_W_ARGS) {
 template <bool P16, bool FUSED, int FST, bool CNT>
 __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_scan_w(SCAN_W_ARGS) {
   extern __shared__ double ldsd[];
-  scan_w_small<P16, FUSED, FST, CNT>(ldsd, SCAN_W_PASS);
+  scan_w_small<P16, FUSED, FST, CNT>(ldsd, blockIdx.x, gridDim.x, SCAN_W_PASS);
 }
 
 // k_scan_w's window loop with u8-packed 2D bins and (FST 4 / 5) the Fst (p, A) table in LDS (see scan_w_small)
 template <bool FUSED, int FST>
 __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_scan_w8(SCAN_W_ARGS) {
   extern __shared__ double ldsd[];
-  scan_w_small<false, FUSED, FST, true, true>(ldsd, SCAN_W_PASS);
+  scan_w_small<false, FUSED, FST, true, true>(ldsd, blockIdx.x, gridDim.x, SCAN_W_PASS);
+}
+
+// ------------------------------------------------------------------------------------------ one pass
+// k_pass: a whole plan run (per-chromosome backgrounds, counts plan, small grid) in ONE launch of resident
+// workgroups that take work items by ticket: the k_prep tiles of every chromosome and the window-scan
+// chunks of k_scan_w, in an order that puts chromosome c's scan chunks after the tiles of c + 1
+// (PassX::items).  A tile item is k_prep's work on the tile; the tile that completes its chromosome
+// (per-chromosome counter) builds the chromosome's background table -- fused_table, k_scan_w's fused
+// prologue, once per chromosome instead of once per scan workgroup -- into the global tables, clears
+// the chromosome's replicas and publishes it (ready[c] = epoch, release).  A scan item waits for its
+// chromosome's flag (acquire), copies the table and scans (scan_w_small, the non-fused path).  A
+// workgroup only waits for tiles with smaller tickets, taken by running workgroups that never wait, so
+// the wait always ends (and is bounded: ERR_WAIT); the bandwidth-bound tile items of later chromosomes
+// run beside the scan items of earlier ones -- the overlap two streams of independent passes give,
+// inside one pass.
+struct PassX {
+  const uint32_t* pos;
+  const Tile* tiles;
+  const uint32_t* items;   // bit 31 clear: tile index; set: chunk index
+  uint32_t nitems, nchunks;
+  uint32_t* pass_ctr;      // ticket counter (the workgroup taking the last ticket resets it)
+  uint32_t* tdone;         // per chromosome: tiles completed (reset by the table builder)
+  uint32_t* ready;         // per chromosome: the epoch of its last table
+  uint32_t epoch;
+  int hr;
+};
+
+template <int FST, bool BP>
+__global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_pass(PassX X, SCAN_W_ARGS) {
+  // one work item per workgroup (grid = the items): its ticket is taken when the workgroup starts, so a
+  // scan item waits only for tiles whose workgroups are already running.  (A loop over items kept every
+  // kernel argument live across both item kinds: 380 SGPRs spilled to VGPR lanes, 83 VGPRs to scratch.)
+  extern __shared__ double ldsd[];
+  __shared__ uint32_t sh_item, sh_last;
+  __shared__ BgHead sh_hbp;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    const uint32_t t = atomicAdd(X.pass_ctr, 1u);
+    if (t == X.nitems - 1u) atomicExch(X.pass_ctr, 0u);   // every ticket taken: reset for the next run
+    sh_item = X.items[t];
+  }
+  __syncthreads();
+  const uint32_t it = sh_item;
+  if (!(it >> 31)) {
+    const Tile tl = X.tiles[it];
+    prep_tile<true, BP, true, false, false, false>(P, tl, it, reinterpret_cast<uint32_t*>(ldsd), bins, X.pos, nullptr,
+                                                    repl, slots, nullptr, bcount, err_word, X.hr, nullptr, nullptr);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // this tile's histogram adds before its count
+    __syncthreads();
+    if (tid == 0) sh_last = atomicAdd(&X.tdone[tl.chrom], 1u) + 1u == tl.pad1;   // (pad1: the chromosome's tiles)
+    __syncthreads();
+    if (!sh_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const uint32_t c = tl.chrom;
+    const size_t rs = (size_t)P.nchrom * P.nh;
+    uint32_t* HB = reinterpret_cast<uint32_t*>(ldsd + ((P.nt + 1) & ~1));   // (LPl = ldsd, then scratch)
+    fused_table(P.nb2, P.nh, P.nt, P.n1p, P.n2p, P.n1, P.n2, P.t1a, P.t1b, P.nchrom, c, true, (int)c,
+                repl + (size_t)c * P.nh, rs, repl, bcount, 0, tab, LPg, head, ldsd, HB, leaves, nleaves, nodes,
+                nnodes, nlevels, lnx, &sh_hbp, reinterpret_cast<double*>(HB) + 1536, HB + FUSED_VCNT);
+    for (int k = tid; k < REPL * P.nh; k += SBLOCK) repl[(size_t)(k / P.nh) * rs + (size_t)c * P.nh + k % P.nh] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // the table before the flag
+    __syncthreads();
+    if (tid == 0) {
+      bcount[c] = 0u;
+      X.tdone[c] = 0u;
+      __hip_atomic_store(&X.ready[c], X.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  const uint32_t ci = it & 0x7fffffffu;
+  if (tid == 0) {
+    const uint32_t c = chunks[ci].chrom;
+    for (uint32_t spin = 0; __hip_atomic_load(&X.ready[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != X.epoch; ++spin) {
+      if (spin == (1u << 22)) {   // (~1 s of s_sleep: a table that never came -- reported, never a hang)
+        atomicOr(err_word, ERR_WAIT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(4);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  scan_w_small<true, false, FST, true>(ldsd, ci, X.nchunks, SCAN_W_PASS);
 }
 
 // K3 for large grids, one wavefront per window (LDS: the wave's histograms only)
