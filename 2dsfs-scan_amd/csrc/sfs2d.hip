@@ -95,7 +95,7 @@ struct sfs2d_ctx {
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   double* d_lnx = nullptr;
-  double* d_df = nullptr;   // D(r), F(x) (LNT each), then (1/k, 1/(k(k-1))) pairs (RCPN), then Fst (p, A) by (n, a) (PA_N, a triangle)
+  double* d_df = nullptr;   // D(r), F(x) (LNT each), then (1/k, 1/(k(k-1))) pairs (RCPN)
   std::string err;
   std::mutex err_mu;
 };
@@ -202,13 +202,6 @@ struct sfs2d_plan {
   bool fst_win = false;           // Fst by window kernels (fst_windows) instead of k_prep's sums
   bool fst_scan = false;          // Fst summed by k_scan_w itself (counts plans, small grids): k_prep has no Fst work
   bool fst_mask = true;           // Fst in the scan: the data set has SNPs with < 2 called alleles (k_scan_w FST 3 / 5)
-  bool w8 = false;                // k_scan_w8 (counts plans, small grids): u8 2D bins, Fst's (p, A) table in LDS
-  bool onepass = false;           // k_pass: the whole run (tiles + tables + scan) in one launch (see plan_create)
-  std::vector<uint32_t> items;    // k_pass work items in ticket order (bit 31: a scan chunk, else a tile)
-  uint32_t* d_items = nullptr;
-  uint32_t* d_pass_ctr = nullptr; // k_pass ticket counter
-  uint32_t* d_ready = nullptr;    // k_pass: per chromosome, the run epoch of its last background table
-  int pass_grid = 0;
   int nfst = 0;                   // k_bg_slice's extra Fst workgroups
 };
 
@@ -254,7 +247,6 @@ void plan_free(sfs2d_plan* p) {
   hipFree(p->d_done); hipFree(p->d_bgval); hipFree(p->d_tab); hipFree(p->d_lp); hipFree(p->d_head);
   hipFree(p->d_bg1d); hipFree(p->d_leafsum); hipFree(p->d_leaves); hipFree(p->d_nodes); hipFree(p->d_slices);
   hipFree(p->d_out); hipFree(p->d_err); hipFree(p->d_bins); hipFree(p->d_fst); hipFree(p->d_fsum); hipFree(p->d_gscr);
-  hipFree(p->d_items); hipFree(p->d_pass_ctr); hipFree(p->d_ready);
   for (auto& e : p->ev) if (e) hipEventDestroy(e);
   for (auto& e : p->tev) if (e) hipEventDestroy(e);
 }
@@ -279,40 +271,6 @@ void launch_scan_w(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
                      (int)(pl->runs & 1), pl->d_leafsum, pl->d_bg1d, pl->sliced ? 1 : 0, nullptr, 0);
 }
 
-template <bool FUSED, int FST>
-void launch_scan_w8(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
-  hipExtLaunchKernelGGL((k_scan_w8<FUSED, FST>), dim3((unsigned)pl->chunks.size()), dim3(SBLOCK), pl->scan_lds,
-                     CTX_STREAM(pl->ctx), pl->kev[4], pl->kev[5], 0, pl->K, scan_src(pl), pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
-                     per_chrom, pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, bp, pl->d_repl, pl->d_bcount,
-                     plan_par(pl), pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels,
-                     pl->extra_rec >= 0 ? (int)pl->last_chrom : -1, pl->d_fsum, pl->d_fst, pl->d_ctr,
-                     (int)(pl->runs & 1), pl->d_leafsum, pl->d_bg1d, pl->sliced ? 1 : 0, pl->d_gscr, pl->nscr);
-}
-
-template <int FST, bool BP>
-void launch_pass_t(sfs2d_plan* pl, sfs2d_window* out) {
-  PassX X;
-  X.pos = pl->data->pos; X.tiles = pl->d_tiles; X.items = pl->d_items; X.nitems = (uint32_t)pl->items.size();
-  X.nchunks = (uint32_t)pl->chunks.size(); X.pass_ctr = pl->d_pass_ctr; X.tdone = pl->d_done; X.ready = pl->d_ready;
-  X.epoch = (uint32_t)(pl->runs % 0xfffffffeull) + 1u;   // (never 0: the flags' initial value)
-  X.hr = pl->hr;
-  hipExtLaunchKernelGGL((k_pass<FST, BP>), dim3((unsigned)pl->items.size()), dim3(SBLOCK), pl->scan_lds, CTX_STREAM(pl->ctx),
-                        pl->kev[4], pl->kev[5], 0, X, pl->K, scan_src(pl), pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp,
-                        pl->d_head, 1, pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, BP ? 1 : 0, pl->d_repl, pl->d_bcount, 0,
-                        pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels,
-                        pl->extra_rec >= 0 ? (int)pl->last_chrom : -1, pl->d_fsum, pl->d_fst, pl->d_ctr, (int)(pl->runs & 1),
-                        pl->d_leafsum, pl->d_bg1d, 0, pl->d_gscr, pl->nscr);
-}
-
-hipError_t launch_pass(sfs2d_plan* pl, sfs2d_window* out) {
-  const int f = !pl->fst ? 0 : pl->fst_mask ? 3 : 2;
-  const bool bp = pl->prm.window_mode == SFS2D_WINDOW_BP;
-  if (f == 0) bp ? launch_pass_t<0, true>(pl, out) : launch_pass_t<0, false>(pl, out);
-  else if (f == 2) bp ? launch_pass_t<2, true>(pl, out) : launch_pass_t<2, false>(pl, out);
-  else bp ? launch_pass_t<3, true>(pl, out) : launch_pass_t<3, false>(pl, out);
-  return hipGetLastError();
-}
-
 template <bool P16, bool FST, bool CNT>
 void launch_scan_g(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
   hipExtLaunchKernelGGL((k_scan_g<P16, FST, CNT>), dim3((unsigned)pl->chunks.size()), dim3(BLOCK), pl->scan_lds,
@@ -333,19 +291,6 @@ template <bool P16, bool CNT>
 hipError_t launch_scan_c(sfs2d_plan* pl, sfs2d_window* out) {
   const int per_chrom = pl->prm.bg_mode == SFS2D_BG_PER_CHROM ? 1 : 0;
   const int bp = pl->prm.window_mode == SFS2D_WINDOW_BP ? 1 : 0;
-  if (CNT && pl->w8) {
-    const int f = !pl->fst ? 0 : pl->fst_mask ? 5 : 4;
-    if (pl->fused) {
-      if (f == 0) launch_scan_w8<true, 0>(pl, out, per_chrom, bp);
-      else if (f == 4) launch_scan_w8<true, 4>(pl, out, per_chrom, bp);
-      else launch_scan_w8<true, 5>(pl, out, per_chrom, bp);
-    } else {
-      if (f == 0) launch_scan_w8<false, 0>(pl, out, per_chrom, bp);
-      else if (f == 4) launch_scan_w8<false, 4>(pl, out, per_chrom, bp);
-      else launch_scan_w8<false, 5>(pl, out, per_chrom, bp);
-    }
-    return hipGetLastError();
-  }
   if (pl->gw) {
     if (pl->fst) launch_scan_gw<P16, true, CNT>(pl, out, per_chrom, bp);
     else launch_scan_gw<P16, false, CNT>(pl, out, per_chrom, bp);
@@ -543,11 +488,11 @@ int sfs2d_ctx_create(int device, sfs2d_ctx** out) {
   c->stream = c->own;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) c->ncu = prop.multiProcessorCount;
-  if (dalloc(c, &c->d_lnx, LNX_N) || dalloc(c, &c->d_df, 2 * LNT + 2 * RCPN + 2 * PA_N)) {
+  if (dalloc(c, &c->d_lnx, LNX_N) || dalloc(c, &c->d_df, 2 * LNT + 2 * RCPN)) {
     hipFree(c->d_lnx); hipStreamDestroy(c->own); delete c; return SFS2D_E_NOMEM;
   }
   hipLaunchKernelGGL(k_init_lnx, dim3(LNX_N / 256), dim3(256), 0, c->stream, c->d_lnx, c->d_df, c->d_df + LNT,
-                     c->d_df + 2 * LNT, c->d_df + 2 * LNT + 2 * RCPN);
+                     c->d_df + 2 * LNT);
   if (hipStreamSynchronize(c->stream) != hipSuccess) {
     hipFree(c->d_lnx); hipFree(c->d_df); hipStreamDestroy(c->own); delete c; return SFS2D_E_HIP;
   }
@@ -1024,39 +969,6 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   }
   const PwTree pw = pw_plan(K.nb2 - 3);
   pl->fst_mask = data->low_nc;
-  // k_scan_w8 for counts plans on the small-grid path whose Fst, if any, is summed in the scan: u8 2D
-  // bins (wrapped bytes re-evaluated exactly) leave LDS for Fst's (p, A) table by (n, a) -- two 16-B
-  // reads per SNP and no conversions or products.  Needs the data's called counts < 128
-  // (the table's rows, and the refs' bit 7 clear) and the workgroup to fit twice per CU beside its
-  // static LDS.  SFS2D_W8=0: k_scan_w (u16 bins, reciprocal table).
-  pl->w8 = false;
-  if (pl->cnt && pl->G == WAVE && !pl->gw && (!pl->fst || pl->fst_scan) && pl->K.rtn <= 128) {
-    const int h2w8 = ((K.nb2 + 3) / 4 + 3) & ~3;
-    const int per8 = h2w8 + w8_h1_words(K.n1p, K.n2p);
-    const size_t hist8 = std::max<size_t>((size_t)(SBLOCK / WAVE) * per8, (size_t)FUSED_VCNT + K.nt + 16);
-    const size_t pa = pl->fst ? (size_t)pl->K.rtn * (pl->K.rtn + 1) : 0;   // doubles: rtn (rtn + 1) / 2 (p, A) pairs
-    const size_t lds8 = sizeof(double) * (size_t)(((K.nt + 1) & ~1) + LDT8 + LNF + pa) + hist8 * 4;
-    hipFuncAttributes fa{};
-    const void* f = pl->fst ? (const void*)k_scan_w8<true, 5> : (const void*)k_scan_w8<true, 0>;
-    const size_t stat = hipFuncGetAttributes(&fa, f) == hipSuccess ? fa.sharedSizeBytes : 8192;
-    const char* ev = std::getenv("SFS2D_W8");
-    if (lds8 + stat <= 80 * 1024 && ev && ev[0] == '1') {   // (opt-in: slower than k_scan_w on config 3)
-      pl->w8 = true;
-      pl->scan_lds = lds8;
-    }
-  }
-  // k_pass (one launch per run: the tiles, each chromosome's table built once by its last tile, the scan
-  // chunks -- DESIGN.md) for counts plans with per-chromosome backgrounds on k_scan_w's path (u16 bins), Fst
-  // summed in the scan or none, not run by phases (SFS2D_F_PHASED).  It replaces k_prep + the fused /
-  // sliced tables + k_scan_w; attaching a plan (sfs2d_plan_attach) turns the base back to the fused path
-  // (so the replicas keep both parities).  SFS2D_ONEPASS=0: the three-kernel pass.
-  pl->onepass = false;
-  if (pl->cnt && pl->do_bg && pl->G == WAVE && !pl->gw && !pl->w8 && pl->p16 && (!pl->fst || pl->fst_scan) &&
-      !(prm->flags & SFS2D_F_PHASED) && force_sliced < 0 /* not an attached plan */) {
-    const char* ev = std::getenv("SFS2D_ONEPASS");
-    pl->onepass = !(ev && ev[0] == '0');
-  }
-  if (pl->onepass) { pl->fused = false; pl->sliced = false; }
   pl->fst_win = pl->sliced && bp && pl->fst && !pl->fst_scan;
   pl->nfst = pl->fst_win ? (int)std::min<int64_t>(1024, std::max<int64_t>(1, (pl->nslots + 7) / 8)) : 0;   // ~1 window per wave
   if (pl->scan_lds > 64 * 1024) {
@@ -1074,10 +986,6 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
                           (const void*)k_scan_w<true, false, 2, true>, (const void*)k_scan_w<false, false, 2, true>,
                           (const void*)k_scan_w<true, true, 3, true>, (const void*)k_scan_w<false, true, 3, true>,
                           (const void*)k_scan_w<true, false, 3, true>, (const void*)k_scan_w<false, false, 3, true>,
-                          (const void*)k_scan_w8<true, 0>, (const void*)k_scan_w8<true, 4>, (const void*)k_scan_w8<true, 5>,
-                          (const void*)k_scan_w8<false, 0>, (const void*)k_scan_w8<false, 4>, (const void*)k_scan_w8<false, 5>,
-                          (const void*)k_pass<0, true>, (const void*)k_pass<2, true>, (const void*)k_pass<3, true>,
-                          (const void*)k_pass<0, false>, (const void*)k_pass<2, false>, (const void*)k_pass<3, false>,
                           (const void*)k_scan_g<true, false, false>, (const void*)k_scan_g<false, false, false>,
                           (const void*)k_scan_g<true, true, false>, (const void*)k_scan_g<false, true, false>,
                           (const void*)k_scan_g<true, false, true>, (const void*)k_scan_g<false, false, true>,
@@ -1099,12 +1007,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
     int occ = 0;
     // (the grid is one dispatch wave of resident workgroups: occupancy of the variant that runs)
     hipError_t oe;
-    if (pl->onepass)
-      oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_pass<3, true>, SBLOCK, pl->scan_lds);
-    else if (pl->w8)
-      oe = pl->fused ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w8<true, 5>, SBLOCK, pl->scan_lds)
-                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w8<false, 5>, SBLOCK, pl->scan_lds);
-    else if (pl->gw)
+    if (pl->gw)
       oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<true, true, true>, WAVE, pl->scan_lds)
                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<false, true, true>, WAVE, pl->scan_lds);
     else if (pl->fst_scan && pl->fused)
@@ -1120,13 +1023,9 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
       oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<true, false, true, true>, SBLOCK, pl->scan_lds)
                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_w<false, false, true, true>, SBLOCK, pl->scan_lds);
     if (oe != hipSuccess || occ < 1) occ = 1;
-    // (k_pass: all the resident workgroups, no cap -- its tile items are the pass's own k_prep)
-    if (!pl->onepass && prm->scan_wgs_per_cu > 0 && (int)prm->scan_wgs_per_cu < occ) occ = (int)prm->scan_wgs_per_cu;
-    pl->pass_grid = occ * ctx->ncu;
+    if (prm->scan_wgs_per_cu > 0 && (int)prm->scan_wgs_per_cu < occ) occ = (int)prm->scan_wgs_per_cu;
     int64_t cap = (int64_t)occ * ctx->ncu;
     if (pl->gw) pl->nscr = (int)cap;   // one exact-path histogram per resident wavefront
-    // k_scan_w8: exact evaluations are rare (|T| ~ 0, a wrapped u8 bin): a few shared slots, taken by CAS
-    if (pl->w8) pl->nscr = (int)std::min<int64_t>(256, cap * (SBLOCK / WAVE));
     if (const char* ev = std::getenv("SFS2D_WGS")) cap = std::max<int64_t>(1, std::atoll(ev));   // tuning
     const double S = (double)std::max<unsigned long long>(1, slot_base[nc] - slot_base[0]);
     const uint32_t NW = pl->gw ? 1u : (uint32_t)(SBLOCK / WAVE);   // wavefronts per workgroup
@@ -1200,22 +1099,6 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
         t.nslots = (uint32_t)(slot_base[c + 1] - slot_base[c]);
         pl->tiles.push_back(t);
       }
-    // k_pass: every tile carries its chromosome's tile count (the completion counter's target), and the
-    // work items go in ticket order -- the tiles of chromosome c, then the scan chunks of c - 1, so that a
-    // chunk's table is (nearly) built by the time a workgroup takes it
-    std::vector<uint32_t> ntc(std::max(1, nc), 0);
-    for (const Tile& t : pl->tiles) ntc[t.chrom]++;
-    for (Tile& t : pl->tiles) t.pad1 = ntc[t.chrom];
-    if (pl->onepass) {
-      std::vector<std::vector<uint32_t>> tof(std::max(1, nc)), cof(std::max(1, nc));
-      for (size_t i = 0; i < pl->tiles.size(); ++i) tof[pl->tiles[i].chrom].push_back((uint32_t)i);
-      for (size_t i = 0; i < pl->chunks.size(); ++i) cof[pl->chunks[i].chrom].push_back((uint32_t)i | 0x80000000u);
-      for (int c = 0; c < nc; ++c) {
-        pl->items.insert(pl->items.end(), tof[c].begin(), tof[c].end());
-        if (c > 0) pl->items.insert(pl->items.end(), cof[c - 1].begin(), cof[c - 1].end());
-      }
-      if (nc > 0) pl->items.insert(pl->items.end(), cof[nc - 1].begin(), cof[nc - 1].end());
-    }
   }
   // one LDS copy per histogram word: four interleaved copies (lane & 3, fewer same-address atomics)
   // cost more in zeroing and flushing than they saved (k_prep config 2 10.3 vs 10.9 us, config 3
@@ -1279,21 +1162,14 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   rc = rc ? rc : dalloc(ctx, &pl->d_tiles, pl->tiles.size());
   rc = rc ? rc : dalloc(ctx, &pl->d_chunks, pl->chunks.size());
   rc = rc ? rc : dalloc(ctx, &pl->d_slots, (size_t)pl->nslots + 1);
-  // (fused plans alternate two replica parities; k_pass plans keep room for both: attaching a plan turns
-  // the base fused)
-  const size_t nrepl = pl->do_bg ? (size_t)((pl->fused || pl->onepass) ? 2 : 1) * REPL * nc * K.nh : 1;
+  const size_t nrepl = pl->do_bg ? (size_t)(pl->fused ? 2 : 1) * REPL * nc * K.nh : 1;
   rc = rc ? rc : dalloc(ctx, &pl->d_repl, nrepl);
   rc = rc ? rc : dalloc(ctx, &pl->d_bcount, (size_t)2 * std::max(1, nc));
   rc = rc ? rc : dalloc(ctx, &pl->d_done, (size_t)pl->nbg);
-  if (pl->onepass) {
-    rc = rc ? rc : dalloc(ctx, &pl->d_items, pl->items.size());
-    rc = rc ? rc : dalloc(ctx, &pl->d_pass_ctr, 1);
-    rc = rc ? rc : dalloc(ctx, &pl->d_ready, (size_t)pl->nbg);
-  }
   const size_t nctr = (size_t)2 * std::max(1, nc) * CTR_POOLS * CTR_STRIDE;
   rc = rc ? rc : dalloc(ctx, &pl->d_ctr, nctr);
-  const size_t ngscr = (pl->gw || pl->w8) ? (size_t)pl->nscr * (K.nb2 + 1) : 0;
-  if (pl->gw || pl->w8) rc = rc ? rc : dalloc(ctx, &pl->d_gscr, ngscr);
+  const size_t ngscr = pl->gw ? (size_t)pl->nscr * (K.nb2 + 1) : 0;
+  if (pl->gw) rc = rc ? rc : dalloc(ctx, &pl->d_gscr, ngscr);
   rc = rc ? rc : dalloc(ctx, &pl->d_bgval, (size_t)pl->nbg * K.nt);
   rc = rc ? rc : dalloc(ctx, &pl->d_tab, (size_t)pl->nbg * K.nt);
   rc = rc ? rc : dalloc(ctx, &pl->d_lp, (size_t)pl->nbg * K.nt);
@@ -1317,16 +1193,13 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   PCPY(pl->d_leaves, pw.leaves);
   PCPY(pl->d_nodes, pw.nodes);
   PCPY(pl->d_slices, pl->slices);
-  PCPY(pl->d_items, pl->items);
 #undef PCPY
-  if (e == hipSuccess && pl->onepass) e = hipMemsetAsync(pl->d_pass_ctr, 0, sizeof(uint32_t), st);
-  if (e == hipSuccess && pl->onepass) e = hipMemsetAsync(pl->d_ready, 0, sizeof(uint32_t) * pl->nbg, st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_slots, 0, sizeof(uint2) * ((size_t)pl->nslots + 1), st);
   if (e == hipSuccess && pl->do_bg) e = hipMemsetAsync(pl->d_repl, 0, sizeof(uint32_t) * nrepl, st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_bcount, 0, sizeof(uint32_t) * 2 * std::max(1, nc), st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_done, 0, sizeof(uint32_t) * pl->nbg, st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_ctr, 0, sizeof(uint32_t) * nctr, st);
-  if (e == hipSuccess && (pl->gw || pl->w8)) e = hipMemsetAsync(pl->d_gscr, 0, sizeof(uint32_t) * ngscr, st);
+  if (e == hipSuccess && pl->gw) e = hipMemsetAsync(pl->d_gscr, 0, sizeof(uint32_t) * ngscr, st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_err, 0, 4 * sizeof(uint32_t), st);
   if (e == hipSuccess) e = hipMemsetAsync(pl->d_bins, 0, sizeof(uint32_t) * nbins, st);
   if (e == hipSuccess && pl->fst) e = hipMemsetAsync(pl->d_fsum, 0, sizeof(unsigned long long) * 2 * ((size_t)pl->nslots + 1), st);
@@ -1385,25 +1258,6 @@ int sfs2d_plan_run_phase(sfs2d_plan* pl, int phase, sfs2d_window* out_dev) {
     return 0;
   };
   int rc = 0;
-  if (pl->onepass) {   // k_pass: the whole run in one launch (its duration in the scan kernel's timing slot)
-    if (phase != 0) return set_err(ctx, SFS2D_E_ARG, "a plan run by phases needs SFS2D_F_PHASED at creation");
-    if ((rc = mark(0)) || (rc = mark(2))) return rc;
-    sfs2d_window* out = out_dev ? out_dev : pl->d_out;
-    if (pl->items.empty()) {
-      if ((rc = mark(4))) return rc;
-    } else {
-      HIPCHK(ctx, launch_pass(pl, out));
-    }
-    if (pl->extra_rec >= 0) {
-      const hipError_t ex = pl->cnt ? launch_extra<true, true>(pl, out) : launch_extra<true, false>(pl, out);
-      HIPCHK(ctx, ex);
-    }
-    pl->last_out = out;
-    pl->runs++;
-    for (auto& e : pl->kev) e = nullptr;
-    if (te) pl->tcount++;
-    return 0;
-  }
   if (phase == 0 || phase == 1) {
     if (synth_seg(pl)) {
       HIPCHK(ctx, launch_slots_synth(pl));
@@ -1434,18 +1288,14 @@ int sfs2d_plan_run_phase(sfs2d_plan* pl, int phase, sfs2d_window* out_dev) {
 
 int sfs2d_plan_grids(const sfs2d_plan* pl, int64_t* prep_threads, int64_t* scan_threads) {
   if (!pl) return SFS2D_E_ARG;
-  if (prep_threads) *prep_threads = pl->onepass ? 0 : (int64_t)pl->tiles.size() * BLOCK1;
-  if (scan_threads)
-    *scan_threads = pl->onepass ? (int64_t)pl->items.size() * SBLOCK
-                                : (int64_t)pl->chunks.size() * (pl->G == WAVE ? SBLOCK : pl->gw ? WAVE : BLOCK);
+  if (prep_threads) *prep_threads = (int64_t)pl->tiles.size() * BLOCK1;
+  if (scan_threads) *scan_threads = (int64_t)pl->chunks.size() * (pl->G == WAVE ? SBLOCK : pl->gw ? WAVE : BLOCK);
   return 0;
 }
 
 const char* sfs2d_plan_scan_kernel(const sfs2d_plan* pl) {
   if (!pl) return nullptr;
   if (pl->gw) return "k_scan_gw";
-  if (pl->w8) return "k_scan_w8";
-  if (pl->onepass) return "k_pass";
   return pl->G == WAVE ? "k_scan_w" : "k_scan_g";
 }
 
@@ -1637,7 +1487,6 @@ int sfs2d_plan_check(sfs2d_plan* pl) {
     HIPCHK(ctx, hipMemsetAsync(pl->d_err, 0, 4, CTX_STREAM(ctx)));
     HIPCHK(ctx, hipStreamSynchronize(CTX_STREAM(ctx)));
     if (e & ERR_OVF) return set_err(ctx, SFS2D_E_ARG, "summed background histograms overflow uint32");
-    if (e & ERR_WAIT) return set_err(ctx, SFS2D_E_HIP, "k_pass: a scan item gave up waiting for its chromosome's background table");
     if (e & ERR_KEY) return set_err(ctx, SFS2D_E_KEY, "allele count above 2*pop_size (reference: KeyError in calculate_1d_sfs)");
     return set_err(ctx, SFS2D_E_GRID, "folded 2D bin outside the (2n1+1)x(2n2+1) grid");
   }
@@ -1737,12 +1586,6 @@ int sfs2d_plan_attach(sfs2d_plan* base, const sfs2d_params* prm, sfs2d_plan** ou
   sfs2d_ctx* ctx = base->ctx;
   *out = nullptr;
   if (base->base) return set_err(ctx, SFS2D_E_ARG, "attach to a base plan, not to an attached one");
-  if (base->onepass) {   // the attached scans read the base's k_prep replicas: the base goes back to the fused
-                         // path (its replicas have both parities; k_pass left them zeroed)
-    HIPCHK(ctx, hipStreamSynchronize(CTX_STREAM(ctx)));
-    base->onepass = false;
-    base->fused = true;
-  }
   const bool large = base->do_bg && base->G != WAVE;   // tables from the base's k_bg_slice (with its tail)
   if (!base->fused && !base->sliced && !large)
     return set_err(ctx, SFS2D_E_ARG, "attached plans need a per-chromosome-background base plan");
@@ -1755,7 +1598,7 @@ int sfs2d_plan_attach(sfs2d_plan* base, const sfs2d_params* prm, sfs2d_plan** ou
   sfs2d_plan* a = nullptr;
   int rc = plan_create(ctx, base->data, prm, base->sliced ? 1 : 0, &a);
   if (rc) return rc;
-  if (a->fused != base->fused || a->sliced != base->sliced || a->G != base->G || a->cnt != base->cnt || a->w8 != base->w8) {
+  if (a->fused != base->fused || a->sliced != base->sliced || a->G != base->G || a->cnt != base->cnt) {
     plan_free(a); delete a;
     return set_err(ctx, SFS2D_E_ARG, "attached plan would take a different kernel path than its base");
   }

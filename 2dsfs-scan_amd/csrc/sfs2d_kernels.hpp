@@ -61,14 +61,9 @@ constexpr int LNF = 256;          // k_scan_w: x ln x entries in LDS (x < LNF; t
 // count of double2
 __host__ __device__ inline int wl_rtn(int n1p, int n2p) { return 2 * (n1p > n2p ? n1p : n2p) + 2; }
 constexpr int RCPN = 512;         // (1/k, 1/(k(k-1))) for k < 512 (Fst: called allele counts ref + alt <= 510), after the LNT tables
-constexpr int PA_ROWS = 256;      // Fst per population and SNP: (p, A) = (a / n, a (a-1) / (n (n-1))) by (n, a), a <= n < PA_ROWS,
-constexpr int PA_N = PA_ROWS * (PA_ROWS + 1) / 2;   // row n at n (n + 1) / 2 (a triangle), after RCPN; (0, 0) for n < 2
-constexpr int LDT8 = 256;         // k_scan_w8: D(r) for u8 ranks r < 255 in LDS; D(255) = NaN marks a wrapped byte
-// k_scan_w8's per-wave 1D histogram words: the folded bins 0..pop_size in R1 replicas
-__host__ __device__ inline int w8_h1_words(int n1p, int n2p) { return 4 * (n1p + 1) + 4 * (n2p + 1); }
 #ifndef SFS2D_ABL   // ablation builds (timing only, results wrong): bit 0 no 2D atomic, 1 no 1D atomics, 2 no D / lp
-#define SFS2D_ABL 0  // reads, 3 no record stores, 4 no Fst table reads, 5 no 1D end pass
-#endif
+#define SFS2D_ABL 0  // reads, 3 no record stores, 4 no Fst table reads, 5 no 1D end pass; k_prep's common step:
+#endif              // 6 no LDS histogram atomics, 7 loads only (no classification, histograms or segmentation)
 constexpr int REPL = 4;           // replicas of the per-chromosome background histograms
 constexpr int PW_MAX_LEAVES = 1024;  // numpy pairwise leaves (64-128 values each): grids up to 255 x 255 (u8 counts)
 constexpr int LEAVES_PER_SLICE = 4;
@@ -103,8 +98,7 @@ __device__ __forceinline__ uint32_t take_replicas(uint32_t* p, uint32_t shift) {
 }
 constexpr int FUSED_VCNT = 2 * (1536 + 256) + 16;   // k_scan_w fused prologue: word offset of the counts
 
-// OVF: summed background rows >= 2^32; WAIT: a k_pass scan item gave up waiting for its chromosome's table
-enum : uint32_t { ERR_KEY = 1u, ERR_GRID = 2u, ERR_OVF = 4u, ERR_WAIT = 8u };
+enum : uint32_t { ERR_KEY = 1u, ERR_GRID = 2u, ERR_OVF = 4u };   // OVF: summed background rows >= 2^32
 enum : uint32_t {
   BGF_B2_ZERO = 1u, BGF_B1A_ZERO = 2u, BGF_B1B_ZERO = 4u, BGF_NAN2 = 8u, BGF_NAN1A = 16u, BGF_NAN1B = 32u,
   BGF_FLOATV = 64u
@@ -512,21 +506,12 @@ __device__ __forceinline__ uint32_t bin_g2(uint32_t w) { return (w >> 23) & 0x7f
 
 // ln k for k < LNX_N; F(x) = x ln x for x < LNT; D(r) = F(r+1) - F(r) for r < LNT-1 and
 // D(LNT-1) = 0 (k_scan_w adds the ranks from LNT-1 on per bin, as F(x) - F(LNT-1))
-__global__ void k_init_lnx(double* lnx, double* dtab, double* ftab, double* rtab, double* patab) {
+__global__ void k_init_lnx(double* lnx, double* dtab, double* ftab, double* rtab) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < LNX_N) lnx[i] = i ? log((double)i) : 0.0;
   if (i < RCPN) {   // Fst: (1/n, 1/(n(n-1))) per called allele count n; 0 below n = 2 (not in the set)
     rtab[2 * i] = i >= 2 ? 1.0 / (double)i : 0.0;
     rtab[2 * i + 1] = i >= 2 ? 1.0 / ((double)i * (double)(i - 1)) : 0.0;
-  }
-  if (i < PA_N) {   // Fst: one population's (p, A) by the triangle index n (n + 1) / 2 + a (k_scan_w8 stages
-                    // rows n < P.rtn in LDS): both correctly rounded quotients of exact integers
-    uint32_t n = (uint32_t)((sqrt(8.0 * (double)i + 1.0) - 1.0) * 0.5);
-    while (n * (n + 1u) / 2u > (uint32_t)i) --n;
-    while ((n + 1u) * (n + 2u) / 2u <= (uint32_t)i) ++n;
-    const uint32_t a = (uint32_t)i - n * (n + 1u) / 2u;
-    patab[2 * i] = n >= 2u ? (double)a / (double)n : 0.0;
-    patab[2 * i + 1] = n >= 2u ? (double)(a * (a - 1u)) / (double)(n * (n - 1u)) : 0.0;
   }
   if (i < LNT) {
     const double a = i ? (double)i * log((double)i) : 0.0;
@@ -634,7 +619,7 @@ __device__ __forceinline__ unsigned long long fst_fixed(double x, double scale) 
 }
 
 // k_prep's work on one tile t (work item ti: its replica is ti % REPL), by a 512-thread workgroup whose
-// dynamic LDS starts at sh_hist (k_prep, and k_pass's prep items)
+// dynamic LDS starts at sh_hist
 template <bool DO_BG, bool DO_SEG, bool LDS_HIST, bool DO_BINS, bool FILT, bool FST>
 __device__ __forceinline__ void prep_tile(const KParams& P, const Tile t, uint32_t ti, uint32_t* sh_hist,
                                           const uint32_t* __restrict__ counts, const uint32_t* __restrict__ pos,
@@ -684,6 +669,14 @@ __device__ __forceinline__ void prep_tile(const KParams& P, const Tile t, uint32
       atomicAdd(&fsum[2 * ((size_t)t.sbase + wid)], qn);
       atomicAdd(&fsum[2 * ((size_t)t.sbase + wid) + 1], qd);
     }
+  };
+  // the empty window slots of the chromosome are written too ((0, 0): before its first SNP's window, in
+  // the gaps, after its last SNP's window), by the lane holding the SNP next to them: the whole table is
+  // rewritten every run, so the scan kernels need not clear it (a scattered 8-B store per window)
+  auto zero_slots = [&](uint32_t a, uint32_t b) {
+#ifndef SFS2D_XSLOT
+    for (uint32_t s = a; s < b; ++s) slots[(size_t)t.sbase + s] = make_uint2(0u, 0u);
+#endif
   };
   // FILT: a position or variant_type filter is set (kept out of the common kernel: its uniform
   // flags would otherwise occupy scalar registers throughout the loop)
@@ -773,7 +766,14 @@ __device__ __forceinline__ void prep_tile(const KParams& P, const Tile t, uint32
         const int bit = __builtin_ctz(c), k = bit >> 1;
         const uint32_t wk = k == 0 ? w[0] : k == 1 ? w[1] : k == 2 ? w[2] : w[3];
         uint32_t* sl = reinterpret_cast<uint32_t*>(slots + ((size_t)t.sbase + wk));
-        sl[bit & 1] = i0 + k + 1u;   // .x = first + 1, .y = last + 1 (0 = unset; the scan kernel clears them)
+        sl[bit & 1] = i0 + k + 1u;   // .x = first + 1, .y = last + 1 (0: an empty slot)
+        const uint32_t i = i0 + k;
+        if (bit & 1) {   // the empty slots after the window: to the next SNP's window or the chromosome's end
+          const uint32_t qn = k == 0 ? w[1] : k == 1 ? w[2] : k == 2 ? w[3] : wnext;
+          zero_slots(wk + 1u, i + 1u == t.ce ? t.nslots : qn);
+        } else if (i == t.cb) {   // the chromosome's empty slots before its first SNP
+          zero_slots(0u, wk);
+        }
       }
     }
     if (DO_BINS) {
@@ -821,7 +821,7 @@ __device__ __forceinline__ void prep_tile(const KParams& P, const Tile t, uint32
       const uint32_t g1 = min(a1, (uint32_t)Q.n1 - a1), g2 = min(a2, (uint32_t)Q.n2 - a2);
       const uint32_t f1 = g1 - 1u < n1pm1 ? g1 : 0u, f2 = g2 - 1u < n2pm1 ? g2 : 0u;
       bw[k] = (last ? B_LAST : k2) | (f1 << 16) | (f2 << 23) | B_VAR;
-      if (DO_BG) {
+      if (DO_BG && !(SFS2D_ABL & 64)) {
         atomicAdd(in2 ? (uint32_t*)((char*)hist_l + (k2 << s2)) : trash_p, 1u);
         atomicAdd(a1 ? (uint32_t*)((char*)h1a_l + (a1 << s2)) : trash_p, 1u);
         atomicAdd(a2 ? (uint32_t*)((char*)h1b_l + (a2 << s2)) : trash_p, 1u);
@@ -857,7 +857,10 @@ __device__ __forceinline__ void prep_tile(const KParams& P, const Tile t, uint32
         const uint32_t qp = k ? w[k - 1] : wprev, qn = k < 3 ? w[k + 1] : wnext;
         uint32_t* sl = reinterpret_cast<uint32_t*>(slots + ((size_t)t.sbase + w[k]));
         if (qp != w[k]) sl[0] = i0 + k + 1u;   // .x = first + 1, .y = last + 1
-        if (qn != w[k]) sl[1] = i0 + k + 1u;
+        if (qn != w[k]) {
+          sl[1] = i0 + k + 1u;
+          zero_slots(w[k] + 1u, qn);   // (a step of the fast path holds neither chromosome end)
+        }
       }
     }
     if (DO_BINS) *reinterpret_cast<uint4*>(bins + i0) = make_uint4(bw[0], bw[1], bw[2], bw[3]);
@@ -881,7 +884,6 @@ __device__ __forceinline__ void prep_tile(const KParams& P, const Tile t, uint32
   const uint32_t tbytes = (alast + 4u - ab) * 4u;
   const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(counts + ab), (short)0, (int)tbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(pos + ab), (short)0, (int)tbytes, 0x00020000);
-  typedef int v4i __attribute__((ext_vector_type(4)));
   auto load_step = [&](uint32_t base) {
     StepIn x;
     const uint32_t ia = base + 4 * threadIdx.x;
@@ -924,8 +926,8 @@ __device__ __forceinline__ void prep_tile(const KParams& P, const Tile t, uint32
     // (called allele counts r + a by byte dot products)
     auto nc1 = [](uint32_t c) { return __builtin_amdgcn_udot4(c, 0x00000101u, 0u, false); };
     auto nc2 = [](uint32_t c) { return __builtin_amdgcn_udot4(c, 0x01010000u, 0u, false); };
-    const bool bad = (max(max(nc1(ca.x), nc1(ca.y)), max(nc1(ca.z), nc1(ca.w))) > (uint32_t)P.n1) |
-                     (max(max(nc2(ca.x), nc2(ca.y)), max(nc2(ca.z), nc2(ca.w))) > (uint32_t)P.n2);
+    const bool bad = (int)(max(max(nc1(ca.x), nc1(ca.y)), max(nc1(ca.z), nc1(ca.w))) > (uint32_t)P.n1) |
+                     (int)(max(max(nc2(ca.x), nc2(ca.y)), max(nc2(ca.z), nc2(ca.w))) > (uint32_t)P.n2);
     // the masked edge path: a step reaching outside the tile (only a chromosome's first / last tile
     // has unaligned ends: the host puts tile edges on multiples of 4 SNPs) or holding the
     // chromosome's first or last SNP (window starts / ends there whatever the neighbours' ids)
@@ -937,7 +939,8 @@ __device__ __forceinline__ void prep_tile(const KParams& P, const Tile t, uint32
 #ifdef SFS2D_MARK
       asm volatile("; HOT_BEGIN");
 #endif
-      process_fast(ia, ca, pa, wpa, wna);
+      if (SFS2D_ABL & 128) asm volatile("" ::"v"(ca.x), "v"(ca.y), "v"(ca.z), "v"(ca.w), "v"(pa.x), "v"(pa.w), "v"(wpa), "v"(wna));
+      else process_fast(ia, ca, pa, wpa, wna);
 #ifdef SFS2D_MARK
       asm volatile("; HOT_END");
 #endif
@@ -1637,7 +1640,7 @@ __device__ __forceinline__ double xlnx(uint32_t x, const double* Ft, const doubl
 // scratch; clears this workgroup's share of the other parity's replicas; the chromosome's first
 // workgroup (writer) also writes the global tables.  The head lands in *hb_out (LDS).
 __device__ __forceinline__ void fused_table(int nb2, int nh, int nt, int n1p, int n2p, int n1, int n2,
-                                                      int t1a, int t1b, int nchrom, uint32_t chrom, bool writer,
+                                            int t1a, int t1b, int nchrom, uint32_t chrom, bool writer,
                                                       int bg, const uint32_t* __restrict__ Rc, size_t rs,
                                                       uint32_t* __restrict__ repl, uint32_t* __restrict__ bcount,
                                                       int par, PL* __restrict__ tab, double* __restrict__ LPg,
@@ -2212,7 +2215,6 @@ __device__ __forceinline__ void scan_gw_body(double* ldsd, SCAN_W_ARGS) {
     }
     if (lane == 0) {
       write_rec(out + s, ch.chrom, wid, cur.b, cur.e, w, zflags);
-      if (mode_bp) slots[s] = make_uint2(0u, 0u);   // leave the slot table clean for the next run
     }
     group_sync<WAVE>();
     if (it == 0) STAMP(14);
@@ -2389,23 +2391,13 @@ __device__ __forceinline__ void lds_copy_d(double* dst, const double* __restrict
 // membership = an inner 2D bin; the unfolded last bin in the rare pass), fp64 lane sums in a fixed order
 // and two wave sums per window: k_prep then runs without the Fst work (DESIGN.md "Fst placement");
 // 3: as 2, for data sets where some SNP has < 2 called alleles in a population (those SNPs masked out)
-// P8 (k_scan_w8, counts plans): the 2D bins u8-packed (a quarter of u32 bins: 652 words at 51 x 51
-// instead of u16's 1,304), which frees the LDS for FST 4 / 5: Hudson's per-population (p, A) read from
-// an LDS table by (n, a) -- one 16-B read per population and SNP, no conversions or products -- instead
-// of (1/n, 1/(n(n-1))) times a and a (a-1).  A 2D atomic returning rank 255 means the byte wrapped (the
-// bin's 256th SNP of the window; the carry corrupts a neighbour): D(255) is NaN, so the window's 2D sum
-// is NaN and the flush re-evaluates it exactly on a u32 histogram in global memory (gscr, as k_scan_gw).
-// Ranks never pass 254 otherwise, so no window needs the clamped D pass of the u16 bins.
-template <bool P16, bool FUSED, int FST, bool CNT, bool P8 = false>
+template <bool P16, bool FUSED, int FST, bool CNT>
 // (wgi: the work item -- chunks[wgi] -- and nwg the items of the launch: k_scan_w's block index and grid)
 __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_t nwg, SCAN_W_ARGS) {
   constexpr bool FSTIN = FST >= 2;
-  constexpr bool FMASK = FST == 3 || FST == 5;
-  constexpr bool PA = FST >= 4;
+  constexpr bool FMASK = FST == 3;
   static_assert(!FSTIN || CNT, "Fst in the scan reads the counts");
-  static_assert(!P8 || (CNT && !P16), "u8-packed 2D bins: counts plans");
-  static_assert(!PA || P8, "the (p, A) table takes the LDS the u8 bins free");
-  constexpr int DT = P8 ? LDT8 : LNT;   // D(r) entries in LDS
+  constexpr int DT = LNT;   // D(r) entries in LDS
   constexpr int R1U = R1;
   constexpr int NWV = SBLOCK / WAVE;
   constexpr int SB = 8;    // windows per batch (see flush; LDS-limited: the 2 KB of the retired trash words)
@@ -2427,10 +2419,10 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
   double* Dt = LPl + ((P.nt + 1) & ~1);   // DT
   double* Ft = Dt + DT;                   // LNF
   double2* RT = reinterpret_cast<double2*>(Ft + LNF);
-  // FSTIN: rtn (1/n, 1/(n(n-1))) pairs, or (PA) the (p, A) triangle of rows n < P.rtn
-  const int rtn = FSTIN ? (PA ? P.rtn * (P.rtn + 1) / 2 : P.rtn) : 0;
+  // FSTIN: rtn (1/n, 1/(n(n-1))) pairs
+  const int rtn = FSTIN ? P.rtn : 0;
   uint32_t* HB = reinterpret_cast<uint32_t*>(RT + rtn);
-  const int h2w = P8 ? ((P.nb2 + 3) / 4 + 3) & ~3 : P16 ? ((P.nb2 + 1) / 2 + 3) & ~3 : (P.nb2 + 3) & ~3;
+  const int h2w = P16 ? ((P.nb2 + 1) / 2 + 3) & ~3 : (P.nb2 + 3) & ~3;
   const int h1w = R1 * (P.n1p + 1), h1wb = R1 * (P.n2p + 1);
   const int per = h2w + h1w + h1wb;   // (no trash words: SNPs outside the 2D SFS skip the atomic)
   uint32_t* W = HB + wv * per;
@@ -2484,11 +2476,10 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
   // of config 2's ~4 us prologue): the D / F tables (two doubles per thread), and for sliced plans the
   // leaf sums, the tree nodes and the head's inputs, then the lp table
   static_assert(LNT == SBLOCK && LNF <= SBLOCK, "one D and at most one F double per thread");
-  const double dfv0 = P8 && tid == LDT8 - 1 ? __builtin_nan("") : dfg[tid], dfv1 = tid < LNF ? dfg[LNT + tid] : 0.0;
-  const double2 rtv = (FSTIN && !PA && tid < rtn) ? reinterpret_cast<const double2*>(dfg + 2 * LNT)[tid] : make_double2(0.0, 0.0);
+  const double dfv0 = dfg[tid], dfv1 = tid < LNF ? dfg[LNT + tid] : 0.0;
+  const double2 rtv = (FSTIN && tid < rtn) ? reinterpret_cast<const double2*>(dfg + 2 * LNT)[tid] : make_double2(0.0, 0.0);
   auto stage_fst = [&]() {   // Fst's LDS table
-    if (PA) lds_copy_d(reinterpret_cast<double*>(RT), dfg + 2 * LNT + 2 * RCPN, 2 * rtn);
-    else if (FSTIN && tid < rtn) RT[tid] = rtv;
+    if (FSTIN && tid < rtn) RT[tid] = rtv;
   };
   BgHead hb;
   const size_t rs = (size_t)P.nchrom * P.nh;     // replica stride
@@ -2614,10 +2605,9 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
     w.t2d = 2.0 * (B2 - xlnx<LNF>(w.n2, Ft, lnx));
     w.t1a = 2.0 * (Ba - xlnx<LNF>(w.n1a, Ft, lnx));
     w.t1b = 2.0 * (Bb - xlnx<LNF>(w.n1b, Ft, lnx));
-    // |T| this small may be an exactly proportional window: the exact evaluation below (P8: also a
-    // window whose 2D sum is NaN -- a u8 bin wrapped -- unless the background makes T2D NaN anyway)
+    // |T| this small may be an exactly proportional window: the exact evaluation below
     const bool exact = mine && !empty &&
-                       (nsnp == 0xffffu || (P8 && !nan2 && B2 != B2) || suspect_zero(w.t2d, w.n2) ||
+                       (nsnp == 0xffffu || suspect_zero(w.t2d, w.n2) ||
                         suspect_zero(w.t1a, w.n1a) || suspect_zero(w.t1b, w.n1b));
     if (nan2) w.t2d = __builtin_nan("");
     if (nan1a) w.t1a = __builtin_nan("");
@@ -2635,12 +2625,14 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
         fst_out[Bs] = fy != 0 ? (double)fx / (double)fy : __builtin_nan("");
         reinterpret_cast<ulonglong2*>(fsum)[Bs] = make_ulonglong2(0ull, 0ull);
       }
-      if (mode_bp) {   // the slot table is left clean for the next run
+    }
+#ifdef SFS2D_XSLOT
+      if (mine && mode_bp) {
         uint32_t z = 0u;
-        asm volatile("" : "+v"(z));   // (a literal 0 here was taken from a spilled register)
+        asm volatile("" : "+v"(z));
         slots[Bs] = make_uint2(z, z);
       }
-    }
+#endif
     MARK(31);
     // rare: exact re-evaluation with the bin-by-bin proportionality test (the histograms are clean)
     for (unsigned long long m = __ballot(exact); m; m &= m - 1) {
@@ -2650,28 +2642,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
       const uint32_t xn = __builtin_amdgcn_readlane(Bnv, l) & 0xffffu;
       const uint32_t xe = xn != 0xffffu ? xb + xn : (mode_bp ? slots[xs].y : xb + P.ws);
       WinOut x;
-      if (P8) {
-        // a u32 histogram in global memory: a gscr slot taken by CAS (nscr slots of nb2 words, then nscr
-        // lock words), left clean by the take-and-clear evaluation
-        uint32_t* lock = gscr + (size_t)nscr * P.nb2;
-        uint32_t sl = (uint32_t)(wgi * NWV + wv) % (uint32_t)nscr;
-        for (;;) {
-          uint32_t got = 1u;
-          if (lane == 0) got = atomicCAS(&lock[sl], 0u, 1u);
-          if (__builtin_amdgcn_readfirstlane(got) == 0u) break;
-          sl = sl + 1u == (uint32_t)nscr ? 0u : sl + 1u;
-        }
-        uint32_t* H2g = gscr + (size_t)sl * P.nb2;
-        if (FUSED)
-          x = eval_exact<WAVE, false, R1U, CNT>(P, bins, xb, xe,
-                                               TabFused{LPl, Rc, rs, P.nb2, P.n1, P.n2, P.n1p, P.h1a, P.h1b, P.t1a, P.t1b},
-                                               hb, lnx, H2g, H1a, H1b, nullptr, nullptr);
-        else
-          x = eval_exact<WAVE, false, R1U, CNT>(P, bins, xb, xe, TabLocal{tab + (size_t)bg * P.nt, LPl}, hb, lnx, H2g,
-                                               H1a, H1b, nullptr, nullptr);
-        __threadfence();   // the slot's words are clean again before it is released
-        if (lane == 0) atomicExch(&lock[sl], 0u);
-      } else if (FUSED) {
+      if (FUSED) {
         x = eval_exact<WAVE, P16, R1, CNT>(P, bins, xb, xe,
                                       TabFused{LPl, Rc, rs, P.nb2, P.n1, P.n2, P.n1p, P.h1a, P.h1b, P.t1a, P.t1b}, hb,
                                       lnx, W, H1a, H1b, nullptr, nullptr);
@@ -2771,7 +2742,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
     // trash word: 2 KB of LDS per workgroup, now the batch's).  n2 is a wave-uniform ballot count.
     const uint32_t nsnp = cur.e - cur.b;
     const int lim = (int)nsnp - lane;
-    const bool clampd = !P8 && nsnp > (uint32_t)(LNT - 1);   // some rank may pass the D table (u8: NaN at 255 instead)
+    const bool clampd = nsnp > (uint32_t)(LNT - 1);   // some rank may pass the D table
     double acc2 = 0.0;
     // FSTIN: this lane's sums of A1 + A2, p1 + p2 and p1 p2 (fst_snp's num = A1 + A2 - 2 p1 p2,
     // den = p1 + p2 - 2 p1 p2, summed per part).  Every SNP takes part: those outside the 2D SFS --
@@ -2792,26 +2763,6 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           const uint32_t w = ww[q];
-          if (PA) {
-            // entry n (n + 1) / 2 + a of the triangle: byte offset 8 (n (n + 1) + 2 a), n (n + 1) by one
-            // 24-bit multiply-add of the two byte dot products (n, n + 1); 2 a straight from the word (the
-            // refs' bit 7 is 0: called counts < 128 on this path)
-            const uint32_t n1c = __builtin_amdgcn_udot4(w, 0x00000101u, 0u, false);
-            const uint32_t n1d = __builtin_amdgcn_udot4(w, 0x00000101u, 1u, false);
-            const uint32_t n2c = __builtin_amdgcn_udot4(w, 0x01010000u, 0u, false);
-            const uint32_t n2d = __builtin_amdgcn_udot4(w, 0x01010000u, 1u, false);
-            uint32_t t1 = __builtin_amdgcn_ubfe(w, 7, 9), t2 = w >> 23;
-            if (FMASK) {
-              const bool ok = min(n1c, n2c) >= 2u;
-              t1 = ok ? t1 : 0u;
-              t2 = ok ? t2 : 0u;
-            }
-            const d2v e1 = *(const lds_d2*)(uintptr_t)(rtb + 8u * (__umul24(n1c, n1d) + t1));
-            const d2v e2 = *(const lds_d2*)(uintptr_t)(rtb + 8u * (__umul24(n2c, n2d) + t2));
-            fq[2 * q] = make_double2(e1.x, e1.y);
-            fq[2 * q + 1] = make_double2(e2.x, e2.y);
-            continue;
-          }
           const uint32_t n1c = __builtin_amdgcn_udot4(w, 0x00000101u, 0u, false);
           const uint32_t n2c = __builtin_amdgcn_udot4(w, 0x01010000u, 0u, false);
           uint32_t a1 = __builtin_amdgcn_ubfe(w, 8, 8), a2 = w >> 24;
@@ -2848,12 +2799,12 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
         else { k2 = bin_k2(w); gp = (bin_g1(w) | (bin_g2(w) << 16)) * (4u * R1); }
         in2[q] = k2 != 0u;   // (one compare: the ballot, the atomic's exec mask, the rank's select)
         n2 += __popcll(__ballot(in2[q]));
-        // low five bits: (k2 & 1) << 4, the u16 half's shift (P8: (k2 & 3) << 3, the byte's)
-        const uint32_t x = (CNT ? k2 : w) << (P8 ? 3 : 4);
-        const uint32_t word = P8 ? (k2 >> 2) : P16 ? (k2 >> 1) : k2;   // (k2 = 0: word 0, cleared after the window anyway)
+        // low five bits: (k2 & 1) << 4, the u16 half's shift
+        const uint32_t x = (CNT ? k2 : w) << 4;
+        const uint32_t word = P16 ? (k2 >> 1) : k2;   // (k2 = 0: word 0, cleared after the window anyway)
         // (v_lshlrev_b32 / v_bfe_u32 read the shift's low five bits: no mask; C's << would need one)
         uint32_t one2 = 1u;
-        if (P16 || P8) asm("v_lshlrev_b32 %0, %1, 1" : "=v"(one2) : "v"(x));
+        if (P16) asm("v_lshlrev_b32 %0, %1, 1" : "=v"(one2) : "v"(x));
         // an SNP outside the 2D SFS skips the atomic (exec mask; its rank is 0 below): no trash word,
         // fewer lanes in the LDS atomic.  (The address before the branch: one v_lshl_add.)
         const uint32_t wa = awb + word * 4u;
@@ -2894,13 +2845,13 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
       // wait held the other SNP's work back: two LDS round trips per pair instead of one)
 #pragma unroll
       for (int q = 0; q < 2; ++q)
-        rk[q] = in2[q] ? (P8 ? __builtin_amdgcn_ubfe(ov[q], xs[q], 8) : P16 ? __builtin_amdgcn_ubfe(ov[q], xs[q], 16) : ov[q]) : 0u;
+        rk[q] = in2[q] ? (P16 ? __builtin_amdgcn_ubfe(ov[q], xs[q], 16) : ov[q]) : 0u;
       double d[2], lp[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         // D[LNT-1] = 0: ranks past the table add 0 (clampd windows); elsewhere rank < nsnp <= LNT-1 and
-        // the min is a no-op, cheaper than selecting it per window (P8: ranks <= 255, D(255) = NaN)
-        d[q] = (SFS2D_ABL & 4) ? (double)rk[q] : P8 ? Dt[rk[q]] : Dt[min(rk[q], (uint32_t)LNT - 1u)];
+        // the min is a no-op, cheaper than selecting it per window
+        d[q] = (SFS2D_ABL & 4) ? (double)rk[q] : Dt[min(rk[q], (uint32_t)LNT - 1u)];
         lp[q] = (SFS2D_ABL & 4) ? (double)kk[q] : LPl[kk[q]];
       }
       const double t = (d[0] - lp[0]) + (d[1] - lp[1]);
@@ -3084,96 +3035,6 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) voi
   scan_w_small<P16, FUSED, FST, CNT>(ldsd, blockIdx.x, gridDim.x, SCAN_W_PASS);
 }
 
-// k_scan_w's window loop with u8-packed 2D bins and (FST 4 / 5) the Fst (p, A) table in LDS (see scan_w_small)
-template <bool FUSED, int FST>
-__global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_scan_w8(SCAN_W_ARGS) {
-  extern __shared__ double ldsd[];
-  scan_w_small<false, FUSED, FST, true, true>(ldsd, blockIdx.x, gridDim.x, SCAN_W_PASS);
-}
-
-// ------------------------------------------------------------------------------------------ one pass
-// k_pass: a whole plan run (per-chromosome backgrounds, counts plan, small grid) in ONE launch of resident
-// workgroups that take work items by ticket: the k_prep tiles of every chromosome and the window-scan
-// chunks of k_scan_w, in an order that puts chromosome c's scan chunks after the tiles of c + 1
-// (PassX::items).  A tile item is k_prep's work on the tile; the tile that completes its chromosome
-// (per-chromosome counter) builds the chromosome's background table -- fused_table, k_scan_w's fused
-// prologue, once per chromosome instead of once per scan workgroup -- into the global tables, clears
-// the chromosome's replicas and publishes it (ready[c] = epoch, release).  A scan item waits for its
-// chromosome's flag (acquire), copies the table and scans (scan_w_small, the non-fused path).  A
-// workgroup only waits for tiles with smaller tickets, taken by running workgroups that never wait, so
-// the wait always ends (and is bounded: ERR_WAIT); the bandwidth-bound tile items of later chromosomes
-// run beside the scan items of earlier ones -- the overlap two streams of independent passes give,
-// inside one pass.
-struct PassX {
-  const uint32_t* pos;
-  const Tile* tiles;
-  const uint32_t* items;   // bit 31 clear: tile index; set: chunk index
-  uint32_t nitems, nchunks;
-  uint32_t* pass_ctr;      // ticket counter (the workgroup taking the last ticket resets it)
-  uint32_t* tdone;         // per chromosome: tiles completed (reset by the table builder)
-  uint32_t* ready;         // per chromosome: the epoch of its last table
-  uint32_t epoch;
-  int hr;
-};
-
-template <int FST, bool BP>
-__global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_pass(PassX X, SCAN_W_ARGS) {
-  // one work item per workgroup (grid = the items): its ticket is taken when the workgroup starts, so a
-  // scan item waits only for tiles whose workgroups are already running.  (A loop over items kept every
-  // kernel argument live across both item kinds: 380 SGPRs spilled to VGPR lanes, 83 VGPRs to scratch.)
-  extern __shared__ double ldsd[];
-  __shared__ uint32_t sh_item, sh_last;
-  __shared__ BgHead sh_hbp;
-  const int tid = threadIdx.x;
-  if (tid == 0) {
-    const uint32_t t = atomicAdd(X.pass_ctr, 1u);
-    if (t == X.nitems - 1u) atomicExch(X.pass_ctr, 0u);   // every ticket taken: reset for the next run
-    sh_item = X.items[t];
-  }
-  __syncthreads();
-  const uint32_t it = sh_item;
-  if (!(it >> 31)) {
-    const Tile tl = X.tiles[it];
-    prep_tile<true, BP, true, false, false, false>(P, tl, it, reinterpret_cast<uint32_t*>(ldsd), bins, X.pos, nullptr,
-                                                    repl, slots, nullptr, bcount, err_word, X.hr, nullptr, nullptr);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // this tile's histogram adds before its count
-    __syncthreads();
-    if (tid == 0) sh_last = atomicAdd(&X.tdone[tl.chrom], 1u) + 1u == tl.pad1;   // (pad1: the chromosome's tiles)
-    __syncthreads();
-    if (!sh_last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    const uint32_t c = tl.chrom;
-    const size_t rs = (size_t)P.nchrom * P.nh;
-    uint32_t* HB = reinterpret_cast<uint32_t*>(ldsd + ((P.nt + 1) & ~1));   // (LPl = ldsd, then scratch)
-    fused_table(P.nb2, P.nh, P.nt, P.n1p, P.n2p, P.n1, P.n2, P.t1a, P.t1b, P.nchrom, c, true, (int)c,
-                repl + (size_t)c * P.nh, rs, repl, bcount, 0, tab, LPg, head, ldsd, HB, leaves, nleaves, nodes,
-                nnodes, nlevels, lnx, &sh_hbp, reinterpret_cast<double*>(HB) + 1536, HB + FUSED_VCNT);
-    for (int k = tid; k < REPL * P.nh; k += SBLOCK) repl[(size_t)(k / P.nh) * rs + (size_t)c * P.nh + k % P.nh] = 0u;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // the table before the flag
-    __syncthreads();
-    if (tid == 0) {
-      bcount[c] = 0u;
-      X.tdone[c] = 0u;
-      __hip_atomic_store(&X.ready[c], X.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return;
-  }
-  const uint32_t ci = it & 0x7fffffffu;
-  if (tid == 0) {
-    const uint32_t c = chunks[ci].chrom;
-    for (uint32_t spin = 0; __hip_atomic_load(&X.ready[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != X.epoch; ++spin) {
-      if (spin == (1u << 22)) {   // (~1 s of s_sleep: a table that never came -- reported, never a hang)
-        atomicOr(err_word, ERR_WAIT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(4);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  __syncthreads();
-  scan_w_small<true, false, FST, true>(ldsd, ci, X.nchunks, SCAN_W_PASS);
-}
-
 // K3 for large grids, one wavefront per window (LDS: the wave's histograms only)
 template <bool P16, bool FST, bool CNT>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(4))) void k_scan_gw(SCAN_W_ARGS) {
@@ -3224,7 +3085,6 @@ __global__ __launch_bounds__(BLOCK) void k_scan_g(KParams P, const uint32_t* __r
     if (FST && threadIdx.x == 0) fst_out[s] = fst_take(fsum, s);
     if (threadIdx.x == 0) {
       write_rec(out + s, ch.chrom, wid, b, e, w, bg_zero_flags(hb));
-      if (mode_bp) slots[s] = make_uint2(0u, 0u);
     }
   }
 }

@@ -20,7 +20,6 @@ WINDOW_BP, WINDOW_SNPS = 0, 1
 BG_PER_CHROM, BG_SUPPLIED = 0, 1
 F_PREV_EXTRA = 1
 F_FST = 2
-F_PHASED = 4
 W_EMPTY = 0x80000000
 W_BG2_ZERO, W_BG1A_ZERO, W_BG1B_ZERO = 0x1, 0x2, 0x4
 W_EXTRA = 0x40000000

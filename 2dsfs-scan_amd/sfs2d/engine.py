@@ -7,7 +7,6 @@ and replays the kernels.  See include/sfs2d.h for the contract.
 from __future__ import annotations
 
 import ctypes as C
-import dataclasses
 from dataclasses import dataclass
 from typing import Optional
 
@@ -31,7 +30,6 @@ class ScanConfig:
     prev_extra: bool = False
     fst: bool = False          # also compute Hudson's Fst per window slot (Plan.read_fst)
     scan_wgs_per_cu: int = 0   # cap on scan workgroups per CU (0: all that fit; see sfs2d_params)
-    phased: bool = False       # run by phases (multi-GPU split, SplitJob): SFS2D_F_PHASED
 
     def params(self) -> L.Params:
         p = L.Params()
@@ -44,8 +42,7 @@ class ScanConfig:
         p.start_pos = 0 if self.start_position is None else clamp(self.start_position)
         p.has_end = 0 if self.end_position is None else 1
         p.end_pos = 0 if self.end_position is None else clamp(self.end_position)
-        p.flags = ((L.F_PREV_EXTRA if self.prev_extra else 0) | (L.F_FST if self.fst else 0) |
-                   (L.F_PHASED if self.phased else 0))
+        p.flags = (L.F_PREV_EXTRA if self.prev_extra else 0) | (L.F_FST if self.fst else 0)
         p.scan_wgs_per_cu = int(self.scan_wgs_per_cu)
         return p
 
@@ -320,7 +317,7 @@ class SplitJob:
         self.dev = eng.upload(sub)
         self.pl = None
         try:
-            self.pl = Plan(eng, self.dev, dataclasses.replace(cfg, phased=True))
+            self.pl = Plan(eng, self.dev, cfg)
             if cfg.bg_mode == L.BG_SUPPLIED:
                 self.pl.set_background(*bg)
         except Exception:

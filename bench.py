@@ -361,7 +361,7 @@ def kernel_times(plan, runs=16):
 def single_pass_ms(cx, plan, runs=10):
     """One plan back to back on one stream: the latency of a single pass (no overlap)."""
     torch = cx.torch
-    plan.run_many(2)
+    plan.run_many(10)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     plan.run_many(runs)
@@ -404,7 +404,13 @@ def config3_strong(cx, args):
     total_windows = n_windows(r["gathered"])
     win_rank = n_windows(r["mine"])
     k1, _, k3 = kernel_times(plans[0])
-    one = single_pass_ms(cx, plans[0]) if cx.rank == 0 else None
+    # a single scan of the genome as a user runs it: the default plan (no scan grid cap), back to back
+    # on one stream
+    one = None
+    if cx.rank == 0:
+        solo = cx.eng.plan(dev, ScanConfig(n1p=POP, n2p=POP, window=WS, fst=True))
+        one = single_pass_ms(cx, solo, runs=50)
+        solo.close()
     extra = {}
     if cx.world == 1 and not args.no_variants:
         # what Hudson's Fst costs the pass: the same loop without Fst (the reference's statistics) and
@@ -459,7 +465,9 @@ def config3_strong(cx, args):
            "rank0": {"snps": sub.n, "windows": win_rank, "slots": nrec,
                      "k_prep_ms": r["k_timed_ms"][0], "scan_ms": r["k_timed_ms"][1],
                      "timed_samples": r["k_timed_samples"], "k_prep_alone_ms": k1, "scan_alone_ms": k3,
-                     "scan_kernel": kname, "single_stream_pass_ms": one, "scan_grid_threads": grids[1]}}
+                     "scan_kernel": kname, "single_stream_pass_ms": one,
+                     "single_stream_pass_windows_per_s": win_rank / (one * 1e-3) if one else None,
+                     "scan_grid_threads": grids[1]}}
     out.update(extra)
     return out, p
 

@@ -59,9 +59,6 @@ extern "C" {
 
 #define SFS2D_F_FST 2u         /* also compute Hudson's Fst per window slot (not in the reference),
                                   read with sfs2d_plan_fst_read / sfs2d_plan_fst_buffer */
-#define SFS2D_F_PHASED 4u      /* the plan will be run by phases (sfs2d_plan_run_phase 1 then 2: the multi-GPU
-                                  split); without it a per-chromosome-background plan may run its whole pass
-                                  as one kernel (k_pass), which has no phase boundary */
 
 /* window record flags */
 #define SFS2D_W_EMPTY 0x80000000u  /* slot holds no SNP (fixed-bp slot between SNPs): not a window */

@@ -27,5 +27,11 @@ for _ in range(reps):
     pl.set_timing(0)
     k1s.append(k1 * 1e3)
     k3s.append(k3 * 1e3)
+import time  # noqa: E402
+pl.check()
+t0 = time.perf_counter()
+pl.run_many(200)
+pl.check()
+pass_us = (time.perf_counter() - t0) / 200 * 1e6
 print(f"{os.path.basename(os.environ.get('SFS2D_LIB', 'libsfs2d.so'))} {which} fst={fst} [{pl.scan_kernel()}] k_prep median {np.median(k1s):.1f} us"
-      f"  scan median {np.median(k3s):.1f} us  (min {min(k3s):.1f} max {max(k3s):.1f})", flush=True)
+      f"  scan median {np.median(k3s):.1f} us  (min {min(k3s):.1f} max {max(k3s):.1f})  pass {pass_us:.1f} us", flush=True)
