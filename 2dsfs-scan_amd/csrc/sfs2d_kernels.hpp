@@ -654,7 +654,20 @@ __device__ __forceinline__ void prep_tile(const KParams& P, const Tile t, uint32
       for (int k = threadIdx.x; k < P.nh * hr + WAVE; k += BLOCK1) sh_hist[k] = 0u;
     if (threadIdx.x == 0) sh_b2 = 0u;
   }
-  if (DO_BG || FST) __syncthreads();
+  if (DO_SEG) {
+    // the slot table is rewritten every run, so that no kernel needs to clear it after reading (the
+    // scans' scattered 8-B stores, one per window): this tile first clears, with coalesced stores, the
+    // slots strictly between its first SNP's window and the next tile's first SNP's window (from slot 0
+    // in a chromosome's first tile, to the chromosome's last slot in its last one).  Only this tile's
+    // SNPs fall in those windows (it writes their ends below, after the barrier); the windows at the
+    // edges hold SNPs of two tiles and get both ends written by them, so no tile clears them.
+    const uint32_t wf = wid_fast(P, pos[t.begin]);
+    const uint32_t lo = t.begin == t.cb ? 0u : wf + 1u;
+    const uint32_t hi = t.end == t.ce ? t.nslots : wid_fast(P, pos[t.end]);
+    for (uint32_t s = lo + threadIdx.x; s < hi; s += BLOCK1)
+      if (s != wf) slots[(size_t)t.sbase + s] = make_uint2(0u, 0u);
+  }
+  if (DO_BG || FST || DO_SEG) __syncthreads();
   const uint32_t wlo = FST ? sh_wlo : 0u;
   // fixed-point add of one lane's (num, den) pair into window wid of this chromosome
   const int frep = threadIdx.x & (FST_R - 1);
@@ -669,14 +682,6 @@ __device__ __forceinline__ void prep_tile(const KParams& P, const Tile t, uint32
       atomicAdd(&fsum[2 * ((size_t)t.sbase + wid)], qn);
       atomicAdd(&fsum[2 * ((size_t)t.sbase + wid) + 1], qd);
     }
-  };
-  // the empty window slots of the chromosome are written too ((0, 0): before its first SNP's window, in
-  // the gaps, after its last SNP's window), by the lane holding the SNP next to them: the whole table is
-  // rewritten every run, so the scan kernels need not clear it (a scattered 8-B store per window)
-  auto zero_slots = [&](uint32_t a, uint32_t b) {
-#ifndef SFS2D_XSLOT
-    for (uint32_t s = a; s < b; ++s) slots[(size_t)t.sbase + s] = make_uint2(0u, 0u);
-#endif
   };
   // FILT: a position or variant_type filter is set (kept out of the common kernel: its uniform
   // flags would otherwise occupy scalar registers throughout the loop)
@@ -767,13 +772,6 @@ __device__ __forceinline__ void prep_tile(const KParams& P, const Tile t, uint32
         const uint32_t wk = k == 0 ? w[0] : k == 1 ? w[1] : k == 2 ? w[2] : w[3];
         uint32_t* sl = reinterpret_cast<uint32_t*>(slots + ((size_t)t.sbase + wk));
         sl[bit & 1] = i0 + k + 1u;   // .x = first + 1, .y = last + 1 (0: an empty slot)
-        const uint32_t i = i0 + k;
-        if (bit & 1) {   // the empty slots after the window: to the next SNP's window or the chromosome's end
-          const uint32_t qn = k == 0 ? w[1] : k == 1 ? w[2] : k == 2 ? w[3] : wnext;
-          zero_slots(wk + 1u, i + 1u == t.ce ? t.nslots : qn);
-        } else if (i == t.cb) {   // the chromosome's empty slots before its first SNP
-          zero_slots(0u, wk);
-        }
       }
     }
     if (DO_BINS) {
@@ -857,10 +855,7 @@ __device__ __forceinline__ void prep_tile(const KParams& P, const Tile t, uint32
         const uint32_t qp = k ? w[k - 1] : wprev, qn = k < 3 ? w[k + 1] : wnext;
         uint32_t* sl = reinterpret_cast<uint32_t*>(slots + ((size_t)t.sbase + w[k]));
         if (qp != w[k]) sl[0] = i0 + k + 1u;   // .x = first + 1, .y = last + 1
-        if (qn != w[k]) {
-          sl[1] = i0 + k + 1u;
-          zero_slots(w[k] + 1u, qn);   // (a step of the fast path holds neither chromosome end)
-        }
+        if (qn != w[k]) sl[1] = i0 + k + 1u;
       }
     }
     if (DO_BINS) *reinterpret_cast<uint4*>(bins + i0) = make_uint4(bw[0], bw[1], bw[2], bw[3]);
@@ -2626,13 +2621,6 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
         reinterpret_cast<ulonglong2*>(fsum)[Bs] = make_ulonglong2(0ull, 0ull);
       }
     }
-#ifdef SFS2D_XSLOT
-      if (mine && mode_bp) {
-        uint32_t z = 0u;
-        asm volatile("" : "+v"(z));
-        slots[Bs] = make_uint2(z, z);
-      }
-#endif
     MARK(31);
     // rare: exact re-evaluation with the bin-by-bin proportionality test (the histograms are clean)
     for (unsigned long long m = __ballot(exact); m; m &= m - 1) {
