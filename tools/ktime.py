@@ -33,5 +33,7 @@ t0 = time.perf_counter()
 pl.run_many(200)
 pl.check()
 pass_us = (time.perf_counter() - t0) / 200 * 1e6
+import hashlib  # noqa: E402
+digest = hashlib.sha1(pl.read().tobytes() + (pl.read_fst().tobytes() if fst else b"")).hexdigest()[:12]
 print(f"{os.path.basename(os.environ.get('SFS2D_LIB', 'libsfs2d.so'))} {which} fst={fst} [{pl.scan_kernel()}] k_prep median {np.median(k1s):.1f} us"
-      f"  scan median {np.median(k3s):.1f} us  (min {min(k3s):.1f} max {max(k3s):.1f})  pass {pass_us:.1f} us", flush=True)
+      f"  scan median {np.median(k3s):.1f} us  (min {min(k3s):.1f} max {max(k3s):.1f})  pass {pass_us:.1f} us  out {digest}", flush=True)
