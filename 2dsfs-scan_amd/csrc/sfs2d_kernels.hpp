@@ -2621,6 +2621,14 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
         reinterpret_cast<ulonglong2*>(fsum)[Bs] = make_ulonglong2(0ull, 0ull);
       }
     }
+      if (mine && mode_bp) {
+        // the slot is cleared after its read although k_prep rewrites the table every run: without this
+        // store the overlapped Fst-free config-3 pass measured 0.194-0.197 vs 0.162-0.174 ms per pass
+        // (profiles/r05r_scan_slot_store_ab.txt; with Fst no difference)
+        uint32_t z = 0u;
+        asm volatile("" : "+v"(z));   // (a literal 0 here was taken from a spilled register)
+        slots[Bs] = make_uint2(z, z);
+      }
     MARK(31);
     // rare: exact re-evaluation with the bin-by-bin proportionality test (the histograms are clean)
     for (unsigned long long m = __ballot(exact); m; m &= m - 1) {
