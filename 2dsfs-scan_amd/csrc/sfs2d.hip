@@ -96,6 +96,7 @@ struct sfs2d_ctx {
   hipStream_t stream = nullptr;
   double* d_lnx = nullptr;
   double* d_df = nullptr;   // D(r), F(x) (LNT each), then (1/k, 1/(k(k-1))) pairs (RCPN)
+  hipEvent_t stagger = nullptr;   // sfs2d_plan_run_streams: the first run's k_prep, awaited by the second stream
   std::string err;
   std::mutex err_mu;
 };
@@ -506,6 +507,7 @@ int sfs2d_ctx_destroy(sfs2d_ctx* ctx) {
   hipStreamSynchronize(CTX_STREAM(ctx));
   hipFree(ctx->d_lnx);
   hipFree(ctx->d_df);
+  if (ctx->stagger) hipEventDestroy(ctx->stagger);
   hipStreamDestroy(ctx->own);
   delete ctx;
   return 0;
@@ -1369,12 +1371,29 @@ int sfs2d_plan_run_streams(sfs2d_plan* const* plans, void* const* streams, sfs2d
   // enqueues: config 2 with 3 streams is not host-bound -- 10.7 us of enqueue per pass vs 14.5 us on
   // the GPU; a thread per stream gained 1.5% at 400 passes and lost its thread starts in 20-pass runs,
   // profiles/r02i_enqueue_probe.txt)
+  // The streams start staggered: the second stream's first run waits for the first run's k_prep, so
+  // that from the start one stream's bandwidth-bound k_prep runs beside the other's latency-bound scan
+  // (started together, the two k_preps competed and then the two scans, and the streams kept that
+  // phase: config 3's 20-step bench loop 0.184 vs 0.190-0.198 ms per pass, without Fst 0.165 vs 0.181;
+  // profiles/r05u_stream_stagger_ab.txt).  Not for plans with attached plans: their longer passes
+  // settled into a worse phase staggered (20 kb + 500 kb: 0.328-0.331 vs 0.285-0.286 ms per step)
+  bool stagger = nplans >= 2 && nruns >= 2;
+  for (int k = 0; k < nplans; ++k) stagger = stagger && plans[k]->attached.empty();
+  if (stagger && !ctx->stagger) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->stagger, hipEventDisableTiming));
   hipStream_t saved = CTX_STREAM(ctx);
   int rc = 0;
   for (int i = 0; i < nruns && !rc; ++i) {
     const int k = i % nplans;
     ctx->stream = (hipStream_t)streams[k];   // (NULL: the null stream, as sfs2d_ctx_set_stream)
-    rc = sfs2d_plan_run_phase(plans[k], 0, outs ? outs[k] : nullptr);
+    if (stagger && i == 0) {
+      rc = sfs2d_plan_run_phase(plans[k], 1, outs ? outs[k] : nullptr);
+      if (!rc && hipEventRecord(ctx->stagger, ctx->stream) != hipSuccess) rc = set_err(ctx, SFS2D_E_HIP, "stagger event");
+      if (!rc) rc = sfs2d_plan_run_phase(plans[k], 2, outs ? outs[k] : nullptr);
+      continue;
+    }
+    if (stagger && i == 1 && hipStreamWaitEvent(ctx->stream, ctx->stagger, 0) != hipSuccess)
+      rc = set_err(ctx, SFS2D_E_HIP, "stagger wait");
+    if (!rc) rc = sfs2d_plan_run_phase(plans[k], 0, outs ? outs[k] : nullptr);
   }
   ctx->stream = saved;
   return rc;

@@ -207,12 +207,11 @@ def test_plan_replay_is_deterministic():
     pl.close()
 
 
-@pytest.mark.parametrize("fst,threads", [(False, "0"), (True, "0"), (True, "1")])
-def test_run_streams_overlapped_plans(monkeypatch, fst, threads):
-    """sfs2d_plan_run_streams: passes round-robin over plans on their own HIP streams (overlapping;
-    enqueued by one host thread or, SFS2D_ENQ_THREADS=1, one per stream) write the same records and
-    Fst as one plan run alone; argument errors are reported."""
-    monkeypatch.setenv("SFS2D_ENQ_THREADS", threads)
+@pytest.mark.parametrize("fst,nplans", [(False, 3), (True, 3), (True, 2)])
+def test_run_streams_overlapped_plans(fst, nplans):
+    """sfs2d_plan_run_streams: passes round-robin over plans on their own HIP streams (overlapping; the
+    second stream's first pass waits for the first pass's k_prep) write the same records and Fst as one
+    plan run alone; argument errors are reported."""
     import torch
     from sfs2d import _lib as L
     from sfs2d.engine import Engine, Plan, ScanConfig
@@ -226,10 +225,10 @@ def test_run_streams_overlapped_plans(monkeypatch, fst, threads):
     ref.check()
     want = ref.read()
     want_f = ref.read_fst() if fst else None
-    plans = [eng.plan(dev, cfg) for _ in range(3)]
-    streams = [torch.cuda.Stream(device=0).cuda_stream for _ in range(3)]
-    outs = [torch.zeros((plans[0].nrec, 64), dtype=torch.uint8, device="cuda:0") for _ in range(3)]
-    Plan.run_streams(plans, streams, 3 * 5 + 1, [o.data_ptr() for o in outs])
+    plans = [eng.plan(dev, cfg) for _ in range(nplans)]
+    streams = [torch.cuda.Stream(device=0).cuda_stream for _ in range(nplans)]
+    outs = [torch.zeros((plans[0].nrec, 64), dtype=torch.uint8, device="cuda:0") for _ in range(nplans)]
+    Plan.run_streams(plans, streams, nplans * 5 + 1, [o.data_ptr() for o in outs])
     torch.cuda.synchronize()
     for k, q in enumerate(plans):
         q.check()
