@@ -279,9 +279,9 @@ void launch_scan_g(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
                      pl->ctx->d_lnx, out, bp, pl->d_fsum, pl->d_fst);
 }
 
-template <bool P16, bool FST, bool CNT>
+template <bool P16, bool FST, bool CNT, bool TRI = false>
 void launch_scan_gw(sfs2d_plan* pl, sfs2d_window* out, int per_chrom, int bp) {
-  hipExtLaunchKernelGGL((k_scan_gw<P16, FST, CNT>), dim3((unsigned)pl->chunks.size()), dim3(WAVE), pl->scan_lds,
+  hipExtLaunchKernelGGL((k_scan_gw<P16, FST, CNT, TRI>), dim3((unsigned)pl->chunks.size()), dim3(WAVE), pl->scan_lds,
                      CTX_STREAM(pl->ctx), pl->kev[4], pl->kev[5], 0, pl->K, scan_src(pl), pl->d_chunks, pl->d_slots, pl->d_tab, pl->d_lp, pl->d_head,
                      per_chrom, pl->ctx->d_lnx, pl->ctx->d_df, out, pl->d_err, bp, pl->d_repl, pl->d_bcount,
                      0, pl->d_leaves, pl->nleaves, pl->d_nodes, pl->nnodes, pl->nlevels, -1, pl->d_fsum, pl->d_fst,
@@ -293,8 +293,14 @@ hipError_t launch_scan_c(sfs2d_plan* pl, sfs2d_window* out) {
   const int per_chrom = pl->prm.bg_mode == SFS2D_BG_PER_CHROM ? 1 : 0;
   const int bp = pl->prm.window_mode == SFS2D_WINDOW_BP ? 1 : 0;
   if (pl->gw) {
-    if (pl->fst) launch_scan_gw<P16, true, CNT>(pl, out, per_chrom, bp);
-    else launch_scan_gw<P16, false, CNT>(pl, out, per_chrom, bp);
+    if (CNT && pl->K.ntri) {
+      if (pl->fst) launch_scan_gw<P16, true, CNT, CNT>(pl, out, per_chrom, bp);
+      else launch_scan_gw<P16, false, CNT, CNT>(pl, out, per_chrom, bp);
+    } else if (pl->fst) {
+      launch_scan_gw<P16, true, CNT>(pl, out, per_chrom, bp);
+    } else {
+      launch_scan_gw<P16, false, CNT>(pl, out, per_chrom, bp);
+    }
   } else if (pl->G == WAVE) {
     if constexpr (CNT) {
       if (pl->fst_scan) {
@@ -744,6 +750,7 @@ int sfs2d_data_free(sfs2d_data* d) {
 }
 
 static int make_kparams(sfs2d_ctx* ctx, const sfs2d_params* prm, int nchrom, KParams* K) {
+  *K = KParams{};   // (every field defined: e.g. ntri stays 0 unless a plan takes k_scan_gw's triangle)
   if (!prm) return set_err(ctx, SFS2D_E_ARG, "params is NULL");
   if (prm->n1p < 1 || prm->n2p < 1 || 2 * prm->n1p > 255 || 2 * prm->n2p > 255)
     return set_err(ctx, SFS2D_E_ARG, "pop sizes must satisfy 1 <= pop_size and 2*pop_size <= 255 (u8 counts)");
@@ -909,7 +916,11 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
       // k_scan_gw (a wavefront per window, tables from L2) when its one-wave workgroups, whose LDS
       // holds only the wave's histograms, still leave >= 2 wavefronts per CU (101 x 101: 7);
       // otherwise k_scan_g (a workgroup per window).  SFS2D_GW=0/1 forces one.
-      const int h2w = ((K.nb2 + 3) / 4 + 3) & ~3;   // u8-packed 2D bins
+      // u8-packed 2D bins; counts plans with folded square grids keep only the reachable triangle
+      // (k_scan_gw TRI: x1 + x2 <= n; 101 x 101: 5,151 of 10,201 bins -- half the LDS per wave)
+      if (pl->cnt && prm->fold && K.n1 == K.n2 && !(std::getenv("SFS2D_TRI") && std::getenv("SFS2D_TRI")[0] == '0'))
+        K.ntri = pl->K.ntri = (K.n1 + 1) * (K.n1 + 2) / 2;
+      const int h2w = (((K.ntri ? K.ntri : K.nb2) + 3) / 4 + 3) & ~3;
       size_t gw_lds = (size_t)(h2w + R1GW * (K.n1p + 1) + R1GW * (K.n2p + 1) + TRASH) * 4;
       int occ = 0;
       if (gw_lds <= 160 * 1024) {
@@ -918,10 +929,15 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
           for (const void* f : {(const void*)k_scan_gw<true, false, false>, (const void*)k_scan_gw<false, false, false>,
                                 (const void*)k_scan_gw<true, true, false>, (const void*)k_scan_gw<false, true, false>,
                                 (const void*)k_scan_gw<true, false, true>, (const void*)k_scan_gw<false, false, true>,
-                                (const void*)k_scan_gw<true, true, true>, (const void*)k_scan_gw<false, true, true>})
+                                (const void*)k_scan_gw<true, true, true>, (const void*)k_scan_gw<false, true, true>,
+                                (const void*)k_scan_gw<true, false, true, true>, (const void*)k_scan_gw<false, false, true, true>,
+                                (const void*)k_scan_gw<true, true, true, true>, (const void*)k_scan_gw<false, true, true, true>})
             hipFuncSetAttribute(f, A, (int)gw_lds);
-        const hipError_t oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<true, true, true>, WAVE, gw_lds)
-                                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<false, true, true>, WAVE, gw_lds);
+        const hipError_t oe =
+            K.ntri ? (pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<true, true, true, true>, WAVE, gw_lds)
+                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<false, true, true, true>, WAVE, gw_lds))
+                   : (pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<true, true, true>, WAVE, gw_lds)
+                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<false, true, true>, WAVE, gw_lds));
         if (oe != hipSuccess) occ = 0;
         pl->gw = occ >= 2;   // measured on 201 x 151 with u16 bins (2 per CU): 22 vs 32 us for k_scan_g
         if (const char* ev = std::getenv("SFS2D_GW")) pl->gw = occ >= 1 && ev[0] == '1';
@@ -1009,7 +1025,10 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
     int occ = 0;
     // (the grid is one dispatch wave of resident workgroups: occupancy of the variant that runs)
     hipError_t oe;
-    if (pl->gw)
+    if (pl->gw && K.ntri)
+      oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<true, true, true, true>, WAVE, pl->scan_lds)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<false, true, true, true>, WAVE, pl->scan_lds);
+    else if (pl->gw)
       oe = pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<true, true, true>, WAVE, pl->scan_lds)
                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<false, true, true>, WAVE, pl->scan_lds);
     else if (pl->fst_scan && pl->fused)

@@ -135,6 +135,8 @@ struct KParams {
   uint32_t n12, lim12;   // u16 pairs (n1, n2), (n1p-1, n2p-1): both folded 1D bins in packed 16-bit ops
   int rtn;               // Fst's (1/n, 1/(n(n-1))) entries in LDS (k_scan_w): n up to the data's
                          // largest called count (even; >= wl_rtn(n1p, n2p))
+  int ntri;              // k_scan_gw TRI (folded counts plans, n1 = n2 = n): the reachable 2D bins
+                         // x1 + x2 <= n, (n+1)(n+2)/2 of them, stored as a triangle (0: full grid)
 };
 
 struct Tile {   // k_prep work item: SNPs [begin, end) of chromosome chrom = [cb, ce), slots from sbase
@@ -454,11 +456,16 @@ __device__ __forceinline__ uint32_t cls_word(const KParams& P, uint32_t c) {
 // range test: 7 operations for the two populations)
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
-__device__ __forceinline__ void cls_fields(const KParams& P, uint32_t c, uint32_t& k2, uint32_t& g1, uint32_t& g2) {
+__device__ __forceinline__ void cls_fields(const KParams& P, uint32_t c, uint32_t& k2, uint32_t& g1, uint32_t& g2,
+                                           uint32_t* ktri = nullptr) {
   const bool sw = (int)__builtin_amdgcn_udot4(c, 0x01000100u, 0u, false) > P.fold_thr;
   const uint32_t x = sw ? c : (c >> 8);
   const uint32_t kk = __builtin_amdgcn_udot4(x, P.kmul, 0u, false);
   k2 = kk < (uint32_t)P.nb2 - 1u ? kk : 0u;
+  if (ktri) {   // (k_scan_gw TRI) the triangle index, clamped into it (counts outside the grid are an error)
+    const uint32_t x1 = x & 0xffu;
+    *ktri = min(kk - ((x1 * (x1 - 1u)) >> 1), (uint32_t)P.ntri - 1u);
+  }
   const u16x2 a = as_u16x2(__builtin_amdgcn_perm(0u, c, 0x0c030c01u));      // (a1, a2)
   const u16x2 g = __builtin_elementwise_min(a, as_u16x2(P.n12) - a);         // min(a, n - a)
   // 1 <= g <= n_p - 1 <=> lim - (g - 1) > 0 (saturating); keep g there, 0 elsewhere
@@ -1861,7 +1868,12 @@ __device__ __forceinline__ void fused_table(int nb2, int nh, int nt, int n1p, in
 
 __device__ __forceinline__ void wave_sum3(double a, double b, double c, double& sa, double& sb, double& sc);
 
-template <bool P16, bool FST, bool CNT>
+// TRI (counts plans, folded, n1 = n2 = n): the wave's u8 2D histogram holds only the bins a folded key
+// can reach, x1 + x2 <= n (the fold swaps to the reference alleles when a1 + a2 > n, and r1 + r2 <=
+// 2n - (a1 + a2) then), as a triangle: bin (x1, x2) at x1 (n + 1) - x1 (x1 - 1) / 2 + x2 = k2 -
+// x1 (x1 - 1) / 2.  101 x 101: 5.2 instead of 10.2 KB per wave.  The tables (lp, the exact path's
+// global histogram) keep the full index k2.
+template <bool P16, bool FST, bool CNT, bool TRI = false>
 __device__ __forceinline__ void scan_gw_body(double* ldsd, SCAN_W_ARGS) {
   STAMP(10);
   BLK_STAMP(1, 0);
@@ -1875,7 +1887,8 @@ __device__ __forceinline__ void scan_gw_body(double* ldsd, SCAN_W_ARGS) {
   const double* LPl = LPg + (size_t)bg * P.nt;
   const double* Dt = dfg;       // LNT
   const double* Ft = Dt + LNT;  // LNT
-  const int h2w = ((P.nb2 + 3) / 4 + 3) & ~3;
+  static_assert(!TRI || CNT, "the triangle index needs the counts (x1)");
+  const int h2w = (((TRI ? P.ntri : P.nb2) + 3) / 4 + 3) & ~3;
   constexpr int RG = R1GW;   // 1D replicas
   const int h1w = RG * (P.n1p + 1), h1wb = RG * (P.n2p + 1);
   const int per = h2w + h1w + h1wb + TRASH;
@@ -2010,9 +2023,10 @@ __device__ __forceinline__ void scan_gw_body(double* ldsd, SCAN_W_ARGS) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const uint32_t w = ww[q];
-        uint32_t k2, g1, g2;
-        if (CNT) cls_fields(P, w, k2, g1, g2);
+        uint32_t k2, g1, g2, kh;   // kh: the bin's index in the LDS histogram
+        if (CNT) cls_fields(P, w, k2, g1, g2, TRI ? &kh : nullptr);
         else { k2 = bin_k2(w); g1 = bin_g1(w); g2 = bin_g2(w); }
+        if (!TRI) kh = k2;
         n2 += 64u - (uint32_t)__popcll(__ballot(k2 == 0u));   // (the compare the selects below use)
         n1a += __popcll(__ballot(g1 != 0u));
         n1b += __popcll(__ballot(g2 != 0u));
@@ -2020,10 +2034,10 @@ __device__ __forceinline__ void scan_gw_body(double* ldsd, SCAN_W_ARGS) {
         // an address select here, not a select of the loaded value in finish(), which the scheduler
         // hoisted next to the load and so waited for the gather on the spot)
         st.lp[q] = *(k2 ? LPl + k2 : Dt + (LNT - 1));
-        const uint32_t word = k2 ? (k2 >> 2) : trash;   // (u8 bins: four to a word)
-        // the byte's shift: the hardware reads shift operands' low five bits, so k2 << 3 serves
+        const uint32_t word = k2 ? (kh >> 2) : trash;   // (u8 bins: four to a word)
+        // the byte's shift: the hardware reads shift operands' low five bits, so kh << 3 serves
         // without a mask (the bins word's low bits are k2's)
-        const uint32_t wk = CNT ? k2 : w;
+        const uint32_t wk = CNT ? kh : w;
         const uint32_t sh = wk << 3;
         uint32_t one2 = 1u;
         asm("v_lshlrev_b32 %0, %1, 1" : "=v"(one2) : "v"(sh));
@@ -3032,10 +3046,10 @@ __global__ __launch_bounds__(SBLOCK) __attribute__((amdgpu_waves_per_eu(4))) voi
 }
 
 // K3 for large grids, one wavefront per window (LDS: the wave's histograms only)
-template <bool P16, bool FST, bool CNT>
+template <bool P16, bool FST, bool CNT, bool TRI = false>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(4))) void k_scan_gw(SCAN_W_ARGS) {
   extern __shared__ double ldsd[];
-  scan_gw_body<P16, FST, CNT>(ldsd, SCAN_W_PASS);
+  scan_gw_body<P16, FST, CNT, TRI>(ldsd, SCAN_W_PASS);
 }
 
 // K3 for large grids: one workgroup per window, exact evaluation.
