@@ -475,7 +475,9 @@ hipError_t launch_attached(sfs2d_plan* a) {
 
 extern "C" {
 
-int sfs2d_abi_version(void) { return SFS2D_ABI_VERSION; }
+// an ablation build (-DSFS2D_ABL=..., timing only, wrong results) reports a negative version, which the
+// loaders refuse (sfs2d/_lib.py) unless SFS2D_ALLOW_ABLATION=1 is set by the timing tool
+int sfs2d_abi_version(void) { return SFS2D_ABL ? -SFS2D_ABL : SFS2D_ABI_VERSION; }
 
 const char* sfs2d_last_error(const sfs2d_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
@@ -524,6 +526,12 @@ int sfs2d_ctx_destroy(sfs2d_ctx* ctx) {
 int sfs2d_ctx_set_stream(sfs2d_ctx* ctx, void* stream) {
   if (!ctx) return SFS2D_E_ARG;
   ctx->stream = (hipStream_t)stream;
+  return 0;
+}
+
+int sfs2d_ctx_get_stream(const sfs2d_ctx* ctx, void** stream) {
+  if (!ctx || !stream) return SFS2D_E_ARG;
+  *stream = (void*)ctx->stream;
   return 0;
 }
 
@@ -817,10 +825,8 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   }
   pl->nslots = (int64_t)slot_base[nc];
   pl->slot_base_h = slot_base;
-  // counts plan: no filter (the scan kernels classify counts without positions / annotations);
-  // SFS2D_CNT=0 forces the bins pipeline (comparison)
+  // counts plan: no filter (the scan kernels classify counts without positions / annotations)
   pl->cnt = prm->ann_want < 0 && !prm->has_start && !prm->has_end;
-  if (const char* ev = std::getenv("SFS2D_CNT")) pl->cnt = pl->cnt && ev[0] != '0';
   // a supplied background: no k_prep pass reads (and validates) the counts of a counts plan, so one is
   // taken only when no SNP can raise an error (max_nc1 / max_nc2); else the bins pipeline's k_prep
   // classifies every SNP and reports KeyError / out-of-grid keys as the reference raises them
@@ -917,8 +923,12 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
       // holds only the wave's histograms, still leave >= 2 wavefronts per CU (101 x 101: 7);
       // otherwise k_scan_g (a workgroup per window).  SFS2D_GW=0/1 forces one.
       // u8-packed 2D bins; counts plans with folded square grids keep only the reachable triangle
-      // (k_scan_gw TRI: x1 + x2 <= n; 101 x 101: 5,151 of 10,201 bins -- half the LDS per wave)
-      if (pl->cnt && prm->fold && K.n1 == K.n2 && !(std::getenv("SFS2D_TRI") && std::getenv("SFS2D_TRI")[0] == '0'))
+      // (k_scan_gw TRI: x1 + x2 <= n; 101 x 101: 5,151 of 10,201 bins -- half the LDS per wave).
+      // x1 + x2 <= n holds only when every SNP's called counts r + a are <= 2 pop_size (then a folded
+      // key has r1 + r2 <= 2n - (a1 + a2) < n); the reference counts any in-grid key
+      // (twoDSFS_class.py:198-217), so data with a larger called count (max_nc1 / max_nc2, known at
+      // upload) keep the full k2-indexed grid
+      if (pl->cnt && prm->fold && K.n1 == K.n2 && data->max_nc1 <= (uint32_t)K.n1 && data->max_nc2 <= (uint32_t)K.n2)
         K.ntri = pl->K.ntri = (K.n1 + 1) * (K.n1 + 2) / 2;
       const int h2w = (((K.ntri ? K.ntri : K.nb2) + 3) / 4 + 3) & ~3;
       size_t gw_lds = (size_t)(h2w + R1GW * (K.n1p + 1) + R1GW * (K.n2p + 1) + TRASH) * 4;

@@ -41,7 +41,9 @@ EXPORTS = [
     "sfs2d_plan_destroy", "sfs2d_scan", "sfs2d_plan_set_timing", "sfs2d_plan_timing_read",
     "sfs2d_plan_stats", "sfs2d_plan_grids", "sfs2d_plan_scan_kernel", "sfs2d_plan_attach", "sfs2d_data_synth_sims",
     "sfs2d_data_read", "sfs2d_plan_run_streams", "sfs2d_ctx_use_own_stream", "sfs2d_bg_hist_dev", "sfs2d_plan_bg_rows_dev", "sfs2d_plan_bg_rows_set_dev",
+    "sfs2d_ctx_get_stream",
 ]
+ABI_VERSION = 2   # SFS2D_ABI_VERSION of include/sfs2d.h
 
 
 class Sfs2dError(RuntimeError):
@@ -92,6 +94,10 @@ def lib():
     L = C.CDLL(os.path.abspath(LIB_PATH))
     vp, i32, i64, u32p = C.c_void_p, C.c_int32, C.c_int64, C.POINTER(C.c_uint32)
     L.sfs2d_abi_version.restype = C.c_int
+    v = L.sfs2d_abi_version()
+    if v != ABI_VERSION and not (v < 0 and os.environ.get("SFS2D_ALLOW_ABLATION") == "1"):
+        raise Sfs2dError(E_ARG, f"{os.path.abspath(LIB_PATH)}: ABI version {v}, expected {ABI_VERSION}"
+                                + (" (an ablation build: timing only, wrong results)" if v < 0 else ""))
     L.sfs2d_ctx_create.argtypes = [C.c_int, C.POINTER(vp)]
     L.sfs2d_ctx_destroy.argtypes = [vp]
     L.sfs2d_last_error.argtypes = [vp]
@@ -132,6 +138,7 @@ def lib():
     L.sfs2d_data_synth_sims.argtypes = [vp, C.POINTER(SynthParams), vp, vp, i32, vp, i32, C.POINTER(vp)]
     L.sfs2d_data_read.argtypes = [vp, vp, vp, i64]
     L.sfs2d_ctx_use_own_stream.argtypes = [vp]
+    L.sfs2d_ctx_get_stream.argtypes = [vp, C.POINTER(vp)]
     L.sfs2d_plan_timing_read.argtypes = [vp, C.POINTER(C.c_int)] + [C.POINTER(C.c_double)] * 3
     L.sfs2d_scan.argtypes = [vp, vp, C.POINTER(Params), vp, vp, vp, vp, i64, C.POINTER(i64)]
     _lib = L

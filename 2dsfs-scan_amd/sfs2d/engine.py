@@ -88,6 +88,13 @@ class Engine:
         self.stream = stream_handle
         return prev
 
+    def stream_handle(self) -> int:
+        """The HIP stream handle the library currently enqueues on (sfs2d_ctx_get_stream): the ctx's own
+        stream after construction or ``set_stream(None)``, 0 for the null stream."""
+        s = C.c_void_p()
+        self.check(self.lib.sfs2d_ctx_get_stream(self.h, C.byref(s)))
+        return int(s.value or 0)
+
     def upload(self, p: PackedSNPs) -> "DeviceData":
         return DeviceData(self, p)
 
@@ -228,13 +235,16 @@ class Plan:
     @staticmethod
     def run_streams(plans, streams, nruns: int, out_dev_ptrs=None):
         """Enqueue `nruns` runs round-robin over distinct plans of one engine, run i on
-        streams[i % len(plans)] (HIP stream handles; 0/None = the engine's stream)
-        (sfs2d_plan_run_streams: independent scans overlap across the streams)."""
+        streams[i % len(plans)] (sfs2d_plan_run_streams: independent scans overlap across the streams).
+        Entries are HIP stream handles, 0 = the HIP null stream (as in Engine.set_stream); None = the
+        stream the engine currently enqueues on (Engine.stream_handle), so that ``read()`` / ``check()``,
+        which synchronise that stream, see those runs finished."""
         k = len(plans)
-        ph = (C.c_void_p * k)(*[p.h.value for p in plans])
-        sh = (C.c_void_p * k)(*[s or None for s in streams])
-        oh = (C.c_void_p * k)(*[o or None for o in out_dev_ptrs]) if out_dev_ptrs else None
         eng = plans[0].eng
+        cur = eng.stream_handle() if any(s is None for s in streams) else 0
+        ph = (C.c_void_p * k)(*[p.h.value for p in plans])
+        sh = (C.c_void_p * k)(*[(cur if s is None else int(s)) or None for s in streams])
+        oh = (C.c_void_p * k)(*[o or None for o in out_dev_ptrs]) if out_dev_ptrs else None
         eng.check(eng.lib.sfs2d_plan_run_streams(ph, sh, oh, k, int(nruns)))
 
     def check(self):

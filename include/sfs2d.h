@@ -34,7 +34,9 @@
 extern "C" {
 #endif
 
-#define SFS2D_ABI_VERSION 1
+/* 2 (round 5-6): sfs2d_ctx_set_stream(ctx, NULL) selects the HIP null stream (1: the ctx's own),
+ * sfs2d_ctx_use_own_stream / sfs2d_ctx_get_stream added, the sfs2d_dist_* entry points removed */
+#define SFS2D_ABI_VERSION 2
 
 /* status codes */
 #define SFS2D_OK 0
@@ -111,6 +113,12 @@ const char* sfs2d_last_error(const sfs2d_ctx* ctx);
  * (twoDSFS_class.py:21-33): one ctx per GPU, calls serialised by the caller. */
 int sfs2d_ctx_set_stream(sfs2d_ctx* ctx, void* hip_stream);
 int sfs2d_ctx_use_own_stream(sfs2d_ctx* ctx);
+/* the HIP stream the ctx currently enqueues on (NULL = the null stream; after sfs2d_ctx_create or
+ * sfs2d_ctx_use_own_stream, the handle of the ctx's own stream) -- e.g. to pass it to
+ * sfs2d_plan_run_streams or to order a caller's stream after the ctx's work */
+int sfs2d_ctx_get_stream(const sfs2d_ctx* ctx, void** hip_stream);
+/* SFS2D_ABI_VERSION of the loaded library (negative: an ablation build for timing experiments, whose
+ * results are wrong -- loaders must refuse it) */
 int sfs2d_abi_version(void);
 
 /* data set: packed SNPs in scan order (sorted by chromosome string, then position) */

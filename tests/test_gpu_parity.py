@@ -97,12 +97,12 @@ def test_bg_hist_bitexact_chr1(golden):
     assert np.array_equal(T._fold_counts(u2), g["bg1b"])
 
 
-def _records_vs_oracle(p, cfg_scan, ocfg, wins, bg_of, guards=True):
+def _records_vs_oracle(p, cfg_scan, ocfg, wins, bg_of, guards=True, bg=None):
     from sfs2d import _lib as L
     from sfs2d.engine import Engine
     eng = Engine.get(0)
     dev = eng.upload(p)
-    recs = eng.scan(dev, cfg_scan)
+    recs = eng.scan(dev, cfg_scan, bg=bg)
     body = recs[(recs["flags"] & (L.W_EMPTY | L.W_EXTRA)) == 0]
     ref = O.window_records(p, wins, ocfg, bg_of, guards)
     assert len(body) == len(ref)
@@ -238,6 +238,38 @@ def test_run_streams_overlapped_plans(fst, nplans):
             assert np.array_equal(q.read_fst(), want_f, equal_nan=True), k
     with pytest.raises(L.Sfs2dError):
         Plan.run_streams([plans[0], plans[0]], streams[:2], 2)
+    for q in plans + [ref]:
+        q.close()
+    dev.close()
+
+
+def test_run_streams_none_is_the_engine_stream():
+    """Plan.run_streams with None entries enqueues on the engine's current stream (its own stream by
+    default, sfs2d_ctx_get_stream), so read() -- which synchronises that stream only -- returns the
+    finished runs' records without any other synchronisation; 0 is the HIP null stream."""
+    from sfs2d.engine import Engine, Plan, ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(2, [300000, 200000], 25, 25, seed=99)
+    eng = Engine.get(0)
+    assert eng.stream_handle() != 0   # the ctx's own non-blocking stream
+    dev = eng.upload(p)
+    cfg = ScanConfig(n1p=25, n2p=25, window=20000, fst=True)
+    ref = eng.plan(dev, cfg)
+    ref.run()
+    want = ref.read()
+    plans = [eng.plan(dev, cfg) for _ in range(2)]
+    Plan.run_streams(plans, [None, None], 6)
+    for q in plans:
+        assert q.read().tobytes() == want.tobytes()
+        q.check()
+    prev = eng.set_stream(0)
+    try:
+        assert eng.stream_handle() == 0
+        Plan.run_streams(plans, [None, 0], 4)
+        for q in plans:
+            assert q.read().tobytes() == want.tobytes()
+    finally:
+        eng.set_stream(prev)
     for q in plans + [ref]:
         q.close()
     dev.close()
@@ -587,6 +619,87 @@ def test_called_counts_above_sample_size_inside_long_tiles():
     pl.close()
 
 
+def _overcall(p, n1p, n2p, frac, seed):
+    """Copy of p with a fraction of SNPs made over-called in both populations: called counts r + a above
+    2 pop_size with a1 + a2 > n1p + n2p (a joint fold) and r1 + r2 > n (a folded key outside the triangle
+    x1 + x2 <= n); e.g. (60, 50, 45, 55) at pop 50/50.  Every alt count stays <= 2 pop_size (no KeyError)
+    and every folded key inside the grid."""
+    from sfs2d.pack import PackedSNPs, pack_counts
+    n1, n2 = 2 * n1p, 2 * n2p
+    rng = np.random.default_rng(seed)
+    r1, a1 = (p.counts & 0xff).astype(np.int64), ((p.counts >> 8) & 0xff).astype(np.int64)
+    r2, a2 = ((p.counts >> 16) & 0xff).astype(np.int64), (p.counts >> 24).astype(np.int64)
+    pick = rng.random(p.n) < frac
+    m = int(pick.sum())
+    na1 = rng.integers(n1p, int(n1 * 0.7) + 1, m)          # a1 + a2 > n1p + n2p: the fold swaps
+    na2 = rng.integers(n2p + 1, int(n2 * 0.7) + 1, m)
+    nr1 = rng.integers(n1p + 1, n1 + 1, m)                 # r1 + r2 > n: outside the triangle
+    nr2 = rng.integers(n2p - 4, n2 + 1, m)
+    r1[pick], a1[pick], r2[pick], a2[pick] = nr1, na1, nr2, na2
+    assert np.all(r1 <= 255) and np.all(r2 <= 255)
+    q = PackedSNPs(pack_counts(r1, a1, r2, a2), p.pos, p.chrom_off, p.chrom_names, p.ann_id, p.ann_names)
+    sel = pick & (a1 + a2 > n1p + n2p)
+    assert np.any(sel & (r1 + r2 > n1)) and np.all(r1[sel] <= n1) and np.all(r2[sel] <= n2)
+    return q
+
+
+@pytest.mark.parametrize("n1p,n2p", [(50, 50), (100, 75)])
+@pytest.mark.parametrize("fst", [False, True])
+def test_large_grid_overcalled_snps_per_chrom(n1p, n2p, fst):
+    """k_scan_gw's triangle histogram (folded square counts plans) is only exact
+    while every called count is <= 2 pop_size; over-called SNPs (called count above 2 pop_size, folded
+    key with x1 + x2 > n, e.g. (60, 50, 45, 55) at 50/50) are counted by the reference at their in-grid
+    key (twoDSFS_class.py:198-217), so such data sets keep the full grid.  Per-chromosome backgrounds,
+    fixed-bp and SNP-count windows, against the oracle; 100 x 75 pins the non-square path.  A data set
+    without over-called SNPs still takes the triangle (k_scan_gw, LDS per wave halved)."""
+    from sfs2d import _lib as L
+    from sfs2d.engine import Engine, ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(4, [5000, 3100, 2200, 700], n1p, n2p, seed=515 + n1p)
+    q = _overcall(p, n1p, n2p, 0.03, seed=n1p)
+    ocfg = O.Cfg(n1p, n2p)
+    bgs = O.chrom_backgrounds(q, ocfg)
+    for mode, ws in ((L.WINDOW_BP, 30000), (L.WINDOW_SNPS, 120)):
+        wins = O.snp_windows(q, ws)[0] if mode == L.WINDOW_SNPS else O.bp_windows(q, ws)
+        _records_vs_oracle(q, ScanConfig(n1p=n1p, n2p=n2p, window_mode=mode, window=ws, fst=fst), ocfg, wins,
+                           lambda c: bgs[c])
+    eng = Engine.get(0)
+    for data in (q, p):
+        dev = eng.upload(data)
+        pl = eng.plan(dev, ScanConfig(n1p=n1p, n2p=n2p, window=30000, fst=fst))
+        assert pl.scan_kernel() == "k_scan_gw"
+        pl.run()
+        pl.check()
+        if fst:
+            recs, got = pl.read(), pl.read_fst()
+            live = (recs["flags"][: len(got)] & L.W_EMPTY) == 0
+            wins = O.bp_windows(data, 30000)
+            assert int(live.sum()) == len(wins)
+            for g, (c, st, b, e) in list(zip(got[live], wins))[::5]:
+                assert _fst_close(float(g), O.window_fst(data, np.arange(b, e), ocfg)), (g, b, e)
+        pl.close()
+        dev.close()
+
+
+@pytest.mark.parametrize("n1p", [50, 100])
+def test_overcalled_supplied_background_sims_shape(n1p):
+    """The same over-called SNPs under a supplied background (sims_scan / scan_chooseChr shape: square
+    folded grid, k_scan_gw): such data sets take the bins pipeline (k_prep validates every SNP), never the
+    triangle; records against the oracle with the background of the whole data set."""
+    from sfs2d import _lib as L
+    from sfs2d.engine import ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(3, [4000, 2500, 900], n1p, n1p, seed=77 + n1p)
+    q = _overcall(p, n1p, n1p, 0.02, seed=3 * n1p)
+    ocfg = O.Cfg(n1p, n1p)
+    idx = np.arange(q.n)
+    bg = (O.sfs2d(q, idx, ocfg), O.fold1d(O.sfs1d(q, idx, 1, ocfg)), O.fold1d(O.sfs1d(q, idx, 2, ocfg)))
+    for mode, ws in ((L.WINDOW_BP, 20000), (L.WINDOW_SNPS, 150)):
+        wins = O.snp_windows(q, ws)[0] if mode == L.WINDOW_SNPS else O.bp_windows(q, ws)
+        _records_vs_oracle(q, ScanConfig(n1p=n1p, n2p=n1p, window_mode=mode, window=ws, bg_mode=L.BG_SUPPLIED),
+                           ocfg, wins, lambda c: bg, bg=bg)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("ws,n1p,n2p", [(100000, 11, 11), (500000, 11, 11), (500000, 18, 14), (2000000, 25, 25)])
 def test_sparse_windows_all_present(ws, n1p, n2p):
@@ -618,10 +731,11 @@ def test_sparse_windows_all_present(ws, n1p, n2p):
     assert got == exp
 
 
-def test_wrapped_u8_bins_take_the_exact_path():
-    """k_scan_wl counts the 2D SFS in u8-packed bins: a window with >= 256 SNPs in one bin wraps a byte
-    (the atomic returns rank 255), and the window is re-evaluated exactly on a u32 histogram in global
-    memory.  Windows of 1,000 identical SNPs (one bin) among ordinary ones, against the oracle."""
+def test_many_snps_in_one_bin_small_grid():
+    """k_scan_w counts the 2D SFS in u16-packed bins and ranks each SNP in its bin by the atomic's return
+    value (D(r) from the LDS table for r < 512, the global ln table beyond): windows of 1,000 identical
+    SNPs (one bin, ranks past the LDS table) among ordinary ones, SNP-count and fixed-bp windows, against
+    the oracle.  (Round 4's k_scan_wl, which wrapped u8 bins here, was removed in round 5.)"""
     from sfs2d.engine import ScanConfig
     from sfs2d.pack import PackedSNPs
     from sfs2d.synth import synth_genome

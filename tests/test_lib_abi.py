@@ -32,7 +32,7 @@ def test_library_exports_every_symbol():
     lib = ctypes.CDLL(path)
     missing = [s for s in _declared() if not hasattr(lib, s)]
     assert not missing, missing
-    assert lib.sfs2d_abi_version() == 1
+    assert lib.sfs2d_abi_version() == 2
 
 
 def test_no_device_is_reported_not_faked():
