@@ -138,14 +138,16 @@ struct sfs2d_plan {
   KParams K{};
   int nbg = 0;
   bool do_bg = false, do_seg = false, lds_hist = true, bg_ready = false;
-  bool seg_synth = false;   // fixed-bp slots from the generator's window offsets (synth_seg)
+  bool seg_synth = false;   // fixed-bp slots from the generator's window offsets (slots_only)
+  bool seg_search = false;  // fixed-bp slots by binary search on the positions, k_slots_search (slots_only)
   bool fused = false;       // per-chromosome tables built inside k_scan_w (parity-alternating replicas)
   bool sliced = false;      // per-chromosome tables by k_bg_slice without its tail; k_scan_w combines
                             // the leaf sums (parity-alternating inner sums)
   bool cnt = false;         // counts plan (no position / variant_type filter): k_prep writes no per-SNP bins,
                             // the scan kernels classify the counts themselves (12 B/SNP per pass instead of 20)
   bool fst = false;         // SFS2D_F_FST: Fst per slot into d_fst
-  double* d_fst = nullptr;
+  double* d_fst = nullptr;      // where runs write Fst: d_fst_own, or the caller's (sfs2d_plan_set_fst_out)
+  double* d_fst_own = nullptr;
   unsigned long long* d_fsum = nullptr;   // k_prep's per-slot Fst sums (int64 fixed point), cleared by the scan
   int hr = 1;               // k_prep LDS histogram copies per word
   uint64_t runs = 0;        // completed runs (the replica parity of a fused plan)
@@ -247,7 +249,7 @@ void plan_free(sfs2d_plan* p) {
   hipFree(p->d_tiles); hipFree(p->d_chunks); hipFree(p->d_slots); hipFree(p->d_repl); hipFree(p->d_bcount); hipFree(p->d_ctr);
   hipFree(p->d_done); hipFree(p->d_bgval); hipFree(p->d_tab); hipFree(p->d_lp); hipFree(p->d_head);
   hipFree(p->d_bg1d); hipFree(p->d_leafsum); hipFree(p->d_leaves); hipFree(p->d_nodes); hipFree(p->d_slices);
-  hipFree(p->d_out); hipFree(p->d_err); hipFree(p->d_bins); hipFree(p->d_fst); hipFree(p->d_fsum); hipFree(p->d_gscr);
+  hipFree(p->d_out); hipFree(p->d_err); hipFree(p->d_bins); hipFree(p->d_fst_own); hipFree(p->d_fsum); hipFree(p->d_gscr);
   for (auto& e : p->ev) if (e) hipEventDestroy(e);
   for (auto& e : p->tev) if (e) hipEventDestroy(e);
 }
@@ -371,18 +373,23 @@ hipError_t launch_prep_cnt(sfs2d_plan* pl) {
   return hipSuccess;
 }
 
-// whether a run takes its slot table from the generator's window offsets instead of k_prep (see
-// seg_synth; k_prep's Fst sums or an attached plan's use of its pass keep k_prep)
-bool synth_seg(const sfs2d_plan* pl) {
-  return pl->seg_synth && pl->attached.empty() && !(pl->fst && !pl->fst_win && !pl->fst_scan);
+// whether a run takes its slot table from the generator's window offsets or a binary search on the
+// positions instead of k_prep (seg_synth / seg_search; k_prep's Fst sums or an attached plan's use of its
+// pass keep k_prep)
+bool slots_only(const sfs2d_plan* pl) {
+  return (pl->seg_synth || pl->seg_search) && pl->attached.empty() && !(pl->fst && !pl->fst_win && !pl->fst_scan);
 }
 
-hipError_t launch_slots_synth(sfs2d_plan* pl) {
+hipError_t launch_slots_only(sfs2d_plan* pl) {
   const unsigned long long nw = (unsigned long long)pl->nslots;
-  const unsigned grid = (unsigned)std::min<unsigned long long>(8192, (nw + 255) / 256);
-  if (nw)   // (the k_prep timing slot: this is the run's segmentation stage)
-    hipExtLaunchKernelGGL(k_slots_synth, dim3(grid), dim3(256), 0, CTX_STREAM(pl->ctx), pl->kev[0], pl->kev[1], 0,
-                          pl->data->d_win_off, nw, pl->d_slots);
+  // (the k_prep timing slot: this is the run's segmentation stage)
+  if (nw && pl->seg_synth)
+    hipExtLaunchKernelGGL(k_slots_synth, dim3((unsigned)std::min<unsigned long long>(8192, (nw + 255) / 256)), dim3(256),
+                          0, CTX_STREAM(pl->ctx), pl->kev[0], pl->kev[1], 0, pl->data->d_win_off, nw, pl->d_slots);
+  else if (nw)
+    hipExtLaunchKernelGGL(k_slots_search, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, CTX_STREAM(pl->ctx),
+                          pl->kev[0], pl->kev[1], 0, pl->data->pos, pl->data->d_chrom_off, pl->d_slot_base,
+                          pl->data->nchrom, (uint32_t)pl->prm.window, (uint32_t)nw, pl->d_slots);
   return hipGetLastError();
 }
 
@@ -837,14 +844,20 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   // replicate c is the generator's window c * win_per_chrom + w, whose SNPs it placed in that window
   // ((pos - 1) / ws == w), so the slot table is the window offsets (k_slots_synth) -- when every
   // replicate holds SNPs (the slot numbering skips empty chromosomes) and the plan has no other k_prep
-  // work (a counts plan with a supplied background; see synth_seg).  SFS2D_SYNTH_SEG=0: k_prep instead.
+  // work (a counts plan with a supplied background; see slots_only).
+  // Any other fixed-bp counts plan with a supplied background (no k_prep histograms) takes its slots by
+  // binary search on the resident positions (k_slots_search) instead of k_prep's segmentation pass.
+  // SFS2D_SEG=prep forces k_prep's segmentation, SFS2D_SEG=search the search (never the generator's
+  // offsets: what a real replicate VCF gets); both are selected by tests/test_synth_device.py
+  const char* seg_ev = std::getenv("SFS2D_SEG");
+  const bool seg_prep = seg_ev && std::strcmp(seg_ev, "prep") == 0, seg_srch = seg_ev && std::strcmp(seg_ev, "search") == 0;
   if (bp && data->d_win_off && (uint32_t)prm->window == data->win_bp && pl->cnt && !pl->do_bg &&
       pl->nslots == (int64_t)nc * (int64_t)data->win_per_chrom) {
     bool all = true;
     for (int c = 0; c < nc && all; ++c) all = data->chrom_off[c + 1] > data->chrom_off[c];
-    const char* ev = std::getenv("SFS2D_SYNTH_SEG");
-    pl->seg_synth = all && !(ev && ev[0] == '0');
+    pl->seg_synth = all && !seg_prep && !seg_srch;
   }
+  pl->seg_search = bp && pl->cnt && !pl->do_bg && !pl->seg_synth && !seg_prep;
   pl->K.nm1 = data->n > 0 ? (uint32_t)(data->n - 1) : 0u;
   pl->K.kmul = (uint32_t)(pl->K.n2 + 1) | (1u << 16);
   pl->K.n12 = (uint32_t)pl->K.n1 | ((uint32_t)pl->K.n2 << 16);
@@ -1215,6 +1228,13 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   rc = rc ? rc : dalloc(ctx, &pl->d_out, (size_t)pl->nrec);
   rc = rc ? rc : dalloc(ctx, &pl->d_err, 4);
   if (pl->fst) rc = rc ? rc : dalloc(ctx, &pl->d_fst, (size_t)pl->nslots + 1);
+  pl->d_fst_own = pl->d_fst;
+  if (pl->seg_search && !rc) {   // k_slots_search's slot bases per chromosome (u32: nslots < 2^31)
+    std::vector<uint32_t> sb(pl->slot_base_h.begin(), pl->slot_base_h.end());
+    rc = dalloc(ctx, &pl->d_slot_base, sb.size());
+    if (!rc && hipMemcpy(pl->d_slot_base, sb.data(), sizeof(uint32_t) * sb.size(), hipMemcpyHostToDevice) != hipSuccess)
+      rc = set_err(ctx, SFS2D_E_HIP, "slot bases upload");
+  }
   if (pl->fst) rc = rc ? rc : dalloc(ctx, &pl->d_fsum, 2 * ((size_t)pl->nslots + 1));
   if (rc) { plan_free(pl); delete pl; return rc; }
   hipError_t e = hipSuccess;
@@ -1290,8 +1310,8 @@ int sfs2d_plan_run_phase(sfs2d_plan* pl, int phase, sfs2d_window* out_dev) {
   };
   int rc = 0;
   if (phase == 0 || phase == 1) {
-    if (synth_seg(pl)) {
-      HIPCHK(ctx, launch_slots_synth(pl));
+    if (slots_only(pl)) {
+      HIPCHK(ctx, launch_slots_only(pl));
       if (pl->nslots == 0 && (rc = mark(0))) return rc;
     } else {
       HIPCHK(ctx, launch_prep(pl, true));
@@ -1513,6 +1533,14 @@ int sfs2d_plan_fst_buffer(sfs2d_plan* pl, void** dev_ptr, int64_t* nslots) {
   return 0;
 }
 
+int sfs2d_plan_set_fst_out(sfs2d_plan* pl, double* d_fst) {
+  if (!pl) return SFS2D_E_ARG;
+  if (!pl->fst) return set_err(pl->ctx, SFS2D_E_ARG, "plan was created without SFS2D_F_FST");
+  if (pl->base) return set_err(pl->ctx, SFS2D_E_ARG, "an attached plan's Fst buffer is its own");
+  pl->d_fst = d_fst ? d_fst : pl->d_fst_own;
+  return 0;
+}
+
 int sfs2d_plan_fst_read(sfs2d_plan* pl, double* out_host, int64_t cap) {
   if (!pl) return SFS2D_E_ARG;
   sfs2d_ctx* ctx = pl->ctx;
@@ -1586,7 +1614,7 @@ int sfs2d_plan_time(sfs2d_plan* pl, int iters, double* ms_run, double* ms_k1, do
   double t1 = 0, t2 = 0, t3 = 0, tall = 0;
   for (int it = 0; it < iters; ++it) {
     HIPCHK(ctx, hipEventRecord(pl->ev[0], st));
-    HIPCHK(ctx, synth_seg(pl) ? launch_slots_synth(pl) : launch_prep(pl, true));
+    HIPCHK(ctx, slots_only(pl) ? launch_slots_only(pl) : launch_prep(pl, true));
     HIPCHK(ctx, hipEventRecord(pl->ev[1], st));
     if (pl->do_bg && !pl->fused) HIPCHK(ctx, launch_bg_slices(pl));
     for (sfs2d_plan* a : pl->attached) HIPCHK(ctx, launch_attached(a));

@@ -3188,6 +3188,39 @@ __global__ __launch_bounds__(256) void k_slots_bp(const uint32_t* __restrict__ p
   slots[s] = b < e ? make_uint2(b + 1u, e) : make_uint2(0u, 0u);
 }
 
+// The slot table of a fixed-bp counts plan that has no other k_prep work (a supplied background, no Fst
+// sums: scan_chooseChr / scan_precomputed_BG / sims_scan.process_window over real replicate VCFs): window j
+// of chromosome c is [B_j, B_{j+1}) with B_j the first SNP of c whose pos > j ws (lower_bound of j ws + 1,
+// pos 0 in window 0 as wid_of), found by binary search on the resident sorted positions instead of
+// k_prep's segmentation pass over every position.  One thread per slot searches B_j; B_{j+1} comes from
+// the next lane (the same chromosome's next window), a second search only in a wave's last lane.  A
+// wave's 64 windows share the searches' upper levels (one broadcast line each); per window the search
+// touches ~6 lines of positions (its deep levels) against the window's whole position run for k_prep
+// (config 4: 358 SNPs = 11 lines).  Writes what k_prep's segmentation writes: (first + 1, last + 1),
+// (0, 0) for an empty window.
+__global__ __launch_bounds__(256) void k_slots_search(const uint32_t* __restrict__ pos,
+                                                      const long long* __restrict__ chrom_off,
+                                                      const uint32_t* __restrict__ slot_base, int nchrom, uint32_t ws,
+                                                      uint32_t nslots, uint2* __restrict__ slots) {
+  const uint32_t s = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t sc = min(s, nslots - 1u);   // (lanes past the end search too: their neighbours read them)
+  int lo = 0, hi = nchrom;                   // chromosome c with slot_base[c] <= sc < slot_base[c+1]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (slot_base[mid] <= sc) lo = mid;
+    else hi = mid;
+  }
+  const uint32_t j = sc - slot_base[lo], ns = slot_base[lo + 1] - slot_base[lo];
+  const uint32_t cb = (uint32_t)chrom_off[lo], ce = (uint32_t)chrom_off[lo + 1];
+  const uint32_t b = j ? lower_bound_pos(pos, cb, ce, (unsigned long long)j * ws + 1ull) : cb;
+  uint32_t e = __shfl_down(b, 1, WAVE);
+  const bool lastw = j + 1u == ns;
+  if (lastw) e = ce;
+  else if ((threadIdx.x & (WAVE - 1)) == WAVE - 1 || s + 1u >= nslots)
+    e = lower_bound_pos(pos, b, ce, (unsigned long long)(j + 1u) * ws + 1ull);
+  if (s < nslots) slots[s] = b < e ? make_uint2(b + 1u, e) : make_uint2(0u, 0u);
+}
+
 // Fst sums of an attached fixed-bp plan whose window is m times the base plan's: window j of
 // chromosome c is base windows [j*m, (j+1)*m) of c, and the base's int64 fixed-point sums add
 // exactly (the same value as k_prep accumulating the attached windows directly).

@@ -41,7 +41,7 @@ EXPORTS = [
     "sfs2d_plan_destroy", "sfs2d_scan", "sfs2d_plan_set_timing", "sfs2d_plan_timing_read",
     "sfs2d_plan_stats", "sfs2d_plan_grids", "sfs2d_plan_scan_kernel", "sfs2d_plan_attach", "sfs2d_data_synth_sims",
     "sfs2d_data_read", "sfs2d_plan_run_streams", "sfs2d_ctx_use_own_stream", "sfs2d_bg_hist_dev", "sfs2d_plan_bg_rows_dev", "sfs2d_plan_bg_rows_set_dev",
-    "sfs2d_ctx_get_stream",
+    "sfs2d_ctx_get_stream", "sfs2d_plan_set_fst_out",
 ]
 ABI_VERSION = 2   # SFS2D_ABI_VERSION of include/sfs2d.h
 
@@ -139,6 +139,7 @@ def lib():
     L.sfs2d_data_read.argtypes = [vp, vp, vp, i64]
     L.sfs2d_ctx_use_own_stream.argtypes = [vp]
     L.sfs2d_ctx_get_stream.argtypes = [vp, C.POINTER(vp)]
+    L.sfs2d_plan_set_fst_out.argtypes = [vp, vp]
     L.sfs2d_plan_timing_read.argtypes = [vp, C.POINTER(C.c_int)] + [C.POINTER(C.c_double)] * 3
     L.sfs2d_scan.argtypes = [vp, vp, C.POINTER(Params), vp, vp, vp, vp, i64, C.POINTER(i64)]
     _lib = L

@@ -227,6 +227,11 @@ class Plan:
         self.eng.check(self.eng.lib.sfs2d_plan_fst_read(self.h, out.ctypes.data if n.value else None, n.value))
         return out
 
+    def set_fst_out(self, dev_ptr: Optional[int]):
+        """Write the Fst of the following runs to the device buffer at ``dev_ptr`` (>= nslots float64; None:
+        the plan's own buffer, which read_fst reads) -- sfs2d_plan_set_fst_out."""
+        self.eng.check(self.eng.lib.sfs2d_plan_set_fst_out(self.h, C.c_void_p(dev_ptr) if dev_ptr else None))
+
     def run_many(self, nruns: int, out_dev_ptr: Optional[int] = None):
         """Enqueue `nruns` back-to-back runs from C (no Python between runs)."""
         self.eng.check(self.eng.lib.sfs2d_plan_run_many(self.h, int(nruns),

@@ -10,13 +10,18 @@ N | 32 they are chromosome ends, so no chromosome's background spans two ranks).
 scan pass over the genome: on every rank, background histograms + window segmentation (k_prep),
 then the window scan (k_scan_w, its table prologue fused) -> HBM-resident 64-B window records + Fst.
 Consecutive passes are independent: they go round-robin over 2 plans on 2 HIP streams (the scan
-capped at one workgroup per CU so the next pass's bandwidth-bound k_prep finds CUs beside it).  The
-timed region ends with ONE RCCL all-gather of every rank's final window table over xGMI (N > 1).
-At N = 1 the 5e7-SNP stream (~609 MB per pass) is far past the 256 MB Infinity Cache: the HBM
-roofline is measured on it.
+capped at one workgroup per CU so the next pass's bandwidth-bound k_prep finds CUs beside it).  At
+N > 1 EVERY pass's window table (64-B records + 8-B Fst per slot) is all-gathered to every rank over
+RCCL / xGMI inside the timed region (run_loop_gathered: groups of passes, each group's gather
+overlapped with the next group's passes), as each reference scan returns its whole per-window dict;
+`value` counts gathered windows only.  At N = 1 the 5e7-SNP stream (~609 MB per pass) is far past
+the 256 MB Infinity Cache: the HBM roofline is measured on it.
 
 Second key ``config2_weak``: BASELINE configs[1] (one 1e6-SNP chromosome per GPU, weak scaling, 3 plans
 on 3 streams), the round-1..3 headline, with its own roofline and the single-stream pass latency.
+``config4_sims`` / ``config5_snp_windows`` (N = 1): BASELINE configs[3] (sims_scan at full size: 4 x
+2,500 replicates generated in HBM, 101 x 101 grid) and configs[4] (500-SNP windows, 201 x 151 grid),
+each with the roofline of its scan kernel (k_scan_gw).
 
 `--gpus N` with no launcher: this script starts the N rank processes itself (before touching the
 GPU) and exits with their status; under torchrun, WORLD_SIZE must equal N, and a box with fewer
@@ -348,6 +353,144 @@ def run_loop(cx, plans, steps, warmup, label, time_kernels=False):
             "k_timed_ms": k_timed, "k_timed_samples": nk}
 
 
+def run_loop_gathered(cx, plans, steps, warmup, label, nstreams=2, time_kernels=False):
+    """The N > 1 timed loop: every pass's window table (64-B records + the 8-B Fst column) is
+    all-gathered to every rank, as each reference scan returns its whole per-window dict
+    (twoDSFS_class.py:882-891).  Passes go in groups of P = len(plans) (plan j on stream j % nstreams, one
+    sfs2d_plan_run_streams call per group), each pass writing into its own slice of the group's buffer;
+    the group's buffer is then all-gathered (RCCL over xGMI) on a separate stream while the next group's
+    passes run, into one of NB = 2 buffer slots (a slot is reused only after its gather finished).  The
+    timed region is exactly `steps` passes and their `steps` gathered tables (a last partial group when
+    P does not divide steps); barrier + synchronize on both sides, max over ranks."""
+    torch, dist = cx.torch, cx.dist
+    from sfs2d.engine import Plan
+    P = len(plans)
+    nrec = plans[0].nrec
+    rows = int(cx.max_over_ranks(nrec))   # tables padded to the largest shard (rows flagged empty)
+    fst = plans[0].cfg.fst
+    if nstreams > len(cx.streams):
+        raise ValueError(f"{label}: {nstreams} streams, {len(cx.streams)} available")
+    sstreams = [cx.streams[j % nstreams] for j in range(P)]
+    used = cx.streams[:nstreams]
+    NB = 2
+    rec_b, fst_b = rows * 64, (rows * 8 if fst else 0)
+    per = P * (rec_b + fst_b)   # bytes of one group's tables on one rank
+    bufs = [torch.zeros(per, dtype=torch.uint8, device=cx.cdev) for _ in range(NB)]
+    for b in bufs:
+        v = b[: P * rec_b].view(P, rows, 64)
+        v[:, nrec:, 39] = 0x80   # padding rows: flags = SFS2D_W_EMPTY
+    gathered = [torch.empty(cx.world * per, dtype=torch.uint8, device=cx.cdev) for _ in range(NB)]
+    gs = torch.cuda.Stream(device=cx.local)   # the gathers' stream
+    ev_pass = [torch.cuda.Event() for _ in range(nstreams)]
+    ev_gdone = [torch.cuda.Event() for _ in range(NB)]
+    ev_g = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    gath_groups = [0]
+    tev = []   # (start, end) events around each timed group's all-gather
+
+    def group(g, npass, timed):
+        slot = g % NB
+        if g >= NB:   # the slot's previous gather has read it
+            for s in used:
+                torch.cuda.ExternalStream(s).wait_event(ev_gdone[slot])
+        base = bufs[slot].data_ptr()
+        if fst:
+            for j in range(npass):
+                plans[j].set_fst_out(base + P * rec_b + j * fst_b)
+        Plan.run_streams(plans[:npass], sstreams[:npass], npass, [base + j * rec_b for j in range(npass)])
+        for k, s in enumerate(used[: min(nstreams, npass)]):
+            ev_pass[k].record(torch.cuda.ExternalStream(s))
+            gs.wait_event(ev_pass[k])
+        with torch.cuda.stream(gs):
+            if timed:
+                tev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+                tev[-1][0].record(gs)
+            if cx.shared:   # SFS2D_BENCH_SHARED_GPU rehearsal (gloo, host-staged)
+                parts = [torch.empty(per, dtype=torch.uint8) for _ in range(cx.world)]
+                dist.all_gather(parts, bufs[slot].cpu())
+                gathered[slot].copy_(torch.cat(parts).to(cx.cdev))
+            else:
+                dist.all_gather_into_tensor(gathered[slot], bufs[slot])
+            if timed:
+                tev[-1][1].record(gs)
+            ev_gdone[slot].record(gs)
+        gath_groups[0] += 1
+
+    def passes(n, timed, g0=0):
+        g = g0
+        while n > 0:
+            k = min(P, n)
+            group(g, k, timed)
+            n -= k
+            g += 1
+        return g
+
+    g = passes(P, False)
+    torch.cuda.synchronize()
+    for q in plans:
+        q.check()
+    t_s = time.perf_counter()
+    settle = 0
+    while time.perf_counter() - t_s < SETTLE_S:
+        g = passes(8 * P, False, g)
+        torch.cuda.synchronize()
+        settle += 8 * P
+    g = passes(warmup * nstreams, False, g)
+    torch.cuda.synchronize()
+    dist.barrier()
+    if time_kernels:
+        for q in plans:
+            q.set_timing(steps, every=4, kernels=5)
+    torch.cuda.synchronize()
+    g0 = g
+    t0 = time.perf_counter()
+    ev_g[0].record(gs)
+    g = passes(steps, True, g)
+    ev_g[1].record(gs)
+    t_enq = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    kt = [q.timing_read() for q in plans] if time_kernels else []
+    if time_kernels:
+        for q in plans:
+            q.set_timing(0)
+    nk = sum(n for n, _ in kt)
+    k_timed = (sum(n * k[0] for n, k in kt) / max(1, nk), sum(n * k[2] for n, k in kt) / max(1, nk))
+    dt = float(cx.max_over_ranks(dt))
+    span_ms = float(cx.max_over_ranks(float(ev_g[0].elapsed_time(ev_g[1]))))
+    gat_ms = float(cx.max_over_ranks(float(sum(a.elapsed_time(b) for a, b in tev))))
+    # every gathered table of the last groups: this rank's section equals its own pass output, every plan's
+    # table the same (independent passes over the same shard), and the windows of all ranks counted
+    last_groups = sorted({(g - 1 - i) for i in range(min(NB, g - g0))})
+    nwin_pass = None
+    for gg in last_groups:
+        slot = gg % NB
+        npass = P if (gg < g - 1 or steps % P == 0) else steps % P
+        G = gathered[slot].view(cx.world, per)
+        for q in plans:
+            q.check()
+        own = bufs[slot][: npass * rec_b].view(npass, rows, 64)
+        for j in range(npass):
+            if not torch.equal(own[j][:nrec], own[0][:nrec]):
+                raise RuntimeError(f"{label}: pass {j} of group {gg} disagrees with pass 0")
+        if not torch.equal(G[cx.rank], bufs[slot]):
+            raise RuntimeError(f"{label}: the gathered tables disagree with this rank's own")
+        tabs = G[:, : P * rec_b].reshape(cx.world, P, rows, 64)[:, :npass].cpu().numpy()
+        counts = {n_windows(tabs[:, j].reshape(-1, 64)) for j in range(npass)}
+        if len(counts) != 1:
+            raise RuntimeError(f"{label}: gathered tables hold different window counts {counts}")
+        nwin_pass = counts.pop()
+    if fst:
+        for q in plans:
+            q.set_fst_out(None)
+    mine = bufs[(g - 1) % NB][:rec_b].view(rows, 64)[:nrec].cpu().numpy()
+    allr = gathered[(g - 1) % NB].view(cx.world, per)[:, :rec_b].reshape(-1, 64).cpu().numpy()
+    return {"dt": dt, "device_ms": span_ms, "gather_ms": gat_ms, "t_enq": t_enq, "rows": rows,
+            "gathered": allr, "mine": mine, "streams": nstreams, "settle_passes": settle,
+            "k_timed_ms": k_timed, "k_timed_samples": nk, "windows_per_pass_gathered": nwin_pass,
+            "gathers": g - g0, "group": P, "gathered_bytes_per_pass": cx.world * (rec_b + fst_b)}
+
+
 def kernel_times(plan, runs=16):
     """k_prep / k_bg_slice / scan kernel durations (events in their dispatch packets), one stream, untimed."""
     plan.set_timing(runs, every=1)
@@ -399,9 +542,17 @@ def config3_strong(cx, args):
     sub, c0 = p.slice_snps(cuts[cx.rank], cuts[cx.rank + 1])
     dev = cx.eng.upload(sub)
     ns = 2
-    plans = [cx.eng.plan(dev, cfg) for _ in range(ns)]
-    r = run_loop(cx, plans, args.steps, args.warmup, "config 3", time_kernels=True)
-    total_windows = n_windows(r["gathered"])
+    if cx.world > 1:
+        # every pass's table gathered (run_loop_gathered): groups of P passes on the 2 streams, P | steps
+        P = next(k for k in (args.group, 4, 2, 1) if k >= 1 and args.steps % k == 0)
+        plans = [cx.eng.plan(dev, cfg) for _ in range(max(P, ns))]
+        r = run_loop_gathered(cx, plans[:P] if P >= ns else plans, args.steps, args.warmup, "config 3",
+                              nstreams=ns, time_kernels=True)
+        total_windows = r["windows_per_pass_gathered"]
+    else:
+        plans = [cx.eng.plan(dev, cfg) for _ in range(ns)]
+        r = run_loop(cx, plans, args.steps, args.warmup, "config 3", time_kernels=True)
+        total_windows = n_windows(r["gathered"])
     win_rank = n_windows(r["mine"])
     k1, _, k3 = kernel_times(plans[0])
     # a single scan of the genome as a user runs it: the default plan (no scan grid cap), back to back
@@ -457,6 +608,9 @@ def config3_strong(cx, args):
     dev.close()
     step_s = r["dt"] / args.steps
     out = {"value": total_windows * args.steps / r["dt"], "ms_per_step": step_s * 1e3,
+           "gathered_info": ({"tables_gathered": r["gathers"] * r["group"], "passes_per_gather": r["group"],
+                              "bytes_per_pass_all_ranks": r["gathered_bytes_per_pass"],
+                              "windows_per_pass": total_windows} if cx.world > 1 else None),
            "host_enqueue_ms_per_step": r["t_enq"] / args.steps * 1e3,
            "device_ms_per_step": r["device_ms"] / args.steps, "gather_ms": r["gather_ms"],
            "settle": {"seconds": SETTLE_S, "passes": r["settle_passes"],
@@ -480,16 +634,21 @@ def config2_weak(cx, args):
     dev = cx.eng.upload(p)
     cfg = ScanConfig(n1p=POP, n2p=POP, window=WS, fst=True)
     ns = max(1, args.streams)
-    plans = [cx.eng.plan(dev, cfg) for _ in range(ns)]
     steps = max(args.steps, args.config2_steps)
-    r = run_loop(cx, plans, steps, max(args.warmup, 20), "config 2")
+    if cx.world > 1:   # every pass's table gathered, groups of P passes over the ns streams
+        P = next(k for k in (args.group, 4, 2, 1) if k >= 1 and steps % k == 0)
+        plans = [cx.eng.plan(dev, cfg) for _ in range(max(P, ns))]
+        r = run_loop_gathered(cx, plans, steps, max(args.warmup, 20), "config 2", nstreams=ns)
+    else:
+        plans = [cx.eng.plan(dev, cfg) for _ in range(ns)]
+        r = run_loop(cx, plans, steps, max(args.warmup, 20), "config 2")
     k1, k2, k3 = kernel_times(plans[0])
     one = single_pass_ms(cx, plans[0], 40) if cx.rank == 0 else None
     nrec, grids, kname = plans[0].nrec, plans[0].grids(), plans[0].scan_kernel()
     for x in plans[::-1]:
         x.close()
     dev.close()
-    total = n_windows(r["gathered"])
+    total = r.get("windows_per_pass_gathered") or n_windows(r["gathered"])
     nwin = n_windows(r["mine"])
     b3 = algorithmic_bytes(p.n, nrec, nwin, "k3")
     ach = b3 / (k3 * 1e-3) / 1e9
@@ -500,13 +659,154 @@ def config2_weak(cx, args):
             "workload": "configs[1]: synthetic 1 chromosome x 1e6 SNPs per GPU (seed 12345 + rank), 20 kb, "
                         "per-chromosome background, T2D + T1D + Fst",
             "windows_per_gpu": nwin, "windows_all_gpus": total,
-            "parallelism": f"one chromosome per GPU, {ns} plans on {ns} HIP streams (passes overlap)"
-                           + ("; one RCCL all-gather of the final tables" if cx.world > 1 else ""),
+            "parallelism": f"one chromosome per GPU, {len(plans)} plans on {ns} HIP streams (passes overlap)"
+                           + ("; every pass's table (records + Fst) all-gathered over RCCL, overlapped with the "
+                              f"next passes (groups of {r.get('group')})" if cx.world > 1 else ""),
             "kernels_ms": {"k_prep": k1, "k_bg_slice": k2, kname: k3},
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                          "traffic": traffic, "kernel": kname, "ms": k3, "algorithmic_bytes": b3,
                          "note": "the 8 MB stream is MALL-resident: not an HBM measurement; traffic: "
                                  + (tsrc or "no PMC pass committed")}}
+
+
+C4_REP, C4_GEN, C4_WIN, C4_POP, C4_SEED = 2500, 4, 2000, 50, 20251016
+
+
+def config4_sims(cx, args):
+    """BASELINE configs[3]: sims_scan.likelihood_scan (sims_scan.py:593-644 -> process_window 451-590) over
+    4 generations x 2,500 replicates x 2,000 windows of 20 kb (Poisson(358.5) SNPs per window: 7.17e9
+    SNPs, 57 GB packed, generated in HBM by k_synth_sims), pop_size 50/50 (101 x 101 grid: k_scan_gw),
+    each generation scanned against its own background (all its SNPs with pos in [0, 500000]: 2D
+    folded, 1D unfolded -- quirk Q7).  The slot table comes from k_prep's segmentation of the resident
+    positions, as real replicate VCFs need (not the generator's window offsets).  A step = one pass over
+    all four generations: the four independent plans go round-robin on 2 HIP streams, so one
+    generation's segmentation (bandwidth-bound) runs beside another's scan (latency-bound).  Inputs
+    resident in HBM; generation time reported apart."""
+    from sfs2d import _lib as L
+    from sfs2d.engine import Plan, ScanConfig
+    from sfs2d.synth import miss_table, sims_window_counts
+    torch = cx.torch
+    n, ws = C4_POP, WS
+    mt = miss_table(2 * n)
+    datas, plans, nsnp, t_gen = [], [], 0, 0.0
+    prev = os.environ.get("SFS2D_SEG")
+    # the slot table real replicate VCFs get: a binary search on the resident positions (k_slots_search),
+    # not the generator's window offsets
+    os.environ["SFS2D_SEG"] = args.c4_seg
+    try:
+        for g in range(C4_GEN):
+            wc = sims_window_counts(C4_SEED, g, C4_REP, C4_WIN)
+            nsnp += int(wc.astype(np.int64).sum())
+            t0 = time.perf_counter()
+            dev = cx.eng.synth_sims(C4_SEED, g, C4_REP, C4_WIN, ws, n, n, wc, mt, mt)
+            torch.cuda.synchronize()
+            t_gen += time.perf_counter() - t0
+            h2, u1, u2 = cx.eng.bg_hist(dev, ScanConfig(n1p=n, n2p=n, start_position=0, end_position=500000), -1)
+            pl = cx.eng.plan(dev, ScanConfig(n1p=n, n2p=n, window=ws, bg_mode=L.BG_SUPPLIED))
+            pl.set_background(h2.reshape(-1).astype(np.float64), u1[: n + 1].astype(np.float64),
+                              u2[: n + 1].astype(np.float64))
+            datas.append(dev)
+            plans.append(pl)
+    finally:
+        if prev is None:
+            os.environ.pop("SFS2D_SEG", None)
+        else:
+            os.environ["SFS2D_SEG"] = prev
+    kname, grids = plans[0].scan_kernel(), plans[0].grids()
+    streams = [cx.streams[j % 2] for j in range(C4_GEN)]
+    # one generation alone on one stream (a user scanning one generation's replicates)
+    one = single_pass_ms(cx, plans[0], runs=5)
+    k1a, _, k3a = kernel_times(plans[0], runs=4)
+    for q in plans:
+        q.run()
+    torch.cuda.synchronize()
+    t_s = time.perf_counter()
+    while time.perf_counter() - t_s < SETTLE_S:
+        Plan.run_streams(plans, streams, C4_GEN, None)
+        torch.cuda.synchronize()
+    steps = max(2, min(args.steps, args.sims_steps))
+    for q in plans:
+        q.set_timing(steps, every=1, kernels=5)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    Plan.run_streams(plans, streams, C4_GEN * steps, None)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kt = [q.timing_read() for q in plans]
+    for q in plans:
+        q.set_timing(0)
+    nk = sum(c for c, _ in kt)
+    k1 = sum(c * k[0] for c, k in kt) / max(1, nk)
+    k3 = sum(c * k[2] for c, k in kt) / max(1, nk)
+    nwin, nslot = 0, 0
+    for q in plans:
+        q.check()
+        recs = q.read()
+        nwin += int(((recs["flags"] & L.W_EMPTY) == 0).sum())
+        nslot += q.nrec
+    ms = dt / steps * 1e3
+    b3 = algorithmic_bytes(nsnp // C4_GEN, nslot // C4_GEN, 0, "k3") - 24 * (nslot // C4_GEN)   # no Fst
+    b3a = b3
+    for q in plans:
+        q.close()
+    for d in datas:
+        d.close()
+    torch.cuda.synchronize()
+    return {"value": nwin / (ms * 1e-3), "unit": "windows/s", "ms_per_step": ms, "steps": steps,
+            "windows": nwin, "snps": nsnp, "generations": C4_GEN, "replicates": C4_REP,
+            "workload": f"configs[3]: sims_scan likelihood_scan, {C4_GEN} generations x {C4_REP} replicates x "
+                        f"{C4_WIN} windows of 20 kb, Poisson(358.5) SNPs per window ({nsnp} SNPs, "
+                        f"{nsnp * 8 / 1e9:.1f} GB resident), pop_size 50/50 (101 x 101 grid), supplied per-generation "
+                        "background; the slot table from the resident positions (no generator knowledge)",
+            "parallelism": f"{C4_GEN} plans (one per generation) round-robin on 2 HIP streams",
+            "generate_s": t_gen,
+            "one_generation_alone_ms": one, "one_generation_alone_windows_per_s": (nwin / C4_GEN) / (one * 1e-3),
+            "slot_table": {"search": "k_slots_search (binary search on the positions)",
+                           "prep": "k_prep's segmentation pass"}.get(args.c4_seg, args.c4_seg),
+            "kernels_ms": {"slots": k1, kname: k3, "alone": {"slots": k1a, kname: k3a}},
+            "roofline": {"bound": "hbm", "kernel": kname, "achieved": b3 / (k3 * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": b3 / (k3 * 1e-3) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": b3,
+                         "frac_alone": b3a / (k3a * 1e-3) / 1e9 / HBM_PEAK_GBS, "scan_grid_threads": grids[1],
+                         "note": "4 B/SNP + 72 B/slot (8-B slot record in, 64-B record out) per generation over the "
+                                 "kernel's average duration in the timed steps (events in its dispatch packets, "
+                                 "overlapped with the other stream's k_prep); frac_alone: one stream"}}
+
+
+def config5_snpwin(cx, args):
+    """BASELINE configs[4]: scan_perChr_bySNPs (twoDSFS_class.py:1422-1541) -- 500-SNP windows, pop_size
+    100/75 (201 x 151 grid: k_scan_gw), per-chromosome backgrounds, T2D + T1D in fp64 (the tolerance
+    sweep showed fp32 misses 1e-10: DESIGN.md), on 1e6 synthetic SNPs (4 chromosomes).  Passes overlapped
+    on 2 HIP streams as the headline loop."""
+    from sfs2d.engine import ScanConfig
+    from sfs2d import _lib as L
+    from sfs2d.synth import synth_genome
+    p = synth_genome(4, 250_000, 100, 75, seed=2024)
+    dev = cx.eng.upload(p)
+    cfg = ScanConfig(n1p=100, n2p=75, window_mode=L.WINDOW_SNPS, window=500)
+    plans = [cx.eng.plan(dev, cfg) for _ in range(2)]
+    steps = max(args.steps, 200)
+    r = run_loop(cx, plans, steps, max(args.warmup, 20), "config 5", time_kernels=True)
+    k1, _, k3 = kernel_times(plans[0])
+    one = single_pass_ms(cx, plans[0], 40)
+    nrec, grids, kname = plans[0].nrec, plans[0].grids(), plans[0].scan_kernel()
+    for q in plans:
+        q.close()
+    dev.close()
+    nwin = n_windows(r["mine"])
+    ms = r["dt"] / steps * 1e3
+    b3 = 4 * p.n + (8 + 64) * nrec
+    kt = r["k_timed_ms"][1]
+    return {"value": nwin / (ms * 1e-3), "unit": "windows/s", "ms_per_step": ms, "steps": steps, "windows": nwin,
+            "snps": p.n, "single_stream_pass_ms": one,
+            "workload": "configs[4]: scan_perChr_bySNPs, 500-SNP windows, n1=200 n2=150 haploid (pop_size 100/75), "
+                        "synthetic 4 chromosomes x 250,000 SNPs, per-chromosome backgrounds, T2D + T1D (fp64)",
+            "parallelism": "2 plans on 2 HIP streams (passes overlap)",
+            "kernels_ms": {"k_prep": k1, kname: k3, "timed_loop": {"k_prep": r["k_timed_ms"][0], kname: kt}},
+            "roofline": {"bound": "hbm", "kernel": kname, "achieved": b3 / (kt * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": b3 / (kt * 1e-3) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": b3,
+                         "scan_grid_threads": grids[1],
+                         "note": "4 B/SNP + 72 B/slot over the kernel's average duration in the timed steps; the 4 MB "
+                                 "stream is MALL-resident, so this is not an HBM measurement"}}
 
 
 def main():
@@ -520,6 +820,12 @@ def main():
     ap.add_argument("--no-variants", action="store_true", help="skip the config-3 run without Fst")
     ap.add_argument("--streams", type=int, default=3, help="config 2: plans / HIP streams (passes overlap)")
     ap.add_argument("--config2-steps", type=int, default=400, help="config 2: at least this many passes")
+    ap.add_argument("--no-sims", action="store_true", help="skip the config-4 / config-5 keys")
+    ap.add_argument("--sims-steps", type=int, default=5, help="config 4: timed passes over the 4 generations")
+    ap.add_argument("--c4-seg", default="search", choices=["search", "prep"],
+                    help="config 4's slot table: binary search on the positions, or k_prep's segmentation")
+    ap.add_argument("--group", type=int, default=4,
+                    help="N > 1: passes per all-gather group (every pass's table is gathered; P must divide steps)")
     args = ap.parse_args()
     if args.gpus < 1 or args.steps < 1:
         raise SystemExit("--gpus and --steps must be >= 1")
@@ -555,6 +861,10 @@ def main():
 
     c3, genome = config3_strong(cx, args)
     c2 = None if args.no_config2 else config2_weak(cx, args)
+    c4 = c5 = None
+    if world == 1 and not args.no_sims:
+        c5 = config5_snpwin(cx, args)
+        c4 = config4_sims(cx, args)
 
     if rank == 0:
         r0 = c3["rank0"]
@@ -574,11 +884,15 @@ def main():
                        "stats": "T2D, T1D_p1, T1D_p2 (reference semantics) + Hudson Fst (DESIGN.md; not in the "
                                 "reference, parity vs its own oracle restatement)",
                        "parallelism": f"{world} GPU(s), SNP ranges cut at window starts ({c3['cuts']}: chromosome "
-                                      "ends, no background exchange); 2 plans on 2 HIP streams per GPU, passes "
-                                      "overlapped" + ("; one RCCL all-gather of the final window tables in the "
-                                                      "timed region" if world > 1 else "")},
+                                      "ends, no background exchange); passes overlapped on 2 HIP streams per GPU"
+                                      + ("; EVERY pass's window table (64-B records + 8-B Fst) all-gathered to every "
+                                         "rank over RCCL inside the timed region, each group's gather overlapped with "
+                                         "the next group's passes; value counts gathered windows only"
+                                         if world > 1 else "")},
             "host_enqueue_ms_per_step": c3["host_enqueue_ms_per_step"],
-            "device_ms_per_step": c3["device_ms_per_step"], "gather_ms": c3["gather_ms"], "settle": c3["settle"],
+            "device_ms_per_step": c3["device_ms_per_step"], "gather_ms": c3["gather_ms"],
+            "gather_ms_per_step": (c3["gather_ms"] / args.steps) if world > 1 else None,
+            "gathered": c3.get("gathered_info"), "settle": c3["settle"],
             "rank0": r0,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "kernel": r0["scan_kernel"],
@@ -599,6 +913,10 @@ def main():
             line["config3_20kb_500kb"] = c3["config3_20kb_500kb"]
         if c2 is not None:
             line["config2_weak"] = c2
+        if c4 is not None:
+            line["config4_sims"] = c4
+        if c5 is not None:
+            line["config5_snp_windows"] = c5
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(genome.subset_chroms([0]))
         if not args.no_e2e and world == 1:

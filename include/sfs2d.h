@@ -212,6 +212,11 @@ int sfs2d_plan_bg_rows_set_dev(sfs2d_plan* plan, const int64_t* d_rows, int64_t 
 /* Fst of the last run per window slot (NaN: no qualifying SNP / empty slot); plans with SFS2D_F_FST */
 int sfs2d_plan_fst_read(sfs2d_plan* plan, double* out_host, int64_t cap);
 int sfs2d_plan_fst_buffer(sfs2d_plan* plan, void** dev_ptr, int64_t* nslots);
+/* Fst output of the following runs: a caller-owned device buffer of >= nslots doubles (NULL = the plan-owned
+ * buffer again), as sfs2d_plan_run's out_dev is for the records -- consecutive runs of one plan can keep their
+ * Fst columns apart (e.g. each pass's table gathered while the next pass runs: bench.py at N > 1).  Attached
+ * plans keep their own buffer. */
+int sfs2d_plan_set_fst_out(sfs2d_plan* plan, double* d_fst);
 int sfs2d_plan_run_phase(sfs2d_plan* plan, int phase, sfs2d_window* out_dev);
 /* Multi-resolution: attach to `base` (a per-chromosome-background plan on the small-grid path) a
  * plan over the same data whose params differ only in window_mode / window / flags.  The base's

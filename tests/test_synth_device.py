@@ -62,8 +62,9 @@ def test_scan_of_generated_data_vs_oracle():
 def test_generator_slots_equal_segmentation(monkeypatch, ws):
     """A fixed-bp plan over generated replicates with the generator's window length takes its slot table
     from the generator's window offsets (k_slots_synth) instead of k_prep's segmentation of the
-    positions: the records are byte-equal to the segmentation path's (SFS2D_SYNTH_SEG=0), including
-    windows without SNPs; another window length (10 kb) takes the segmentation path either way."""
+    positions: the records are byte-equal to the segmentation path's (SFS2D_SEG=prep) and to the binary
+    search on the positions (SFS2D_SEG=search, k_slots_search: what real replicate VCFs get), including
+    windows without SNPs; another window length (10 kb) takes the search or k_prep either way."""
     from sfs2d import _lib as L
     from sfs2d.engine import Engine, ScanConfig
     from sfs2d.synth import miss_table, sims_window_counts
@@ -80,8 +81,8 @@ def test_generator_slots_equal_segmentation(monkeypatch, ws):
         bg = (h2.reshape(-1).astype(np.float64), u1[: n + 1].astype(np.float64), u2[: n + 1].astype(np.float64))
         cfg = ScanConfig(n1p=n, n2p=n, window=ws, bg_mode=L.BG_SUPPLIED)
         outs = []
-        for flag in ("1", "0"):
-            monkeypatch.setenv("SFS2D_SYNTH_SEG", flag)
+        for flag in ("auto", "prep", "search"):
+            monkeypatch.setenv("SFS2D_SEG", flag)
             pl = eng.plan(dev, cfg)
             pl.set_background(*bg)
             for _ in range(2):   # the scan clears the slot table after use: a second run rebuilds it
@@ -91,7 +92,52 @@ def test_generator_slots_equal_segmentation(monkeypatch, ws):
             pl.close()
     finally:
         dev.close()
-    assert outs[0] == outs[1]
+    assert outs[0] == outs[1] == outs[2]
+
+
+@pytest.mark.parametrize("ws", [20000, 3000, 100000])
+def test_slot_search_equals_segmentation(monkeypatch, ws):
+    """Supplied-background fixed-bp counts plans (scan_chooseChr / scan_precomputed_BG / sims over real
+    VCFs) take their slot table from k_slots_search (binary search on the resident positions) instead of
+    k_prep's segmentation: byte-equal records on data with empty windows (3 kb), windows of one or two
+    SNPs, a one-SNP chromosome, and with Fst (k_prep's sums keep k_prep), on small (k_scan_w) and large
+    (k_scan_gw) grids; and the search path against the oracle."""
+    from oracle import sfs_oracle as O
+    from sfs2d import _lib as L
+    from sfs2d.engine import Engine, ScanConfig
+    from sfs2d.synth import synth_genome
+    import golden_util as gu
+    eng = Engine.get(0)
+    for n in (25, 50):
+        p = synth_genome(5, [5000, 1, 3000, 70, 900], n, n, seed=ws + n)
+        dev = eng.upload(p)
+        cfg_o = O.Cfg(n, n)
+        idx = np.arange(p.chrom_off[0], p.chrom_off[1])
+        bg = (O.sfs2d(p, idx, cfg_o), O.fold1d(O.sfs1d(p, idx, 1, cfg_o)), O.fold1d(O.sfs1d(p, idx, 2, cfg_o)))
+        try:
+            for fst in (False, True):
+                outs = []
+                for flag in ("search", "prep"):
+                    monkeypatch.setenv("SFS2D_SEG", flag)
+                    pl = eng.plan(dev, ScanConfig(n1p=n, n2p=n, window=ws, bg_mode=L.BG_SUPPLIED, fst=fst))
+                    pl.set_background(*bg)
+                    for _ in range(2):
+                        pl.run()
+                        pl.check()
+                    outs.append(pl.read())
+                    pl.close()
+                assert outs[0].tobytes() == outs[1].tobytes()
+            recs = outs[0]
+            body = recs[(recs["flags"] & L.W_EMPTY) == 0]
+            ref = O.window_records(p, O.bp_windows(p, ws), cfg_o, lambda c: bg)
+            assert len(body) == len(ref)
+            for r, o in zip(body, ref):
+                assert int(r["snp_count"]) == o["snp_count"] and int(r["n2"]) == o["N2"]
+                for f, g in (("t2d", "T2D"), ("t1d_p1", "T1D_p1"), ("t1d_p2", "T1D_p2")):
+                    if o[g] is not None:
+                        assert gu.close(float(r[f]), o[g]), (f, float(r[f]), o[g])
+        finally:
+            dev.close()
 
 
 @pytest.mark.timeout(600)
