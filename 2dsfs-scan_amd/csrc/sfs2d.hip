@@ -857,6 +857,10 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
     for (int c = 0; c < nc && all; ++c) all = data->chrom_off[c + 1] > data->chrom_off[c];
     pl->seg_synth = all && !seg_prep && !seg_srch;
   }
+  // (Not with per-chromosome backgrounds, whose k_prep runs anyway: there a search before a counts-only
+  // k_prep cost more than the positions it saved k_prep -- config 3: k_prep 83.5 -> 64.5 us but one pass
+  // 0.214 -> 0.225 ms, the overlapped step 0.184 -> 0.191 ms, config 2 2.4e8 -> 2.0e8 windows/s; as extra
+  // blocks of k_prep itself, concurrent with its tiles: 0.185 -> 0.193 ms; profiles/r06e_*, r06f_*.)
   pl->seg_search = bp && pl->cnt && !pl->do_bg && !pl->seg_synth && !seg_prep;
   pl->K.nm1 = data->n > 0 ? (uint32_t)(data->n - 1) : 0u;
   pl->K.kmul = (uint32_t)(pl->K.n2 + 1) | (1u << 16);

@@ -275,6 +275,36 @@ def test_run_streams_none_is_the_engine_stream():
     dev.close()
 
 
+def test_fst_out_buffers_per_run():
+    """sfs2d_plan_set_fst_out: consecutive runs of one plan write their Fst columns into caller buffers
+    (bench.py's per-pass gathered loop), equal to the plan-owned buffer's values; None restores it."""
+    import torch
+    from sfs2d.engine import Engine, ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(2, [200000, 90000], 25, 25, seed=31)
+    eng = Engine.get(0)
+    dev = eng.upload(p)
+    pl = eng.plan(dev, ScanConfig(n1p=25, n2p=25, window=20000, fst=True))
+    pl.run()
+    want = pl.read_fst()
+    bufs = [torch.full((len(want),), -1.0, dtype=torch.float64, device="cuda:0") for _ in range(2)]
+    prev = eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        for b in bufs:
+            pl.set_fst_out(b.data_ptr())
+            pl.run()
+        torch.cuda.synchronize()
+        for b in bufs:
+            assert np.array_equal(b.cpu().numpy(), want, equal_nan=True)
+        pl.set_fst_out(None)
+        pl.run()
+        assert np.array_equal(pl.read_fst(), want, equal_nan=True)
+    finally:
+        eng.set_stream(prev)
+    pl.close()
+    dev.close()
+
+
 def test_key_error_on_counts_above_sample_size():
     import twoDSFS_class as T
     d = {"c-1": {"calls": {"uv": (0, 3), "bv": (2, 0)}, "annotation": "x"},
