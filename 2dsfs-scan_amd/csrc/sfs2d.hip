@@ -1124,6 +1124,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   pl->last_chrom = last_c;
 
   // k_prep tiles (never crossing a chromosome); k_prep always runs (it writes the per-SNP bins)
+  int64_t tileT = 0;
   {
     const int64_t n = data->n;
     // ~1000+ tiles for big inputs (several workgroups per CU), >= 4096 SNPs each (flush amortised)
@@ -1133,6 +1134,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
     const int64_t Tmax = kfst_t ? 32768 : 65536;
     int64_t T = std::max<int64_t>(4096, std::min<int64_t>(Tmax, (n / 768 + 4095) / 4096 * 4096));
     if (const char* ev = std::getenv("SFS2D_TILE")) T = std::max<int64_t>(2048, std::atoll(ev) & ~int64_t(3));   // tuning
+    tileT = T;
     // tile edges on absolute multiples of 4 SNPs (T is): only a chromosome's first and last step
     // take k_prep's masked edge path, every interior step of every tile the fast one
     for (int c = 0; c < nc; ++c)
@@ -1163,6 +1165,18 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
                                : hipFuncGetAttributes(&fa, (const void*)k_prep<true, true, true, true, false, false>);
     const size_t stat = ae == hipSuccess ? fa.sharedSizeBytes : (kfst ? 24 * 1024 : 1024);
     pl->lds_hist = pl->bg_lds + stat <= 160 * 1024;
+    // k_prep's joint (alt1, alt2) histogram (prep_tile, JNT): counts plans whose k_prep only histograms
+    // and segments, with tiles of >= 16k SNPs (its margins pass at the tile's end cost config 2's 4k-SNP
+    // tiles more than the atomics saved: 2.25e8 vs 2.32-2.46e8 windows/s, profiles/r06i_prep_joint_hist.txt),
+    // while the LDS stays <= 64 KB (nb2 words more).  SFS2D_JNT=0: three atomics per SNP; =1: the joint
+    // histogram whatever the tile size (tests)
+    const char* jev = std::getenv("SFS2D_JNT");
+    const size_t jl = pl->bg_lds + (size_t)K.nb2 * 4;
+    const bool jwant = jev ? jev[0] == '1' : tileT >= 16384;
+    if (pl->lds_hist && pl->cnt && !kfst && jl + stat <= 64 * 1024 && jwant) {
+      pl->K.jnt = K.nb2;
+      pl->bg_lds = jl;
+    }
   }
   if (pl->lds_hist && pl->bg_lds > 64 * 1024) {
     const hipFuncAttribute A = hipFuncAttributeMaxDynamicSharedMemorySize;

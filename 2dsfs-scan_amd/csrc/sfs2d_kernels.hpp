@@ -62,8 +62,9 @@ constexpr int LNF = 256;          // k_scan_w: x ln x entries in LDS (x < LNF; t
 __host__ __device__ inline int wl_rtn(int n1p, int n2p) { return 2 * (n1p > n2p ? n1p : n2p) + 2; }
 constexpr int RCPN = 512;         // (1/k, 1/(k(k-1))) for k < 512 (Fst: called allele counts ref + alt <= 510), after the LNT tables
 #ifndef SFS2D_ABL   // ablation builds (timing only, results wrong): bit 0 no 2D atomic, 1 no 1D atomics, 2 no D / lp
-#define SFS2D_ABL 0  // reads, 3 no record stores, 4 no Fst table reads, 5 no 1D end pass; k_prep's common step:
-#endif              // 6 no LDS histogram atomics, 7 loads only (no classification, histograms or segmentation)
+#define SFS2D_ABL 0  // reads, 3 no record stores, 4 no Fst table reads, 5 no 1D end pass, 8 no per-window wave
+#endif              // sums, 9 no batched finish; k_prep's common step: 6 no LDS histogram atomics, 7 loads only
+                    // (no classification, histograms or segmentation)
 constexpr int REPL = 4;           // replicas of the per-chromosome background histograms
 constexpr int PW_MAX_LEAVES = 1024;  // numpy pairwise leaves (64-128 values each): grids up to 255 x 255 (u8 counts)
 constexpr int LEAVES_PER_SLICE = 4;
@@ -137,6 +138,7 @@ struct KParams {
                          // largest called count (even; >= wl_rtn(n1p, n2p))
   int ntri;              // k_scan_gw TRI (folded counts plans, n1 = n2 = n): the reachable 2D bins
                          // x1 + x2 <= n, (n+1)(n+2)/2 of them, stored as a triangle (0: full grid)
+  int jnt;               // k_prep (counts plans, LDS histogram): the joint (alt1, alt2) histogram, see prep_tile
 };
 
 struct Tile {   // k_prep work item: SNPs [begin, end) of chromosome chrom = [cb, ce), slots from sbase
@@ -644,6 +646,14 @@ __device__ __forceinline__ void prep_tile(const KParams& P, const Tile t, uint32
   // the exact path (any u8 counts, n <= 510) reads the global table
   __shared__ double2 sh_rcp[FST ? RCPN / 2 : 1];
   __shared__ uint32_t sh_wlo;
+  // JNT (P.jnt = nb2 words, plans whose k_prep only histograms and segments): the common step counts
+  // every SNP once in the joint histogram of its unfolded alt counts (alt1, alt2), laid out as the 2D
+  // grid, and a folded SNP once more in the 2D histogram at its (ref1, ref2) key: 1 + (folded) LDS
+  // atomics per SNP instead of 3 (2D key, both unfolded 1D spectra).  The tile's end derives both 1D
+  // spectra as the joint histogram's margins and adds its bins with alt1 + alt2 <= fold_thr -- the
+  // unfolded SNPs' 2D keys -- to the 2D histogram (the edge steps' process() counts the three directly)
+  constexpr bool JNT = DO_BG && LDS_HIST && !DO_BINS && !FST;
+  const bool jnt = JNT && P.jnt != 0;
   STAMP(20);
   BLK_STAMP(0, 0);
   uint32_t* gh = repl + ((size_t)(ti % REPL) * P.nchrom + t.chrom) * (size_t)P.nh;
@@ -658,7 +668,7 @@ __device__ __forceinline__ void prep_tile(const KParams& P, const Tile t, uint32
   }
   if (DO_BG) {
     if (LDS_HIST)
-      for (int k = threadIdx.x; k < P.nh * hr + WAVE; k += BLOCK1) sh_hist[k] = 0u;
+      for (int k = threadIdx.x; k < P.nh * hr + WAVE + (JNT ? P.jnt : 0); k += BLOCK1) sh_hist[k] = 0u;
     if (threadIdx.x == 0) sh_b2 = 0u;
   }
   if (DO_SEG) {
@@ -804,6 +814,7 @@ __device__ __forceinline__ void prep_tile(const KParams& P, const Tile t, uint32
   uint32_t* const h1a_l = hist_l + ((uint32_t)P.h1a << hsh);
   uint32_t* const h1b_l = hist_l + ((uint32_t)P.h1b << hsh);
   uint32_t* const trash_p = sh_hist + trash;
+  uint32_t* const jh_l = sh_hist + P.nh * hr + WAVE;             // JNT: the joint histogram
   const uint32_t n2p1 = vreg(P.n2 + 1), nb2m1 = vreg(P.nb2 - 1), n1pm1 = vreg(P.n1p - 1), n2pm1 = vreg(P.n2p - 1);
   auto process_fast = [&](uint32_t i0, const uint4& cv, const uint4& pv, uint32_t wprev, uint32_t wnext) {
     const uint32_t cc[4] = {cv.x, cv.y, cv.z, cv.w};
@@ -818,6 +829,16 @@ __device__ __forceinline__ void prep_tile(const KParams& P, const Tile t, uint32
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint32_t c = cc[k];
+      if (JNT && jnt) {
+        if (!(SFS2D_ABL & 64)) {
+          const uint32_t ka = __builtin_amdgcn_udot4(c >> 8, Q.kmul, 0u, false);   // a1 (n2+1) + a2
+          const uint32_t kr = __builtin_amdgcn_udot4(c, Q.kmul, 0u, false);        // r1 (n2+1) + r2
+          const bool sw = (int)__builtin_amdgcn_udot4(c, 0x01000100u, 0u, false) > Q.fold_thr;
+          atomicAdd(ka ? (uint32_t*)((char*)jh_l + (ka << 2)) : trash_p, 1u);
+          atomicAdd((sw & (kr != 0u)) ? (uint32_t*)((char*)hist_l + (kr << 2)) : trash_p, 1u);
+        }
+        continue;
+      }
       const uint32_t r1 = c & 0xffu, a1 = (c >> 8) & 0xffu, r2 = (c >> 16) & 0xffu, a2 = c >> 24;
       const bool sw = (int)(a1 + a2) > Q.fold_thr;
       const uint32_t x1 = sw ? r1 : a1, x2 = sw ? r2 : a2;
@@ -891,6 +912,17 @@ __device__ __forceinline__ void prep_tile(const KParams& P, const Tile t, uint32
     const uint32_t ia = base + 4 * threadIdx.x;
     const int off = (int)((ia - ab) * 4u);
     x.c = NEED_C ? __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(crs, off, 0, 0)) : make_uint4(0, 0, 0, 0);
+    if (SFS2D_ABL & (1024 | 2048)) {   // timing only: 2 B (1024) or 0 B (2048) of position per SNP, synthetic ids
+      if (SFS2D_ABL & 1024) {
+        uint2 h = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(prs, off / 2, 0, 0));
+        asm volatile("" : "+v"(h.x), "+v"(h.y));
+        x.p = make_uint4(h.x & 0u, 0u, 0u, 0u);
+      } else {
+        x.p = make_uint4(0u, 0u, 0u, 0u);
+      }
+      const uint32_t q = pos[t.cb] + (ia - t.cb) * 56u;
+      x.p.x += q; x.p.y = q + 56u; x.p.z = q + 112u; x.p.w = q + 168u;
+    } else
     x.p = need_pos ? __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(prs, off, 0, 0)) : make_uint4(0, 0, 0, 0);
     x.a = filt ? *reinterpret_cast<const uint2*>(ann + min(ia, alast)) : make_uint2(0, 0);
     x.xp = 0;
@@ -976,11 +1008,31 @@ __device__ __forceinline__ void prep_tile(const KParams& P, const Tile t, uint32
 #endif
   STAMP(22);
   if (err) atomicOr(err_word, err);
-  if (DO_BG) {
+  if (DO_BG && !jnt) {
     b2 = wave_sum_u(b2);
     if (lane == 0 && b2) atomicAdd(&sh_b2, b2);
   }
   if (DO_BG || FST) __syncthreads();
+  if (JNT && jnt) {
+    // the joint histogram's margins into the 1D spectra, its unfolded keys into the 2D bins; the inner
+    // 2D count (bins 1 .. nb2-2) from the finished tile histogram (edge-step SNPs included)
+    const uint32_t n2p1 = (uint32_t)P.n2 + 1u;
+    uint32_t bs = 0;
+    for (int k = threadIdx.x; k < P.nb2; k += BLOCK1) {
+      const uint32_t j = jh_l[k];
+      const uint32_t x1 = (uint32_t)k / n2p1, x2 = (uint32_t)k - x1 * n2p1;
+      if (j) {
+        if (x1) atomicAdd(&sh_hist[P.h1a + (int)x1], j);
+        if (x2) atomicAdd(&sh_hist[P.h1b + (int)x2], j);
+      }
+      const uint32_t v = sh_hist[k] + ((int)(x1 + x2) <= P.fold_thr ? j : 0u);
+      if (k) sh_hist[k] = v;
+      if (k >= 1 && k <= P.nb2 - 2) bs += v;
+    }
+    bs = wave_sum_u(bs);
+    if (lane == 0 && bs) atomicAdd(&sh_b2, bs);
+    __syncthreads();
+  }
   if (FST)
     for (int j = threadIdx.x; j < FST_LDS; j += BLOCK1) {
       unsigned long long qn = 0, qd = 0;
@@ -2596,6 +2648,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
   uint32_t jb = 0;
   auto flush = [&]() {
     MARK(30);
+    if (SFS2D_ABL & 512) { jb = 0; return; }
     // (the lane id and the batch addresses recomputed here: kept live across the window loop they
     // were spilled, and their scratch reloads put an L2 round trip in front of every flush)
     uint32_t ln = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -2635,10 +2688,11 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
         reinterpret_cast<ulonglong2*>(fsum)[Bs] = make_ulonglong2(0ull, 0ull);
       }
     }
-      if (mine && mode_bp) {
+      if (mine && mode_bp && !FSTIN) {
         // the slot is cleared after its read although k_prep rewrites the table every run: without this
         // store the overlapped Fst-free config-3 pass measured 0.194-0.197 vs 0.162-0.174 ms per pass
-        // (profiles/r05r_scan_slot_store_ab.txt; with Fst no difference)
+        // (profiles/r05r_scan_slot_store_ab.txt).  With Fst in the scan it is left out: no difference in
+        // time (profiles/r06g_scan_ablation_noclr.txt) and 8 B fewer scattered writes per window
         uint32_t z = 0u;
         asm volatile("" : "+v"(z));   // (a literal 0 here was taken from a spilled register)
         slots[Bs] = make_uint2(z, z);
@@ -3001,7 +3055,8 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
     // the sums, replicated in every lane (fixed trees: deterministic), into lane jb of the batch
     if (half1d) {
       const double m2 = 2.0 * fM;
-      const double v = wave_sum5(acc2, acca, FSTIN ? fA - m2 : 0.0, FSTIN ? fP - m2 : 0.0, (uint32_t)lane);
+      const double v = (SFS2D_ABL & 256) ? acc2 + acca + (FSTIN ? fA - m2 + fP : 0.0)
+                                         : wave_sum5(acc2, acca, FSTIN ? fA - m2 : 0.0, FSTIN ? fP - m2 : 0.0, (uint32_t)lane);
       MARK(26);
       put5(v, fq);
       if (lane == 0) put_u(s, cur.b, nsnp, n2, n1a, n1b, nvar, nlast);

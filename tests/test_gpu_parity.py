@@ -649,6 +649,44 @@ def test_called_counts_above_sample_size_inside_long_tiles():
     pl.close()
 
 
+@pytest.mark.parametrize("n1p,n2p,fold,ws", [(25, 25, True, 20000), (25, 25, False, 20000), (18, 14, True, 20000),
+                                               (3, 2, True, 1000)])
+def test_prep_joint_histogram(monkeypatch, n1p, n2p, fold, ws):
+    """k_prep's joint (alt1, alt2) histogram (the common step of counts plans: one LDS atomic per SNP
+    plus one per folded SNP, both 1D spectra from its margins at the tile's end) against the three
+    atomics per SNP it replaced (SFS2D_JNT=0): byte-equal records and Fst, both against the oracle, on
+    chromosomes long enough for many common steps (a step is 2,048 SNPs; edge steps and steps with
+    over-called SNPs take the exact classify in the same tiles).  (The 7-bin grid scans 1 kb windows: at
+    20 kb its T1D values of ~4e-4 are differences of ~2e3-sized sums, below 1e-10 relative in fp64 for
+    any evaluation order, the oracle's included.)"""
+    from sfs2d.engine import Engine, ScanConfig
+    from sfs2d.pack import PackedSNPs, pack_counts
+    from sfs2d.synth import synth_genome
+    p = synth_genome(3, [70001, 30000, 9], n1p, n2p, seed=n1p * 13 + n2p + fold)
+    r1, a1 = p.counts & 0xff, (p.counts >> 8) & 0xff
+    r2, a2 = (p.counts >> 16) & 0xff, p.counts >> 24
+    pick = (np.random.default_rng(5).random(p.n) < 0.0005) & (a1 + a2 <= n1p + n2p)
+    q = PackedSNPs(pack_counts(np.where(pick, r1 + 3, r1), a1, r2, a2), p.pos, p.chrom_off, p.chrom_names,
+                   p.ann_id, p.ann_names)
+    eng = Engine.get(0)
+    dev = eng.upload(q)
+    cfg = ScanConfig(n1p=n1p, n2p=n2p, fold=fold, window=ws, fst=True)
+    out = {}
+    for jnt in ("1", "0"):
+        monkeypatch.setenv("SFS2D_JNT", jnt)
+        pl = eng.plan(dev, cfg)
+        pl.run()
+        pl.check()
+        out[jnt] = (pl.read(), pl.read_fst())
+        pl.close()
+    assert out["1"][0].tobytes() == out["0"][0].tobytes()
+    assert out["1"][1].tobytes() == out["0"][1].tobytes()
+    monkeypatch.setenv("SFS2D_JNT", "1")
+    ocfg = O.Cfg(n1p, n2p, fold=fold)
+    bgs = O.chrom_backgrounds(q, ocfg)
+    _records_vs_oracle(q, cfg, ocfg, O.bp_windows(q, ws), lambda c: bgs[c])
+
+
 def _overcall(p, n1p, n2p, frac, seed):
     """Copy of p with a fraction of SNPs made over-called in both populations: called counts r + a above
     2 pop_size with a1 + a2 > n1p + n2p (a joint fold) and r1 + r2 > n (a folded key outside the triangle
