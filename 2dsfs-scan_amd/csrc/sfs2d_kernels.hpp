@@ -64,7 +64,8 @@ constexpr int RCPN = 512;         // (1/k, 1/(k(k-1))) for k < 512 (Fst: called 
 #ifndef SFS2D_ABL   // ablation builds (timing only, results wrong): bit 0 no 2D atomic, 1 no 1D atomics, 2 no D / lp
 #define SFS2D_ABL 0  // reads, 3 no record stores, 4 no Fst table reads, 5 no 1D end pass, 8 no per-window wave
 #endif              // sums, 9 no batched finish; k_prep's common step: 6 no LDS histogram atomics, 7 loads only
-                    // (no classification, histograms or segmentation)
+                    // (no classification, histograms or segmentation); round 6's position-byte probes (10, 11:
+                    // profiles/r06h_prep_position_bytes.txt) are not kept
 constexpr int REPL = 4;           // replicas of the per-chromosome background histograms
 constexpr int PW_MAX_LEAVES = 1024;  // numpy pairwise leaves (64-128 values each): grids up to 255 x 255 (u8 counts)
 constexpr int LEAVES_PER_SLICE = 4;
@@ -912,17 +913,6 @@ __device__ __forceinline__ void prep_tile(const KParams& P, const Tile t, uint32
     const uint32_t ia = base + 4 * threadIdx.x;
     const int off = (int)((ia - ab) * 4u);
     x.c = NEED_C ? __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(crs, off, 0, 0)) : make_uint4(0, 0, 0, 0);
-    if (SFS2D_ABL & (1024 | 2048)) {   // timing only: 2 B (1024) or 0 B (2048) of position per SNP, synthetic ids
-      if (SFS2D_ABL & 1024) {
-        uint2 h = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(prs, off / 2, 0, 0));
-        asm volatile("" : "+v"(h.x), "+v"(h.y));
-        x.p = make_uint4(h.x & 0u, 0u, 0u, 0u);
-      } else {
-        x.p = make_uint4(0u, 0u, 0u, 0u);
-      }
-      const uint32_t q = pos[t.cb] + (ia - t.cb) * 56u;
-      x.p.x += q; x.p.y = q + 56u; x.p.z = q + 112u; x.p.w = q + 168u;
-    } else
     x.p = need_pos ? __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(prs, off, 0, 0)) : make_uint4(0, 0, 0, 0);
     x.a = filt ? *reinterpret_cast<const uint2*>(ann + min(ia, alast)) : make_uint2(0, 0);
     x.xp = 0;
