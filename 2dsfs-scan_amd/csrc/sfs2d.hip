@@ -191,6 +191,7 @@ struct sfs2d_plan {
   int tevery = 1;                // sample every tevery-th run
   int tmask = 7;                 // kernels with events: bit 0 k_prep, 1 k_bg_slice, 2 the scan kernel
   int64_t tseen = 0;             // runs since timing was set
+  hipEvent_t* tpend = nullptr;   // a sampled run's events between its phase 1 and phase 2
   // events of the run being enqueued: k_prep start/stop, scan start/stop (null: not sampled).  They
   // go into the kernels' own dispatch packets (hipExtLaunchKernelGGL), so they stamp the kernel's
   // start and end as the command processor sees them -- the durations rocprofv3 reports.
@@ -1311,9 +1312,15 @@ int sfs2d_plan_run_phase(sfs2d_plan* pl, int phase, sfs2d_window* out_dev) {
   sfs2d_ctx* ctx = pl->ctx;
   if (pl->base) return set_err(ctx, SFS2D_E_ARG, "an attached plan runs with its base plan (sfs2d_plan_attach)");
   HIPCHK(ctx, hipSetDevice(ctx->device));
+  // a sampled run split into phases 1 and 2 (sfs2d_plan_run_streams' staggered / chained runs) keeps
+  // its events from phase 1 to phase 2 (tpend)
   hipEvent_t* te = nullptr;
-  if (pl->timing && phase == 0 && (pl->tseen++ % pl->tevery) == 0 && pl->tcount * 6 < (int)pl->tev.size())
+  if (phase == 2) {
+    te = pl->tpend;
+    pl->tpend = nullptr;
+  } else if (pl->timing && (pl->tseen++ % pl->tevery) == 0 && pl->tcount * 6 < (int)pl->tev.size()) {
     te = &pl->tev[(size_t)pl->tcount * 6];
+  }
   if (!pl->do_bg && !pl->bg_ready && phase != 1)
     return set_err(ctx, SFS2D_E_ARG, "supplied-background plan run before sfs2d_plan_set_background");
   // sampled runs: each kernel carries its start / end events in its own dispatch packet; a kernel
@@ -1335,8 +1342,6 @@ int sfs2d_plan_run_phase(sfs2d_plan* pl, int phase, sfs2d_window* out_dev) {
       HIPCHK(ctx, launch_prep(pl, true));
       if (!prep_runs(pl) && (rc = mark(0))) return rc;
     }
-  } else if ((rc = mark(0))) {
-    return rc;
   }
   if (phase == 0 || phase == 2) {
     if (pl->do_bg && !pl->fused) HIPCHK(ctx, launch_bg_slices(pl));
@@ -1347,11 +1352,10 @@ int sfs2d_plan_run_phase(sfs2d_plan* pl, int phase, sfs2d_window* out_dev) {
     HIPCHK(ctx, launch_scan_any(pl, out));
     pl->last_out = out;
     pl->runs++;
-  } else if ((rc = mark(2)) || (rc = mark(4))) {
-    return rc;
   }
   for (auto& e : pl->kev) e = nullptr;
-  if (te) pl->tcount++;
+  if (te && phase == 1) pl->tpend = te;   // (counted when its phase 2 has run)
+  else if (te) pl->tcount++;
   return 0;
 }
 
@@ -1385,6 +1389,7 @@ int sfs2d_plan_set_timing_kernels(sfs2d_plan* pl, int max_runs, int every, int k
   pl->tev.assign((size_t)max_runs * 6, nullptr);
   for (auto& e : pl->tev) HIPCHK(ctx, hipEventCreate(&e));
   pl->tcount = 0;
+  pl->tpend = nullptr;
   pl->timing = max_runs > 0;
   return 0;
 }
@@ -1443,7 +1448,9 @@ int sfs2d_plan_run_streams(sfs2d_plan* const* plans, void* const* streams, sfs2d
   // (started together, the two k_preps competed and then the two scans, and the streams kept that
   // phase: config 3's 20-step bench loop 0.184 vs 0.190-0.198 ms per pass, without Fst 0.165 vs 0.181;
   // profiles/r05u_stream_stagger_ab.txt).  Not for plans with attached plans: their longer passes
-  // settled into a worse phase staggered (20 kb + 500 kb: 0.328-0.331 vs 0.285-0.286 ms per step)
+  // settled into a worse phase staggered (20 kb + 500 kb: 0.328-0.331 vs 0.285-0.286 ms per step).
+  // Chaining every run's k_prep after the previous run's k_prep (and its scan after the previous scan)
+  // measured slower: 0.1852-0.1857 (0.238-0.248) vs 0.1821-0.1828 ms (profiles/r06l_stream_chain_ab.txt)
   bool stagger = nplans >= 2 && nruns >= 2;
   for (int k = 0; k < nplans; ++k) stagger = stagger && plans[k]->attached.empty();
   if (stagger && !ctx->stagger) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->stagger, hipEventDisableTiming));
