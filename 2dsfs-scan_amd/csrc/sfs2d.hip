@@ -924,7 +924,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
       // scan may sum it), then 8 per-wave histogram blocks (also the fused prologue's scratch: u1 words,
       // 1D proportions, leaf accumulators and sums)
       const int h2w = pl->p16 ? (((K.nb2 + 1) / 2 + 3) & ~3) : ((K.nb2 + 3) & ~3);
-      const int per = h2w + R1 * (K.n1p + 1) + R1 * (K.n2p + 1);   // (no trash words: scan_w_small)
+      const int per = (h2w + R1 * (K.n1p + 1) + R1 * (K.n2p + 1) + 3) & ~3;   // (no trash words: scan_w_small)
       const size_t hist_words = std::max<size_t>((size_t)(SBLOCK / WAVE) * per, (size_t)FUSED_VCNT + K.nt + 16);
       const size_t rt = (prm->flags & SFS2D_F_FST) ? 2 * (size_t)pl->K.rtn : 0;
       pl->scan_lds = sizeof(double) * (size_t)(((K.nt + 1) & ~1) + LNT + LNF + rt) + hist_words * 4;
@@ -1312,7 +1312,7 @@ int sfs2d_plan_run_phase(sfs2d_plan* pl, int phase, sfs2d_window* out_dev) {
   sfs2d_ctx* ctx = pl->ctx;
   if (pl->base) return set_err(ctx, SFS2D_E_ARG, "an attached plan runs with its base plan (sfs2d_plan_attach)");
   HIPCHK(ctx, hipSetDevice(ctx->device));
-  // a sampled run split into phases 1 and 2 (sfs2d_plan_run_streams' staggered / chained runs) keeps
+  // a sampled run split into phases 1 and 2 (sfs2d_plan_run_streams' staggered first run) keeps
   // its events from phase 1 to phase 2 (tpend)
   hipEvent_t* te = nullptr;
   if (phase == 2) {

@@ -71,7 +71,9 @@ constexpr int PW_MAX_LEAVES = 1024;  // numpy pairwise leaves (64-128 values eac
 constexpr int LEAVES_PER_SLICE = 4;
 constexpr int FIN_LDS_BINS = 12288;  // backgrounds with nt <= this keep values / proportions in LDS
 constexpr int TRASH = WAVE;       // lane-private scratch words after each wave's histograms
-constexpr int R1 = 4;             // replicas of the folded 1D window histograms (lane & 3)
+// replicas of the folded 1D window histograms (lane & 3).  Round 6, k_scan_w on config 3 with Fst:
+// 4 / 2 / 1 replicas 131.8-132.7 / 142.8-142.9 / 173.6-174.0 us (profiles/r06m_scan_r1_sb_ab.txt)
+constexpr int R1 = 4;
 #ifndef SFS2D_GW_R1
 #define SFS2D_GW_R1 1
 #endif
@@ -2451,7 +2453,9 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
   constexpr int DT = LNT;   // D(r) entries in LDS
   constexpr int R1U = R1;
   constexpr int NWV = SBLOCK / WAVE;
-  constexpr int SB = 8;    // windows per batch (see flush; LDS-limited: the 2 KB of the retired trash words)
+  // windows per batch (see flush; LDS-limited: the 2 KB of the retired trash words; 16 with two 1D
+  // replicas instead of four measured 1-2 us faster than 8 with two: not worth the replicas)
+  constexpr int SB = 8;
   __shared__ BgHead sh_hb;
   __shared__ double sh_bd[NWV][3][SB];      // batch: the three sums of window j
   __shared__ uint32_t sh_bu[NWV][5][SB];    // batch: slot, begin, n2 | n2_all, n1a | n1b, nsnp | nvar
@@ -2475,7 +2479,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
   uint32_t* HB = reinterpret_cast<uint32_t*>(RT + rtn);
   const int h2w = P16 ? ((P.nb2 + 1) / 2 + 3) & ~3 : (P.nb2 + 3) & ~3;
   const int h1w = R1 * (P.n1p + 1), h1wb = R1 * (P.n2p + 1);
-  const int per = h2w + h1w + h1wb;   // (no trash words: SNPs outside the 2D SFS skip the atomic)
+  const int per = (h2w + h1w + h1wb + 3) & ~3;   // (16-B rows; no trash words: SNPs outside the 2D SFS skip the atomic)
   uint32_t* W = HB + wv * per;
   uint32_t* H1a = W + h2w;
   uint32_t* H1b = H1a + h1w;
@@ -3001,10 +3005,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
     // folded bin k (<= n_p) of a population's spectrum, its replicas read and cleared
     auto take1 = [&](uint32_t* H, int k) -> uint32_t {
       if (SFS2D_ABL & 32) return (uint32_t)k;
-      uint4* q = reinterpret_cast<uint4*>(H + k * R1);
-      const uint4 v = *q;
-      *q = make_uint4(0, 0, 0, 0);
-      return (v.x >> S1) + (v.y >> S1) + (v.z >> S1) + (v.w >> S1);
+      return take_replicas<R1U>(H + k * R1, S1);
     };
     if (half1d) {
       const bool pa = lane < 32;
