@@ -2875,6 +2875,8 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
         if (keep) kw[(j + q) & 7] = word;
         // every SNP slot adds to one bin of each folded 1D spectrum (no range test, no trash select: the
         // window's end drops bins 0 and n_p and counts n1a / n1b from them)
+        // (bin 0 -- the fixed SNPs and every padding slot -- counted by ballot with its atomics on lane-private
+        // words measured slower: profiles/r06p_scan_bin0_ballot_ab.txt)
         const uint32_t u1 = a1b + (gp & 0xffffu), u2 = a2b + (gp >> 16);
         if (!(SFS2D_ABL & 2)) {
           __hip_atomic_fetch_add((lds_u32*)(uintptr_t)u1, one1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
