@@ -188,6 +188,7 @@ struct sfs2d_plan {
   bool timing = false;
   std::vector<hipEvent_t> tev;   // 6 per sampled run (start / end of k_prep, k_bg_slice, the scan)
   int tcount = 0;
+  int tmax = 0;                  // samples of the current timing session (<= tev.size() / 6)
   int tevery = 1;                // sample every tevery-th run
   int tmask = 7;                 // kernels with events: bit 0 k_prep, 1 k_bg_slice, 2 the scan kernel
   int64_t tseen = 0;             // runs since timing was set
@@ -1318,7 +1319,7 @@ int sfs2d_plan_run_phase(sfs2d_plan* pl, int phase, sfs2d_window* out_dev) {
   if (phase == 2) {
     te = pl->tpend;
     pl->tpend = nullptr;
-  } else if (pl->timing && (pl->tseen++ % pl->tevery) == 0 && pl->tcount * 6 < (int)pl->tev.size()) {
+  } else if (pl->timing && (pl->tseen++ % pl->tevery) == 0 && pl->tcount < pl->tmax) {
     te = &pl->tev[(size_t)pl->tcount * 6];
   }
   if (!pl->do_bg && !pl->bg_ready && phase != 1)
@@ -1385,9 +1386,15 @@ int sfs2d_plan_set_timing_kernels(sfs2d_plan* pl, int max_runs, int every, int k
   pl->tseen = 0;
   sfs2d_ctx* ctx = pl->ctx;
   HIPCHK(ctx, hipStreamSynchronize(CTX_STREAM(ctx)));
-  for (auto& e : pl->tev) if (e) hipEventDestroy(e);
-  pl->tev.assign((size_t)max_runs * 6, nullptr);
-  for (auto& e : pl->tev) HIPCHK(ctx, hipEventCreate(&e));
+  // the event ring only grows (turning timing off keeps it): re-arming a sampled loop then costs no
+  // event creation -- hundreds of hipEventCreate calls right before a timed loop left the GPU idle for
+  // milliseconds first
+  if ((size_t)max_runs * 6 > pl->tev.size()) {
+    for (auto& e : pl->tev) if (e) hipEventDestroy(e);
+    pl->tev.assign((size_t)max_runs * 6, nullptr);
+    for (auto& e : pl->tev) HIPCHK(ctx, hipEventCreate(&e));
+  }
+  pl->tmax = max_runs;
   pl->tcount = 0;
   pl->tpend = nullptr;
   pl->timing = max_runs > 0;
