@@ -74,9 +74,6 @@ constexpr int TRASH = WAVE;       // lane-private scratch words after each wave'
 // replicas of the folded 1D window histograms (lane & 3).  Round 6, k_scan_w on config 3 with Fst:
 // 4 / 2 / 1 replicas 131.8-132.7 / 142.8-142.9 / 173.6-174.0 us (profiles/r06m_scan_r1_sb_ab.txt)
 constexpr int R1 = 4;
-#ifndef SFS2D_FLN
-#define SFS2D_FLN 0
-#endif
 #ifndef SFS2D_GW_R1
 #define SFS2D_GW_R1 1
 #endif
@@ -2452,7 +2449,6 @@ template <bool P16, bool FUSED, int FST, bool CNT>
 __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_t nwg, SCAN_W_ARGS) {
   constexpr bool FSTIN = FST >= 2;
   constexpr bool FMASK = FST == 3;
-  constexpr bool FLN = SFS2D_FLN;
   static_assert(!FSTIN || CNT, "Fst in the scan reads the counts");
   constexpr int DT = LNT;   // D(r) entries in LDS
   constexpr int R1U = R1;
@@ -2644,9 +2640,10 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
   // sums' wave reductions run, and the T values, the zero / NaN rules, the Fst value and the 64-B
   // record of up to 64 windows are computed per lane, in one pass (flush)
   uint32_t jb = 0;
-  // FLN: lane j holds ln of window j's totals (n2, n1a, n1b), loaded by that lane alone at the window's end:
+  // lane j holds ln of window j's totals (n2, n1a, n1b), loaded by that lane alone at the window's end:
   // the batched finish then reads no global table (x ln x for x >= LNF came from the global ln table there,
-  // an L2 round trip per finish)
+  // an L2 round trip per finish; config 3's totals are ~300-450).  Overlapped config-3 step 0.1808-0.1810
+  // vs 0.1822-0.1825 ms (profiles/r06r_scan_finish_ln_prefetch_ab.txt)
   double fl2 = 0.0, fla = 0.0, flb = 0.0;
   auto flush = [&]() {
     MARK(30);
@@ -2666,15 +2663,11 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
     const uint32_t Bse = Bsb + nsnp;
     WinOut w;
     w.snp_count = Bnv >> 16; w.n2 = Bn2 & 0xffffu; w.n2_all = Bn2 >> 16; w.n1a = Bn1 & 0xffffu; w.n1b = Bn1 >> 16;
-    if (FLN) {   // ln of the window's totals, loaded into this lane at the window's end (F(x) = x * ln x)
-      w.t2d = 2.0 * (B2 - (double)w.n2 * fl2);
-      w.t1a = 2.0 * (Ba - (double)w.n1a * fla);
-      w.t1b = 2.0 * (Bb - (double)w.n1b * flb);
-    } else {
-      w.t2d = 2.0 * (B2 - xlnx<LNF>(w.n2, Ft, lnx));
-      w.t1a = 2.0 * (Ba - xlnx<LNF>(w.n1a, Ft, lnx));
-      w.t1b = 2.0 * (Bb - xlnx<LNF>(w.n1b, Ft, lnx));
-    }
+    // F(x) = x ln x of the window's totals from the ln values this lane loaded at the window's end
+    // (__dmul_rn: the F table's own rounding, k_init_lnx)
+    w.t2d = 2.0 * (B2 - __dmul_rn((double)w.n2, fl2));
+    w.t1a = 2.0 * (Ba - __dmul_rn((double)w.n1a, fla));
+    w.t1b = 2.0 * (Bb - __dmul_rn((double)w.n1b, flb));
     // |T| this small may be an exactly proportional window: the exact evaluation below
     const bool exact = mine && !empty &&
                        (nsnp == 0xffffu || suspect_zero(w.t2d, w.n2) ||
@@ -3067,7 +3060,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
       MARK(26);
       put5(v, fq);
       if (lane == 0) put_u(s, cur.b, nsnp, n2, n1a, n1b, nvar, nlast);
-      if (FLN && (uint32_t)lane == jb) {
+      if ((uint32_t)lane == jb) {
         fl2 = lnx[min(n2, 0xffffu)];
         fla = lnx[min(n1a, 0xffffu)];
         flb = lnx[min(n1b, 0xffffu)];
@@ -3082,7 +3075,7 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
       }
       MARK(26);
       put(s, cur.b, nsnp, n2, n1a, n1b, nvar, nlast, s2, sa, sb, fq);
-      if (FLN && (uint32_t)lane == jb) {
+      if ((uint32_t)lane == jb) {
         fl2 = lnx[min(n2, 0xffffu)];
         fla = lnx[min(n1a, 0xffffu)];
         flb = lnx[min(n1b, 0xffffu)];
