@@ -968,6 +968,33 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
                    : (pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<true, true, true>, WAVE, gw_lds)
                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_scan_gw<false, true, true>, WAVE, gw_lds));
         if (oe != hipSuccess) occ = 0;
+        // the LDS ln table (KParams::lnl) when it costs no workgroup per CU (config 4's 101 x 101 triangle:
+        // 16 one-wave workgroups either way; config 5's 201 x 151 grid would lose one)
+        {
+          const size_t lds2 = gw_lds + 8 + (size_t)LNL * 8;
+          int occ2 = 0;
+          const bool big = lds2 > 64 * 1024 && lds2 <= 160 * 1024;
+          if (big)
+            for (const void* f : {(const void*)k_scan_gw<true, false, false>, (const void*)k_scan_gw<false, false, false>,
+                                  (const void*)k_scan_gw<true, true, false>, (const void*)k_scan_gw<false, true, false>,
+                                  (const void*)k_scan_gw<true, false, true>, (const void*)k_scan_gw<false, false, true>,
+                                  (const void*)k_scan_gw<true, true, true>, (const void*)k_scan_gw<false, true, true>,
+                                  (const void*)k_scan_gw<true, false, true, true>, (const void*)k_scan_gw<false, false, true, true>,
+                                  (const void*)k_scan_gw<true, true, true, true>, (const void*)k_scan_gw<false, true, true, true>})
+              hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2);
+          const hipError_t oe2 =
+              lds2 > 160 * 1024 ? hipErrorInvalidValue
+              : K.ntri ? (pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, k_scan_gw<true, true, true, true>, WAVE, lds2)
+                                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, k_scan_gw<false, true, true, true>, WAVE, lds2))
+                       : (pl->p16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, k_scan_gw<true, true, true>, WAVE, lds2)
+                                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, k_scan_gw<false, true, true>, WAVE, lds2));
+          const char* lev = std::getenv("SFS2D_LNL");
+          if (oe2 == hipSuccess && occ2 == occ && occ >= 2 && !(lev && lev[0] == '0')) {
+            gw_lds = lds2;
+            K.lnl = pl->K.lnl = 1;
+          }
+          (void)hipGetLastError();
+        }
         pl->gw = occ >= 2;   // measured on 201 x 151 with u16 bins (2 per CU): 22 vs 32 us for k_scan_g
         if (const char* ev = std::getenv("SFS2D_GW")) pl->gw = occ >= 1 && ev[0] == '1';
       }

@@ -142,7 +142,9 @@ struct KParams {
   int ntri;              // k_scan_gw TRI (folded counts plans, n1 = n2 = n): the reachable 2D bins
                          // x1 + x2 <= n, (n+1)(n+2)/2 of them, stored as a triangle (0: full grid)
   int jnt;               // k_prep (counts plans, LDS histogram): the joint (alt1, alt2) histogram, see prep_tile
+  int lnl;               // k_scan_gw: ln(x) for x < LNL in the wave's LDS (when it costs no occupancy)
 };
+constexpr int LNL = 512;   // k_scan_gw's LDS ln table (window totals and 1D bin counts below it)
 
 struct Tile {   // k_prep work item: SNPs [begin, end) of chromosome chrom = [cb, ce), slots from sbase
   uint32_t chrom, begin, end, cb, ce, sbase, nslots, pad1;   // nslots: the chromosome's window slots
@@ -1937,6 +1939,9 @@ __device__ __forceinline__ void scan_gw_body(double* ldsd, SCAN_W_ARGS) {
   const int h1w = RG * (P.n1p + 1), h1wb = RG * (P.n2p + 1);
   const int per = h2w + h1w + h1wb + TRASH;
   uint32_t* W = reinterpret_cast<uint32_t*>(ldsd);
+  // P.lnl: ln(x) for x < LNL after the histograms, copied from the global ln table at the start: the window's
+  // end reads ln of its totals and 1D counts from LDS instead of an L2 round trip per window
+  double* LNLt = reinterpret_cast<double*>(W + ((per + 1) & ~1));
   uint32_t* H1a = W + h2w;
   uint32_t* H1b = H1a + h1w;
   const uint32_t trash = (uint32_t)(h2w + h1w + h1wb + lane);   // word offset from W
@@ -1980,6 +1985,8 @@ __device__ __forceinline__ void scan_gw_body(double* ldsd, SCAN_W_ARGS) {
 
   const BgHead hb = head[bg];
   for (int k = lane; k < per / 4; k += WAVE) reinterpret_cast<uint4*>(W)[k] = make_uint4(0, 0, 0, 0);
+  if (P.lnl)
+    for (int k = lane; k < LNL; k += WAVE) LNLt[k] = lnx[k];
   __syncthreads();
   const bool filt = P.ann_want >= 0;
   const bool half1d = P.n1p <= 33 && P.n2p <= 33;
@@ -2164,7 +2171,11 @@ __device__ __forceinline__ void scan_gw_body(double* ldsd, SCAN_W_ARGS) {
     // with the 1D background terms in registers, so that no wait here is a wait for those rows (loads
     // complete in order; the rows then get the rest of this window's end to arrive)
     auto lnld = [&](uint32_t x) { return lnx[min(x, (uint32_t)LNX_N - 1u)]; };
-    const double ln2 = lnld(n2), ln1a = lnld(n1a), ln1b = lnld(n1b);
+    // ln of the totals from the global table only when the LDS copy is absent or too short (wave-uniform;
+    // the 1D counts are checked below)
+    const bool lq0 = P.lnl && (n2 | n1a | n1b) < (uint32_t)LNL;
+    double ln2 = 0.0, ln1a = 0.0, ln1b = 0.0;
+    if (!lq0) { ln2 = lnld(n2); ln1a = lnld(n1a); ln1b = lnld(n1b); }
     ulonglong2 fq = make_ulonglong2(0ull, 0ull);   // this window's Fst sums (k_prep), used at the end
     if (FST && lane == 0) fq = reinterpret_cast<const ulonglong2*>(fsum)[s];
     if (it == 0) STAMP(12);
@@ -2184,8 +2195,15 @@ __device__ __forceinline__ void scan_gw_body(double* ldsd, SCAN_W_ARGS) {
       }
     }
     double la[2], lb[2];
+    if (lq0 && __ballot((xa[0] | xa[1] | xb[0] | xb[1]) >= (uint32_t)LNL) == 0ull) {
+      ln2 = LNLt[n2]; ln1a = LNLt[n1a]; ln1b = LNLt[n1b];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) { la[j] = lnld(xa[j]); lb[j] = lnld(xb[j]); }
+      for (int j = 0; j < 2; ++j) { la[j] = LNLt[xa[j]]; lb[j] = LNLt[xb[j]]; }
+    } else {
+      if (lq0) { ln2 = lnld(n2); ln1a = lnld(n1a); ln1b = lnld(n1b); }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) { la[j] = lnld(xa[j]); lb[j] = lnld(xb[j]); }
+    }
     __builtin_amdgcn_sched_barrier(0);
     // next window: its slot record is in, issue its first rows now (the record made wave-uniform
     // here: its load, issued at the window's start, was otherwise waited for right there)
