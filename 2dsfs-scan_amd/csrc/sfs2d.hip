@@ -97,6 +97,7 @@ struct sfs2d_ctx {
   double* d_lnx = nullptr;
   double* d_df = nullptr;   // D(r), F(x) (LNT each), then (1/k, 1/(k(k-1))) pairs (RCPN)
   hipEvent_t stagger = nullptr;   // sfs2d_plan_run_streams: the first run's k_prep, awaited by the second stream
+  hipEvent_t chain = nullptr;     // sfs2d_plan_run_streams (SFS2D_CHAIN=1): the last run's k_prep
   std::string err;
   std::mutex err_mu;
 };
@@ -525,6 +526,7 @@ int sfs2d_ctx_destroy(sfs2d_ctx* ctx) {
   hipFree(ctx->d_lnx);
   hipFree(ctx->d_df);
   if (ctx->stagger) hipEventDestroy(ctx->stagger);
+  if (ctx->chain) hipEventDestroy(ctx->chain);
   hipStreamDestroy(ctx->own);
   delete ctx;
   return 0;
@@ -1490,6 +1492,22 @@ int sfs2d_plan_run_streams(sfs2d_plan* const* plans, void* const* streams, sfs2d
   if (stagger && !ctx->stagger) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->stagger, hipEventDisableTiming));
   hipStream_t saved = CTX_STREAM(ctx);
   int rc = 0;
+  // (experiment) SFS2D_CHAIN=1: each run's k_prep waits for the previous run's k_prep (no two k_preps together)
+  const char* cev = std::getenv("SFS2D_CHAIN");
+  if (stagger && cev && cev[0] == '1') {
+    if (!ctx->chain) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->chain, hipEventDisableTiming));
+    for (int i = 0; i < nruns && !rc; ++i) {
+      const int k = i % nplans;
+      ctx->stream = (hipStream_t)streams[k];
+      sfs2d_window* o = outs ? outs[k] : nullptr;
+      if (i && hipStreamWaitEvent(ctx->stream, ctx->chain, 0) != hipSuccess) rc = set_err(ctx, SFS2D_E_HIP, "chain wait");
+      if (!rc) rc = sfs2d_plan_run_phase(plans[k], 1, o);
+      if (!rc && hipEventRecord(ctx->chain, ctx->stream) != hipSuccess) rc = set_err(ctx, SFS2D_E_HIP, "chain event");
+      if (!rc) rc = sfs2d_plan_run_phase(plans[k], 2, o);
+    }
+    ctx->stream = saved;
+    return rc;
+  }
   for (int i = 0; i < nruns && !rc; ++i) {
     const int k = i % nplans;
     ctx->stream = (hipStream_t)streams[k];   // (NULL: the null stream, as sfs2d_ctx_set_stream)

@@ -2797,7 +2797,8 @@ __device__ __forceinline__ void scan_w_small(double* ldsd, uint32_t wgi, uint32_
   while (s < ch.slot_hi) {
     // the batch's last window prefetches nothing: the flush after it (with the rare exact
     // evaluations) then runs with no rows in flight and no row registers live
-    const bool fill = jb + 1u < (uint32_t)SB;
+    const bool fill = jb + 1u < (uint32_t)SB;   // (prefetching here too, the finish with rows in flight, measured
+                                                // slower: 127 VGPRs, profiles/r06u_scan_prefetch_across_finish_ab.txt)
     const bool more = s1 < ch.slot_hi;
     const uint2 sr1u = make_uint2(__builtin_amdgcn_readfirstlane(sr1.x), __builtin_amdgcn_readfirstlane(sr1.y));
     Win nxt;
