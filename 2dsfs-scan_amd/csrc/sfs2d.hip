@@ -1492,17 +1492,19 @@ int sfs2d_plan_run_streams(sfs2d_plan* const* plans, void* const* streams, sfs2d
   if (stagger && !ctx->stagger) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->stagger, hipEventDisableTiming));
   hipStream_t saved = CTX_STREAM(ctx);
   int rc = 0;
-  // (experiment) SFS2D_CHAIN=1: each run's k_prep waits for the previous run's k_prep (no two k_preps together)
+  // (experiment) SFS2D_CHAIN=1: each run's k_prep waits for the previous run's k_prep (no two k_preps together);
+  // =2: only the first 2 * nplans runs' (the streams' starting phase), then free
   const char* cev = std::getenv("SFS2D_CHAIN");
-  if (stagger && cev && cev[0] == '1') {
+  const int nchain = (cev && cev[0] == '2') ? 2 * nplans : nruns;
+  if (stagger && cev && (cev[0] == '1' || cev[0] == '2')) {
     if (!ctx->chain) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->chain, hipEventDisableTiming));
     for (int i = 0; i < nruns && !rc; ++i) {
       const int k = i % nplans;
       ctx->stream = (hipStream_t)streams[k];
       sfs2d_window* o = outs ? outs[k] : nullptr;
-      if (i && hipStreamWaitEvent(ctx->stream, ctx->chain, 0) != hipSuccess) rc = set_err(ctx, SFS2D_E_HIP, "chain wait");
+      if (i && i <= nchain && hipStreamWaitEvent(ctx->stream, ctx->chain, 0) != hipSuccess) rc = set_err(ctx, SFS2D_E_HIP, "chain wait");
       if (!rc) rc = sfs2d_plan_run_phase(plans[k], 1, o);
-      if (!rc && hipEventRecord(ctx->chain, ctx->stream) != hipSuccess) rc = set_err(ctx, SFS2D_E_HIP, "chain event");
+      if (!rc && i < nchain && hipEventRecord(ctx->chain, ctx->stream) != hipSuccess) rc = set_err(ctx, SFS2D_E_HIP, "chain event");
       if (!rc) rc = sfs2d_plan_run_phase(plans[k], 2, o);
     }
     ctx->stream = saved;
