@@ -97,7 +97,6 @@ struct sfs2d_ctx {
   double* d_lnx = nullptr;
   double* d_df = nullptr;   // D(r), F(x) (LNT each), then (1/k, 1/(k(k-1))) pairs (RCPN)
   hipEvent_t stagger = nullptr;   // sfs2d_plan_run_streams: the first run's k_prep, awaited by the second stream
-  hipEvent_t chain = nullptr;     // sfs2d_plan_run_streams (SFS2D_CHAIN=1): the last run's k_prep
   std::string err;
   std::mutex err_mu;
 };
@@ -141,6 +140,7 @@ struct sfs2d_plan {
   bool do_bg = false, do_seg = false, lds_hist = true, bg_ready = false;
   bool seg_synth = false;   // fixed-bp slots from the generator's window offsets (slots_only)
   bool seg_search = false;  // fixed-bp slots by binary search on the positions, k_slots_search (slots_only)
+  bool srch_guess = true;   // k_slots_search starts from interpolated guesses (SFS2D_SRCH_GUESS=0: plain bisection)
   bool fused = false;       // per-chromosome tables built inside k_scan_w (parity-alternating replicas)
   bool sliced = false;      // per-chromosome tables by k_bg_slice without its tail; k_scan_w combines
                             // the leaf sums (parity-alternating inner sums)
@@ -392,7 +392,7 @@ hipError_t launch_slots_only(sfs2d_plan* pl) {
   else if (nw)
     hipExtLaunchKernelGGL(k_slots_search, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, CTX_STREAM(pl->ctx),
                           pl->kev[0], pl->kev[1], 0, pl->data->pos, pl->data->d_chrom_off, pl->d_slot_base,
-                          pl->data->nchrom, (uint32_t)pl->prm.window, (uint32_t)nw, pl->d_slots);
+                          pl->data->nchrom, (uint32_t)pl->prm.window, (uint32_t)nw, pl->d_slots, pl->srch_guess ? 1 : 0);
   return hipGetLastError();
 }
 
@@ -526,7 +526,6 @@ int sfs2d_ctx_destroy(sfs2d_ctx* ctx) {
   hipFree(ctx->d_lnx);
   hipFree(ctx->d_df);
   if (ctx->stagger) hipEventDestroy(ctx->stagger);
-  if (ctx->chain) hipEventDestroy(ctx->chain);
   hipStreamDestroy(ctx->own);
   delete ctx;
   return 0;
@@ -854,6 +853,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   // SFS2D_SEG=prep forces k_prep's segmentation, SFS2D_SEG=search the search (never the generator's
   // offsets: what a real replicate VCF gets); both are selected by tests/test_synth_device.py
   const char* seg_ev = std::getenv("SFS2D_SEG");
+  if (const char* gev = std::getenv("SFS2D_SRCH_GUESS")) pl->srch_guess = gev[0] != '0';
   const bool seg_prep = seg_ev && std::strcmp(seg_ev, "prep") == 0, seg_srch = seg_ev && std::strcmp(seg_ev, "search") == 0;
   if (bp && data->d_win_off && (uint32_t)prm->window == data->win_bp && pl->cnt && !pl->do_bg &&
       pl->nslots == (int64_t)nc * (int64_t)data->win_per_chrom) {
@@ -1486,30 +1486,16 @@ int sfs2d_plan_run_streams(sfs2d_plan* const* plans, void* const* streams, sfs2d
   // profiles/r05u_stream_stagger_ab.txt).  Not for plans with attached plans: their longer passes
   // settled into a worse phase staggered (20 kb + 500 kb: 0.328-0.331 vs 0.285-0.286 ms per step).
   // Chaining every run's k_prep after the previous run's k_prep (and its scan after the previous scan)
-  // measured slower: 0.1852-0.1857 (0.238-0.248) vs 0.1821-0.1828 ms (profiles/r06l_stream_chain_ab.txt)
+  // measured slower: 0.1852-0.1857 (0.238-0.248) vs 0.1821-0.1828 ms (profiles/r06l_stream_chain_ab.txt).
+  // About one 20-run loop in eight settles into a slower phase (0.19-0.216 ms per run, the scans of both
+  // streams overlapping more); the k_prep chain never did in 8 runs but costs ~2% in the typical one, a
+  // chained start made the slow phase likelier (5 of 8), the scan chain is far slower
+  // (profiles/r06v_*, r06w_*, r06x_*)
   bool stagger = nplans >= 2 && nruns >= 2;
   for (int k = 0; k < nplans; ++k) stagger = stagger && plans[k]->attached.empty();
   if (stagger && !ctx->stagger) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->stagger, hipEventDisableTiming));
   hipStream_t saved = CTX_STREAM(ctx);
   int rc = 0;
-  // (experiment) SFS2D_CHAIN=1: each run's k_prep waits for the previous run's k_prep (no two k_preps together);
-  // =2: only the first 2 * nplans runs' (the streams' starting phase), then free
-  const char* cev = std::getenv("SFS2D_CHAIN");
-  const int nchain = (cev && cev[0] == '2') ? 2 * nplans : nruns;
-  if (stagger && cev && (cev[0] == '1' || cev[0] == '2')) {
-    if (!ctx->chain) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->chain, hipEventDisableTiming));
-    for (int i = 0; i < nruns && !rc; ++i) {
-      const int k = i % nplans;
-      ctx->stream = (hipStream_t)streams[k];
-      sfs2d_window* o = outs ? outs[k] : nullptr;
-      if (i && i <= nchain && hipStreamWaitEvent(ctx->stream, ctx->chain, 0) != hipSuccess) rc = set_err(ctx, SFS2D_E_HIP, "chain wait");
-      if (!rc) rc = sfs2d_plan_run_phase(plans[k], 1, o);
-      if (!rc && i < nchain && hipEventRecord(ctx->chain, ctx->stream) != hipSuccess) rc = set_err(ctx, SFS2D_E_HIP, "chain event");
-      if (!rc) rc = sfs2d_plan_run_phase(plans[k], 2, o);
-    }
-    ctx->stream = saved;
-    return rc;
-  }
   for (int i = 0; i < nruns && !rc; ++i) {
     const int k = i % nplans;
     ctx->stream = (hipStream_t)streams[k];   // (NULL: the null stream, as sfs2d_ctx_set_stream)
