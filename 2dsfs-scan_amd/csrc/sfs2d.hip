@@ -140,7 +140,6 @@ struct sfs2d_plan {
   bool do_bg = false, do_seg = false, lds_hist = true, bg_ready = false;
   bool seg_synth = false;   // fixed-bp slots from the generator's window offsets (slots_only)
   bool seg_search = false;  // fixed-bp slots by binary search on the positions, k_slots_search (slots_only)
-  bool srch_guess = true;   // k_slots_search starts from interpolated guesses (SFS2D_SRCH_GUESS=0: plain bisection)
   bool fused = false;       // per-chromosome tables built inside k_scan_w (parity-alternating replicas)
   bool sliced = false;      // per-chromosome tables by k_bg_slice without its tail; k_scan_w combines
                             // the leaf sums (parity-alternating inner sums)
@@ -392,7 +391,7 @@ hipError_t launch_slots_only(sfs2d_plan* pl) {
   else if (nw)
     hipExtLaunchKernelGGL(k_slots_search, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, CTX_STREAM(pl->ctx),
                           pl->kev[0], pl->kev[1], 0, pl->data->pos, pl->data->d_chrom_off, pl->d_slot_base,
-                          pl->data->nchrom, (uint32_t)pl->prm.window, (uint32_t)nw, pl->d_slots, pl->srch_guess ? 1 : 0);
+                          pl->data->nchrom, (uint32_t)pl->prm.window, (uint32_t)nw, pl->d_slots);
   return hipGetLastError();
 }
 
@@ -853,7 +852,6 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
   // SFS2D_SEG=prep forces k_prep's segmentation, SFS2D_SEG=search the search (never the generator's
   // offsets: what a real replicate VCF gets); both are selected by tests/test_synth_device.py
   const char* seg_ev = std::getenv("SFS2D_SEG");
-  if (const char* gev = std::getenv("SFS2D_SRCH_GUESS")) pl->srch_guess = gev[0] != '0';
   const bool seg_prep = seg_ev && std::strcmp(seg_ev, "prep") == 0, seg_srch = seg_ev && std::strcmp(seg_ev, "search") == 0;
   if (bp && data->d_win_off && (uint32_t)prm->window == data->win_bp && pl->cnt && !pl->do_bg &&
       pl->nslots == (int64_t)nc * (int64_t)data->win_per_chrom) {

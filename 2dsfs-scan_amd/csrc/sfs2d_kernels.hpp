@@ -3282,62 +3282,24 @@ __global__ __launch_bounds__(256) void k_slots_bp(const uint32_t* __restrict__ p
 // touches ~6 lines of positions (its deep levels) against the window's whole position run for k_prep
 // (config 4: 358 SNPs = 11 lines).  Writes what k_prep's segmentation writes: (first + 1, last + 1),
 // (0, 0) for an empty window.
-// lower_bound_pos from a guess g: doubling steps out of g bracket the answer, then bisection (a guess off
-// by d costs ~2 log2(d) probes instead of log2(hi - lo))
-__device__ __forceinline__ uint32_t lower_bound_from(const uint32_t* __restrict__ pos, uint32_t lo, uint32_t hi,
-                                                     unsigned long long v, uint32_t g) {
-  if (hi - lo <= 32u) return lower_bound_pos(pos, lo, hi, v);
-  g = min(max(g, lo), hi - 1u);
-  uint32_t step = 16u;
-  if ((unsigned long long)pos[g] < v) {   // the answer is in (g, hi]
-    uint32_t a = g + 1u;
-    for (;;) {
-      const uint32_t t = a + step - 1u;
-      if (t >= hi) return lower_bound_pos(pos, a, hi, v);
-      if ((unsigned long long)pos[t] >= v) return lower_bound_pos(pos, a, t, v);
-      a = t + 1u;
-      step <<= 1;
-    }
-  }
-  uint32_t c = g;                         // pos[c] >= v: the answer is in [lo, c]
-  for (;;) {
-    if (c - lo <= step) return lower_bound_pos(pos, lo, c, v);
-    const uint32_t t = c - step;
-    if ((unsigned long long)pos[t] < v) return lower_bound_pos(pos, t + 1u, c, v);
-    c = t;
-    step <<= 1;
-  }
-}
-
 __global__ __launch_bounds__(256) void k_slots_search(const uint32_t* __restrict__ pos,
                                                       const long long* __restrict__ chrom_off,
                                                       const uint32_t* __restrict__ slot_base, int nchrom, uint32_t ws,
-                                                      uint32_t nslots, uint2* __restrict__ slots, int guess) {
+                                                      uint32_t nslots, uint2* __restrict__ slots) {
+  // (starting from interpolated guesses -- galloping out of the index the chromosome's position range
+  // predicts -- measured slower: 0.75-0.77 vs 0.64 ms per config-4 generation; bisection's upper levels are
+  // lines the wave shares, profiles/r06z_slot_search_guess_ab.txt)
   const uint32_t s = blockIdx.x * 256u + threadIdx.x;
   const uint32_t sc = min(s, nslots - 1u);   // (lanes past the end search too: their neighbours read them)
   int lo = 0, hi = nchrom;                   // chromosome c with slot_base[c] <= sc < slot_base[c+1]
-  // guess: chromosomes of equal slot counts (replicates) take slot s / slots per chromosome, one check
-  const int c0 = guess ? (int)min((unsigned long long)nchrom - 1ull, (unsigned long long)sc * (unsigned)nchrom / nslots) : 0;
-  if (guess && slot_base[c0] <= sc && sc < slot_base[c0 + 1]) {
-    lo = c0;
-  } else {
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (slot_base[mid] <= sc) lo = mid;
-      else hi = mid;
-    }
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (slot_base[mid] <= sc) lo = mid;
+    else hi = mid;
   }
   const uint32_t j = sc - slot_base[lo], ns = slot_base[lo + 1] - slot_base[lo];
   const uint32_t cb = (uint32_t)chrom_off[lo], ce = (uint32_t)chrom_off[lo + 1];
-  // guess: the SNP index the chromosome's position range puts the window start at (positions roughly
-  // uniform: a Poisson stream is off by ~sqrt(n) SNPs)
-  auto lb = [&](uint32_t a, unsigned long long v) -> uint32_t {
-    if (!guess) return lower_bound_pos(pos, a, ce, v);
-    const unsigned long long p0 = pos[cb], p1 = pos[ce - 1u];
-    const double f = p1 > p0 ? ((double)v - (double)p0) / (double)(p1 - p0 + 1ull) : 0.0;
-    const uint32_t g = cb + (uint32_t)fmin(fmax(f, 0.0) * (double)(ce - cb), (double)(ce - cb - 1u));
-    return lower_bound_from(pos, a, ce, v, g);
-  };
+  auto lb = [&](uint32_t a, unsigned long long v) -> uint32_t { return lower_bound_pos(pos, a, ce, v); };
   const uint32_t b = j ? lb(cb, (unsigned long long)j * ws + 1ull) : cb;
   uint32_t e = __shfl_down(b, 1, WAVE);
   const bool lastw = j + 1u == ns;

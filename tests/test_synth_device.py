@@ -101,8 +101,7 @@ def test_slot_search_equals_segmentation(monkeypatch, ws):
     VCFs) take their slot table from k_slots_search (binary search on the resident positions) instead of
     k_prep's segmentation: byte-equal records on data with empty windows (3 kb), windows of one or two
     SNPs, a one-SNP chromosome, and with Fst (k_prep's sums keep k_prep), on small (k_scan_w) and large
-    (k_scan_gw) grids, with and without the search's interpolated starting guesses (chromosomes of unequal
-    slot counts: the chromosome guess falls back to bisection); and the search path against the oracle."""
+    (k_scan_gw) grids; and the search path against the oracle."""
     from oracle import sfs_oracle as O
     from sfs2d import _lib as L
     from sfs2d.engine import Engine, ScanConfig
@@ -118,9 +117,8 @@ def test_slot_search_equals_segmentation(monkeypatch, ws):
         try:
             for fst in (False, True):
                 outs = []
-                for flag in ("search", "search-bisect", "prep"):   # (bisect: no interpolated guesses)
-                    monkeypatch.setenv("SFS2D_SEG", flag.split("-")[0])
-                    monkeypatch.setenv("SFS2D_SRCH_GUESS", "0" if flag.endswith("bisect") else "1")
+                for flag in ("search", "prep"):
+                    monkeypatch.setenv("SFS2D_SEG", flag)
                     pl = eng.plan(dev, ScanConfig(n1p=n, n2p=n, window=ws, bg_mode=L.BG_SUPPLIED, fst=fst))
                     pl.set_background(*bg)
                     for _ in range(2):
@@ -128,7 +126,7 @@ def test_slot_search_equals_segmentation(monkeypatch, ws):
                         pl.check()
                     outs.append(pl.read())
                     pl.close()
-                assert outs[0].tobytes() == outs[1].tobytes() == outs[2].tobytes()
+                assert outs[0].tobytes() == outs[1].tobytes()
             recs = outs[0]
             body = recs[(recs["flags"] & L.W_EMPTY) == 0]
             ref = O.window_records(p, O.bp_windows(p, ws), cfg_o, lambda c: bg)
