@@ -1106,6 +1106,8 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
     if (const char* ev = std::getenv("SFS2D_WGS")) cap = std::max<int64_t>(1, std::atoll(ev));   // tuning
     const double S = (double)std::max<unsigned long long>(1, slot_base[nc] - slot_base[0]);
     const uint32_t NW = pl->gw ? 1u : (uint32_t)(SBLOCK / WAVE);   // wavefronts per workgroup
+    int64_t gw_win = 64;   // k_scan_gw: windows per workgroup of a small chromosome
+    if (const char* ev = std::getenv("SFS2D_GWWIN")) gw_win = std::max<int64_t>(1, std::atoll(ev));   // tuning
     std::vector<double> order;
     for (int c = 0; c < nc; ++c) {
       const uint32_t ns = (uint32_t)(slot_base[c + 1] - slot_base[c]);
@@ -1115,7 +1117,7 @@ static int plan_create(sfs2d_ctx* ctx, const sfs2d_data* data, const sfs2d_param
       // k_scan_gw has no table prologue: many small chromosomes (sims batches: thousands of
       // replicates) get ~64 windows per workgroup instead of one workgroup each, which would leave
       // the last dispatch wave's workgroups running alone
-      if (pl->gw) want = std::max<int64_t>(want, (ns + 63) / 64);
+      if (pl->gw) want = std::max<int64_t>(want, (ns + gw_win - 1) / gw_win);
       const uint32_t nwg = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(wmax, want));
       uint32_t npool = std::min<uint32_t>(nwg, CTR_POOLS);
       if (const char* ev = std::getenv("SFS2D_POOLS")) npool = std::max(1u, std::min<uint32_t>(npool, (uint32_t)std::atoi(ev)));   // tuning
