@@ -1513,6 +1513,107 @@ int sfs2d_plan_run_streams(sfs2d_plan* const* plans, void* const* streams, sfs2d
   return rc;
 }
 
+// A run_streams sequence captured into HIP graphs, one per stream (each a chain of its plans' runs), and
+// replayed with one hipGraphLaunch per stream: short passes (config 2's 1e6-SNP chromosome, ~12 us of
+// GPU time per pass) are host-bound when each of their three launches is enqueued on its own.  One graph
+// holding all the streams' chains as parallel branches (forked and joined through events) measured 6-9x
+// slower than run_streams (0.066-0.107 vs 0.0117 ms per pass, profiles/r06ad_*): the replay does not
+// overlap the branches the way independent streams do.  The runs' kernel arguments (parity-selected
+// buffers, output pointers) are fixed at capture: every plan runs an even number of times per replay, so
+// its buffer parity is the same before and after each replay, and a replay refuses to start when a plan
+// ran an odd number of times since the capture.
+struct sfs2d_graph {
+  sfs2d_ctx* ctx = nullptr;
+  std::vector<hipStream_t> streams;
+  std::vector<hipGraph_t> graphs;
+  std::vector<hipGraphExec_t> execs;
+  std::vector<sfs2d_plan*> plans;
+  std::vector<int64_t> par;
+};
+
+static void graph_free(sfs2d_graph* g) {
+  for (auto& x : g->execs) if (x) hipGraphExecDestroy(x);
+  for (auto& x : g->graphs) if (x) hipGraphDestroy(x);
+  delete g;
+}
+
+int sfs2d_graph_create(sfs2d_plan* const* plans, void* const* streams, sfs2d_window* const* outs, int nplans,
+                       int nruns, sfs2d_graph** out) {
+  if (!plans || !streams || !out || nplans < 1 || nruns < 1) return SFS2D_E_ARG;
+  *out = nullptr;
+  sfs2d_ctx* ctx = plans[0] ? plans[0]->ctx : nullptr;
+  if (!ctx) return SFS2D_E_ARG;
+  if (nruns % (2 * nplans))
+    return set_err(ctx, SFS2D_E_ARG, "a graph holds an even number of runs of every plan (nruns % (2 * nplans) == 0)");
+  for (int k = 0; k < nplans; ++k) {
+    if (!plans[k] || plans[k]->ctx != ctx) return set_err(ctx, SFS2D_E_ARG, "plans must share one ctx");
+    for (int j = 0; j < k; ++j)
+      if (plans[j] == plans[k]) return set_err(ctx, SFS2D_E_ARG, "a plan may appear once (its per-run state is not shareable)");
+    if (plans[k]->timing) return set_err(ctx, SFS2D_E_ARG, "a plan with timing on cannot be captured");
+    if (plans[k]->base) return set_err(ctx, SFS2D_E_ARG, "an attached plan runs with its base plan (sfs2d_plan_attach)");
+    if (!streams[k]) return set_err(ctx, SFS2D_E_ARG, "graph capture needs non-null streams");
+  }
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  sfs2d_graph* g = new sfs2d_graph;
+  g->ctx = ctx;
+  for (int k = 0; k < nplans; ++k) {
+    hipStream_t s = (hipStream_t)streams[k];
+    if (std::find(g->streams.begin(), g->streams.end(), s) == g->streams.end()) g->streams.push_back(s);
+  }
+  hipStream_t saved = CTX_STREAM(ctx);
+  int rc = 0;
+  hipError_t e = hipSuccess;
+  for (hipStream_t s : g->streams) {
+    // run i of the sequence is plan i % nplans on its stream: this stream's chain, in sequence order
+    e = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+    if (e != hipSuccess) break;
+    ctx->stream = s;
+    for (int i = 0; i < nruns && !rc; ++i) {
+      const int k = i % nplans;
+      if ((hipStream_t)streams[k] == s) rc = sfs2d_plan_run_phase(plans[k], 0, outs ? outs[k] : nullptr);
+    }
+    hipGraph_t gr = nullptr;
+    e = hipStreamEndCapture(s, &gr);
+    g->graphs.push_back(gr);
+    hipGraphExec_t x = nullptr;
+    if (!rc && e == hipSuccess) e = hipGraphInstantiate(&x, gr, nullptr, nullptr, 0);
+    g->execs.push_back(x);
+    if (rc || e != hipSuccess) break;
+  }
+  ctx->stream = saved;
+  if (rc || e != hipSuccess) {
+    graph_free(g);
+    return rc ? rc : set_err(ctx, SFS2D_E_HIP, std::string("graph capture: ") + hipGetErrorString(e));
+  }
+  for (int k = 0; k < nplans; ++k) {
+    g->plans.push_back(plans[k]);
+    g->par.push_back(plans[k]->runs & 1);
+  }
+  *out = g;
+  return 0;
+}
+
+int sfs2d_graph_launch(sfs2d_graph* g, int nlaunch) {
+  if (!g || nlaunch < 0) return SFS2D_E_ARG;
+  sfs2d_ctx* ctx = g->ctx;
+  for (size_t k = 0; k < g->plans.size(); ++k)
+    if ((g->plans[k]->runs & 1) != g->par[k])
+      return set_err(ctx, SFS2D_E_ARG, "a captured plan ran an odd number of times since the capture");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  for (int i = 0; i < nlaunch; ++i)
+    for (size_t j = 0; j < g->execs.size(); ++j) HIPCHK(ctx, hipGraphLaunch(g->execs[j], g->streams[j]));
+  return 0;
+}
+
+int sfs2d_graph_destroy(sfs2d_graph* g) {
+  if (!g) return SFS2D_E_ARG;
+  hipSetDevice(g->ctx->device);
+  for (hipStream_t s : g->streams) hipStreamSynchronize(s);   // (no replay in flight)
+  graph_free(g);
+  return 0;
+}
+
 int sfs2d_plan_bg_buffer(sfs2d_plan* pl, void** dev_ptr, int64_t* nbytes) {
   if (!pl || !dev_ptr || !nbytes) return SFS2D_E_ARG;
   // the replica buffer the next run's k_prep accumulates into (fused plans alternate two)

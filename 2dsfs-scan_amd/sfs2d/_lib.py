@@ -41,7 +41,7 @@ EXPORTS = [
     "sfs2d_plan_destroy", "sfs2d_scan", "sfs2d_plan_set_timing", "sfs2d_plan_timing_read",
     "sfs2d_plan_stats", "sfs2d_plan_grids", "sfs2d_plan_scan_kernel", "sfs2d_plan_attach", "sfs2d_data_synth_sims",
     "sfs2d_data_read", "sfs2d_plan_run_streams", "sfs2d_ctx_use_own_stream", "sfs2d_bg_hist_dev", "sfs2d_plan_bg_rows_dev", "sfs2d_plan_bg_rows_set_dev",
-    "sfs2d_ctx_get_stream", "sfs2d_plan_set_fst_out",
+    "sfs2d_ctx_get_stream", "sfs2d_plan_set_fst_out", "sfs2d_graph_create", "sfs2d_graph_launch", "sfs2d_graph_destroy",
 ]
 ABI_VERSION = 2   # SFS2D_ABI_VERSION of include/sfs2d.h
 
@@ -114,6 +114,9 @@ def lib():
     L.sfs2d_plan_run.argtypes = [vp, vp]
     L.sfs2d_plan_run_many.argtypes = [vp, C.c_int, vp]
     L.sfs2d_plan_run_streams.argtypes = [vp, vp, vp, C.c_int, C.c_int]
+    L.sfs2d_graph_create.argtypes = [vp, vp, vp, C.c_int, C.c_int, C.POINTER(vp)]
+    L.sfs2d_graph_launch.argtypes = [vp, C.c_int]
+    L.sfs2d_graph_destroy.argtypes = [vp]
     L.sfs2d_plan_set_timing_sampled.argtypes = [vp, C.c_int, C.c_int]
     L.sfs2d_plan_set_timing_kernels.argtypes = [vp, C.c_int, C.c_int, C.c_int]
     L.sfs2d_plan_fst_read.argtypes = [vp, vp, i64]

@@ -252,6 +252,23 @@ class Plan:
         oh = (C.c_void_p * k)(*[o or None for o in out_dev_ptrs]) if out_dev_ptrs else None
         eng.check(eng.lib.sfs2d_plan_run_streams(ph, sh, oh, k, int(nruns)))
 
+    @staticmethod
+    def graph(plans, streams, nruns: int, out_dev_ptrs=None):
+        """``run_streams(plans, streams, nruns, out_dev_ptrs)`` captured once into a HIP graph
+        (sfs2d_graph_create, one graph per stream): ``RunGraph.launch(n)`` replays it n times, one
+        hipGraphLaunch per stream and replay.
+        `nruns` a multiple of 2 * len(plans); streams non-null HIP stream handles."""
+        k = len(plans)
+        eng = plans[0].eng
+        if any(not s for s in streams):
+            raise ValueError("Plan.graph: non-null stream handles")
+        ph = (C.c_void_p * k)(*[p.h.value for p in plans])
+        sh = (C.c_void_p * k)(*[int(s) for s in streams])
+        oh = (C.c_void_p * k)(*[o or None for o in out_dev_ptrs]) if out_dev_ptrs else None
+        h = C.c_void_p()
+        eng.check(eng.lib.sfs2d_graph_create(ph, sh, oh, k, int(nruns), C.byref(h)))
+        return RunGraph(eng, h, list(plans), int(nruns))
+
     def check(self):
         self.eng.check(self.eng.lib.sfs2d_plan_check(self.h))
 
@@ -306,6 +323,28 @@ class Plan:
             if self.base is not None and self in self.base.attached:
                 self.base.attached.remove(self)
             self.eng.lib.sfs2d_plan_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class RunGraph:
+    """A captured run sequence (Plan.graph / sfs2d_graph_*): `runs` plan runs per launch."""
+
+    def __init__(self, eng, h, plans, runs):
+        self.eng, self.h, self.plans, self.runs = eng, h, plans, runs
+
+    def launch(self, n: int = 1):
+        """Replay n times, on the capture streams (each replay after the stream's earlier work)."""
+        self.eng.check(self.eng.lib.sfs2d_graph_launch(self.h, int(n)))
+
+    def close(self):
+        if self.h:
+            self.eng.lib.sfs2d_graph_destroy(self.h)
             self.h = C.c_void_p()
 
     def __del__(self):

@@ -254,7 +254,17 @@ class Ctx:
         return t.item()
 
 
-def run_loop(cx, plans, steps, warmup, label, time_kernels=False):
+def sample_every(passes_per_plan):
+    """Every how many passes (per plan) a timed loop's kernels carry start / end events: 2 sampled passes
+    per plan, the first and the last one (a perturbed last pass shifts no later pass).  The events perturb the two streams' overlap: at 20 steps,
+    sampling every 2nd pass per plan put 1-2 of 8 runs of the driver's command into the slow phase
+    (0.19-0.22 ms), every pass 4 of 8, every 10th none (0.180-0.183 ms, profiles/r06ac_*).
+    SFS2D_BENCH_EVERY overrides."""
+    ev = os.environ.get("SFS2D_BENCH_EVERY")
+    return int(ev) if ev else max(1, passes_per_plan - 1)
+
+
+def run_loop(cx, plans, steps, warmup, label, time_kernels=False, graph_runs=0):
     """The timed loop shared by both workloads: `warmup` untimed rounds, then exactly `steps` passes
     round-robin over the plans (plan i % S on stream i % S), then (N > 1) ONE all-gather of every
     rank's final window table; barrier + synchronize on both sides, the max over ranks.  Returns the
@@ -297,9 +307,25 @@ def run_loop(cx, plans, steps, warmup, label, time_kernels=False):
 
     plans[0].run(optrs[0])
     plans[0].check()
+    # graph_runs > 0: the run sequence captured once into a HIP graph of graph_runs runs (Plan.graph),
+    # replayed steps / graph_runs times -- one host launch per replay instead of three per run
+    rg = None
+    if graph_runs:
+        if steps % graph_runs or time_kernels:
+            raise ValueError(f"{label}: graph of {graph_runs} runs, {steps} steps (timing: {time_kernels})")
+        rg = Plan.graph(plans, sstreams, graph_runs, optrs)
+
+    def enqueue(n):
+        if rg is not None:
+            rg.launch(-(-n // graph_runs))
+            return -(-n // graph_runs) * graph_runs
+        Plan.run_streams(plans, sstreams, n, optrs)
+        return n
+
+    every = sample_every(-(-steps // len(plans)))
     if time_kernels:   # the timing events made now: re-armed right before the timed steps at no cost
         for q in plans:
-            q.set_timing(steps, every=max(1, min(4, steps // 10)), kernels=5)
+            q.set_timing(steps, every=every, kernels=5)
             q.set_timing(0)
     # device settle (untimed): passes for SETTLE_S of wall time before the warmup, so that the timed
     # steps run at the GPU's sustained clock rather than on its ramp out of idle (a 100-step timed loop
@@ -307,24 +333,23 @@ def run_loop(cx, plans, steps, warmup, label, time_kernels=False):
     t_s = time.perf_counter()
     settle = 0
     while time.perf_counter() - t_s < SETTLE_S:
-        Plan.run_streams(plans, sstreams, 8 * ns, optrs)
+        settle += enqueue(8 * ns)
         torch.cuda.synchronize()
-        settle += 8 * ns
-    Plan.run_streams(plans, sstreams, warmup * ns, optrs)
+    enqueue(warmup * ns)
     gather_final(last, False)
     torch.cuda.synchronize()
     if cx.world > 1:
         dist.barrier()
     # k_prep / scan-kernel durations over the timed steps themselves (start / end events in the
-    # kernels' dispatch packets of >= 10 of the timed passes -- every pass cost 2% of the step time, every
-    # 4th ~0.5%): the overlapped launches the roofline prices
+    # kernels' dispatch packets of 2 timed passes per plan, sample_every): the overlapped launches the
+    # roofline prices
     if time_kernels:
         for q in plans:
-            q.set_timing(steps, every=max(1, min(4, steps // 10)), kernels=5)
+            q.set_timing(steps, every=every, kernels=5)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev[0].record(cx.scan_s)
-    Plan.run_streams(plans, sstreams, steps, optrs)
+    enqueue(steps)
     gather_final(last, True)
     t_enq = time.perf_counter() - t0   # host time to enqueue the timed steps (diagnostic)
     torch.cuda.synchronize()
@@ -352,6 +377,8 @@ def run_loop(cx, plans, steps, warmup, label, time_kernels=False):
         allr = g.cpu().numpy().reshape(-1, 64)
     else:
         allr = mine
+    if rg is not None:
+        rg.close()
     return {"dt": dt, "device_ms": dev_ms, "gather_ms": gat_ms, "t_enq": t_enq, "rows": rows,
             "gathered": allr, "mine": mine, "streams": ns, "settle_passes": settle,
             "k_timed_ms": k_timed, "k_timed_samples": nk}
@@ -432,9 +459,10 @@ def run_loop_gathered(cx, plans, steps, warmup, label, nstreams=2, time_kernels=
     torch.cuda.synchronize()
     for q in plans:
         q.check()
+    every = sample_every(-(-steps // len(plans)))
     if time_kernels:   # the timing events made now: re-armed right before the timed steps at no cost
         for q in plans:
-            q.set_timing(steps, every=max(1, min(4, steps // 10)), kernels=5)
+            q.set_timing(steps, every=every, kernels=5)
             q.set_timing(0)
     t_s = time.perf_counter()
     settle = 0
@@ -447,7 +475,7 @@ def run_loop_gathered(cx, plans, steps, warmup, label, nstreams=2, time_kernels=
     dist.barrier()
     if time_kernels:
         for q in plans:
-            q.set_timing(steps, every=max(1, min(4, steps // 10)), kernels=5)
+            q.set_timing(steps, every=every, kernels=5)
     torch.cuda.synchronize()
     g0 = g
     t0 = time.perf_counter()
@@ -643,13 +671,17 @@ def config2_weak(cx, args):
     cfg = ScanConfig(n1p=POP, n2p=POP, window=WS, fst=True)
     ns = max(1, args.streams)
     steps = max(args.steps, args.config2_steps)
+    gr = 0
     if cx.world > 1:   # every pass's table gathered, groups of P passes over the ns streams
         P = next(k for k in (args.group, 4, 2, 1) if k >= 1 and steps % k == 0)
         plans = [cx.eng.plan(dev, cfg) for _ in range(max(P, ns))]
         r = run_loop_gathered(cx, plans, steps, max(args.warmup, 20), "config 2", nstreams=ns)
     else:
         plans = [cx.eng.plan(dev, cfg) for _ in range(ns)]
-        r = run_loop(cx, plans, steps, max(args.warmup, 20), "config 2")
+        gr = 2 * ns * args.config2_graph if args.config2_graph > 0 else 0
+        if gr:
+            steps = -(-steps // gr) * gr
+        r = run_loop(cx, plans, steps, max(args.warmup, 20), "config 2", graph_runs=gr)
     k1, k2, k3 = kernel_times(plans[0])
     one = single_pass_ms(cx, plans[0], 40) if cx.rank == 0 else None
     nrec, grids, kname = plans[0].nrec, plans[0].grids(), plans[0].scan_kernel()
@@ -668,6 +700,7 @@ def config2_weak(cx, args):
                         "per-chromosome background, T2D + T1D + Fst",
             "windows_per_gpu": nwin, "windows_all_gpus": total,
             "parallelism": f"one chromosome per GPU, {len(plans)} plans on {ns} HIP streams (passes overlap)"
+                           + (f"; replayed as a HIP graph of {gr} runs" if cx.world == 1 and gr else "")
                            + ("; every pass's table (records + Fst) all-gathered over RCCL, overlapped with the "
                               f"next passes (groups of {r.get('group')})" if cx.world > 1 else ""),
             "kernels_ms": {"k_prep": k1, "k_bg_slice": k2, kname: k3},
@@ -734,7 +767,7 @@ def config4_sims(cx, args):
         torch.cuda.synchronize()
     steps = max(2, min(args.steps, args.sims_steps))
     for q in plans:
-        q.set_timing(steps, every=max(1, min(4, steps // 10)), kernels=5)
+        q.set_timing(steps, every=1, kernels=5)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     Plan.run_streams(plans, streams, C4_GEN * steps, None)
@@ -826,8 +859,12 @@ def main():
     ap.add_argument("--no-e2e", action="store_true", help="skip the VCF -> CSV end-to-end timing")
     ap.add_argument("--no-config2", action="store_true", help="skip the config-2 (weak scaling) key")
     ap.add_argument("--no-variants", action="store_true", help="skip the config-3 run without Fst")
-    ap.add_argument("--streams", type=int, default=3, help="config 2: plans / HIP streams (passes overlap)")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="config 2: plans / HIP streams (passes overlap); 0: 4 at N = 1 (replayed as HIP graphs), 3 at N > 1")
     ap.add_argument("--config2-steps", type=int, default=400, help="config 2: at least this many passes")
+    ap.add_argument("--config2-graph", type=int, default=8,
+                    help="config 2 at N = 1: k > 0 replays per-stream HIP graphs of 2 k runs per plan (Plan.graph), "
+                         "0: run_streams")
     ap.add_argument("--no-sims", action="store_true", help="skip the config-4 / config-5 keys")
     ap.add_argument("--sims-steps", type=int, default=5, help="config 4: timed passes over the 4 generations")
     ap.add_argument("--c4-seg", default="search", choices=["search", "prep"],
@@ -840,6 +877,11 @@ def main():
     # hardware queues per process: HIP maps streams onto GPU_MAX_HW_QUEUES queues (4 on the box); the
     # pass streams + the library's and torch's own need more than 4 or two passes share a queue and
     # serialise (profiles/r02h_*).  Set before the HIP runtime starts (rank processes inherit it).
+    if args.streams <= 0:
+        # config 2, measured at N = 1 (profiles/r06ad3*): 4 streams replayed as graphs 2.65-2.75e8
+        # windows/s, 3 streams 2.41e8, 2 1.97e8, 5-6 1.4-1.6e8; without graphs 4 streams are host-bound
+        # (2.30-2.63e8).  N > 1 keeps the 3 measured with the all-gather stream beside them.
+        args.streams = 4 if args.gpus == 1 else 3
     need = max(2, args.streams) + 4
     if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < need:
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(8, need)))
@@ -907,7 +949,7 @@ def main():
                          "ms": r0["scan_ms"], "algorithmic_bytes": b3,
                          "note": r0["scan_kernel"] + " on rank 0's shard: 4 B/SNP + 96 B/slot per launch over its average "
                                  "duration in the timed steps (start / end events in the kernels' dispatch packets, "
-                                 ">= 10 timed passes of both plans, overlapped with the other stream's k_prep; alone on one "
+                                 "2 timed passes per plan, overlapped with the other stream's k_prep; alone on one "
                                  "stream: rank0.scan_alone_ms); traffic: " + (tsrc or "no PMC pass committed")},
             "roofline_pipeline": {"bound": "hbm", "achieved": bp / step_s / 1e9, "peak": HBM_PEAK_GBS * world,
                                   "unit": "GB/s", "frac": bp / step_s / 1e9 / (HBM_PEAK_GBS * world),

@@ -35,7 +35,8 @@ extern "C" {
 #endif
 
 /* 2 (round 5-6): sfs2d_ctx_set_stream(ctx, NULL) selects the HIP null stream (1: the ctx's own),
- * sfs2d_ctx_use_own_stream / sfs2d_ctx_get_stream added, the sfs2d_dist_* entry points removed */
+ * sfs2d_ctx_use_own_stream / sfs2d_ctx_get_stream added, the sfs2d_dist_* entry points removed;
+ * sfs2d_graph_* added (round 6, additive) */
 #define SFS2D_ABI_VERSION 2
 
 /* status codes */
@@ -72,6 +73,7 @@ extern "C" {
 typedef struct sfs2d_ctx sfs2d_ctx;
 typedef struct sfs2d_data sfs2d_data;
 typedef struct sfs2d_plan sfs2d_plan;
+typedef struct sfs2d_graph sfs2d_graph;
 
 typedef struct {
   int32_t n1p, n2p;       /* pop1_size, pop2_size: diploid individuals (twoDSFS_class.py:22); grid (2n1p+1)x(2n2p+1) */
@@ -186,6 +188,19 @@ int sfs2d_plan_run_many(sfs2d_plan* plan, int nruns, sfs2d_window* out_dev);
  * only). */
 int sfs2d_plan_run_streams(sfs2d_plan* const* plans, void* const* streams, sfs2d_window* const* outs, int nplans,
                            int nruns);
+/* the same run sequence captured once into HIP graphs, one per distinct stream (that stream's runs in
+ * sequence order), and replayed by sfs2d_graph_launch: one hipGraphLaunch per stream and replay instead of
+ * a launch per kernel (short passes are host-bound otherwise).  nruns must be a multiple of 2 * nplans
+ * (every plan runs an even number of times per replay, so its buffer parity is unchanged); streams
+ * non-null; no plan with timing on or attached.  The outputs are fixed at capture.  Replays run on the
+ * capture streams, each after that stream's earlier work, without run_streams' staggered start.  A launch
+ * fails with SFS2D_E_ARG when a captured plan ran an odd number of times since the capture.  Not a
+ * reference interface: repeated scans of the same data (the bench's loops; replicate loops as
+ * sims_scan.py:593-644). */
+int sfs2d_graph_create(sfs2d_plan* const* plans, void* const* streams, sfs2d_window* const* outs, int nplans,
+                       int nruns, sfs2d_graph** out);
+int sfs2d_graph_launch(sfs2d_graph* graph, int nlaunch);
+int sfs2d_graph_destroy(sfs2d_graph* graph);
 /* copy the last run's records to host (synchronises the stream) */
 int sfs2d_plan_read(sfs2d_plan* plan, sfs2d_window* out_host, int64_t cap, int64_t* nrec_out);
 /* device pointers of the plan's per-chromosome background histogram replicas (uint32), for a

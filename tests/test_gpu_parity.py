@@ -243,6 +243,67 @@ def test_run_streams_overlapped_plans(fst, nplans):
     dev.close()
 
 
+@pytest.mark.parametrize("fst,nplans", [(True, 3), (False, 2), (True, 1)])
+def test_graph_replay(fst, nplans):
+    """sfs2d_graph_*: a run_streams sequence captured into a HIP graph and replayed writes the same
+    records and Fst as one plan run alone, every replay (outputs cleared in between); a capture of an
+    odd number of runs per plan, or with timing on, is refused, and so is a replay after a plan ran an
+    odd number of times since the capture (its buffer parity changed); an even number brings it back."""
+    import torch
+    from sfs2d import _lib as L
+    from sfs2d.engine import Engine, Plan, ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(2, [200000, 60000], 25, 25, seed=5151)
+    eng = Engine.get(0)
+    dev = eng.upload(p)
+    cfg = ScanConfig(n1p=25, n2p=25, window=20000, fst=fst)
+    ref = eng.plan(dev, cfg)
+    ref.run()
+    ref.check()
+    want = ref.read()
+    want_f = ref.read_fst() if fst else None
+    plans = [eng.plan(dev, cfg) for _ in range(nplans)]
+    streams = [torch.cuda.Stream(device=0).cuda_stream for _ in range(nplans)]
+    outs = [torch.zeros((plans[0].nrec, 64), dtype=torch.uint8, device="cuda:0") for _ in range(nplans)]
+    optrs = [o.data_ptr() for o in outs]
+    with pytest.raises(L.Sfs2dError):
+        Plan.graph(plans, streams, 2 * nplans + nplans, optrs)
+    plans[0].set_timing(4)
+    with pytest.raises(L.Sfs2dError):
+        Plan.graph(plans, streams, 2 * nplans, optrs)
+    plans[0].set_timing(0)
+    g = Plan.graph(plans, streams, 4 * nplans, optrs)
+
+    def check_all():
+        torch.cuda.synchronize()
+        for k, q in enumerate(plans):
+            q.check()
+            got = np.frombuffer(outs[k].cpu().numpy().tobytes(), dtype=L.WINDOW_DTYPE)
+            assert got.tobytes() == want.tobytes(), k
+            if fst:
+                assert np.array_equal(q.read_fst(), want_f, equal_nan=True), k
+
+    for rep in range(3):
+        for o in outs:
+            o.zero_()
+        torch.cuda.synchronize()
+        g.launch(rep + 1)
+        check_all()
+    plans[0].run(optrs[0])
+    with pytest.raises(L.Sfs2dError):
+        g.launch()
+    plans[0].run(optrs[0])
+    for o in outs:
+        o.zero_()
+    torch.cuda.synchronize()
+    g.launch(2)
+    check_all()
+    g.close()
+    for q in plans + [ref]:
+        q.close()
+    dev.close()
+
+
 def test_run_streams_none_is_the_engine_stream():
     """Plan.run_streams with None entries enqueues on the engine's current stream (its own stream by
     default, sfs2d_ctx_get_stream), so read() -- which synchronises that stream only -- returns the
