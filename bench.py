@@ -537,6 +537,27 @@ def kernel_times(plan, runs=16):
     return k1, k2, k3
 
 
+def dense_kernel_samples(cx, plans, passes, every):
+    """Untimed, after the timed loop: `passes` more passes over the same plans and streams, every
+    `every`-th pass per plan carrying kernel start / end events -- more sampled launches of the
+    overlapped k_prep / scan than the timed loop's 2 per plan, at a density that leaves the streams'
+    phase alone (events on every pass move the two streams into the phase where their scans overlap:
+    0.275 ms per scan launch instead of ~0.19, profiles/r06ah_*; sample_every).
+    Returns (k_prep ms, scan ms, launches sampled)."""
+    from sfs2d.engine import Plan
+    ns = len(plans)
+    for q in plans:
+        q.set_timing(passes, every=every, kernels=5)
+    Plan.run_streams(plans, cx.streams[:ns], passes)
+    cx.torch.cuda.synchronize()
+    kt = [q.timing_read() for q in plans]
+    for q in plans:
+        q.set_timing(0)
+        q.check()
+    nk = sum(n for n, _ in kt)
+    return (sum(n * k[0] for n, k in kt) / max(1, nk), sum(n * k[2] for n, k in kt) / max(1, nk), nk)
+
+
 def single_pass_ms(cx, plan, runs=10):
     """One plan back to back on one stream: the latency of a single pass (no overlap)."""
     torch = cx.torch
@@ -591,6 +612,7 @@ def config3_strong(cx, args):
         total_windows = n_windows(r["gathered"])
     win_rank = n_windows(r["mine"])
     k1, _, k3 = kernel_times(plans[0])
+    dense = dense_kernel_samples(cx, plans, 400, 10) if cx.rank == 0 else None
     # a single scan of the genome as a user runs it: the default plan (no scan grid cap), back to back
     # on one stream
     one = None
@@ -655,6 +677,8 @@ def config3_strong(cx, args):
            "rank0": {"snps": sub.n, "windows": win_rank, "slots": nrec,
                      "k_prep_ms": r["k_timed_ms"][0], "scan_ms": r["k_timed_ms"][1],
                      "timed_samples": r["k_timed_samples"], "k_prep_alone_ms": k1, "scan_alone_ms": k3,
+                     "dense_samples": dense and dense[2], "k_prep_dense_ms": dense and dense[0],
+                     "scan_dense_ms": dense and dense[1],
                      "scan_kernel": kname, "single_stream_pass_ms": one,
                      "single_stream_pass_windows_per_s": win_rank / (one * 1e-3) if one else None,
                      "scan_grid_threads": grids[1]}}
@@ -950,7 +974,12 @@ def main():
                          "note": r0["scan_kernel"] + " on rank 0's shard: 4 B/SNP + 96 B/slot per launch over its average "
                                  "duration in the timed steps (start / end events in the kernels' dispatch packets, "
                                  "2 timed passes per plan, overlapped with the other stream's k_prep; alone on one "
-                                 "stream: rank0.scan_alone_ms); traffic: " + (tsrc or "no PMC pass committed")},
+                                 "stream: rank0.scan_alone_ms); traffic: " + (tsrc or "no PMC pass committed"),
+                         "dense_check": ({"ms": r0["scan_dense_ms"], "launches": r0["dense_samples"],
+                                          "frac": b3 / (r0["scan_dense_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                          "note": "the same kernel over 400 untimed passes after the timed loop "
+                                                  "on the same 2 streams, every 10th pass per plan sampled"}
+                                         if r0.get("scan_dense_ms") else None)},
             "roofline_pipeline": {"bound": "hbm", "achieved": bp / step_s / 1e9, "peak": HBM_PEAK_GBS * world,
                                   "unit": "GB/s", "frac": bp / step_s / 1e9 / (HBM_PEAK_GBS * world),
                                   "note": "whole step over all GPUs (SURVEY 8(d): 12 B/SNP + 64 B/window) over "
