@@ -537,25 +537,33 @@ def kernel_times(plan, runs=16):
     return k1, k2, k3
 
 
-def dense_kernel_samples(cx, plans, passes, every):
-    """Untimed, after the timed loop: `passes` more passes over the same plans and streams, every
-    `every`-th pass per plan carrying kernel start / end events -- more sampled launches of the
-    overlapped k_prep / scan than the timed loop's 2 per plan, at a density that leaves the streams'
-    phase alone (events on every pass move the two streams into the phase where their scans overlap:
-    0.275 ms per scan launch instead of ~0.19, profiles/r06ah_*; sample_every).
+def dense_kernel_samples(cx, plans, loops, steps):
+    """Untimed, after the timed loop: `loops` more loops of `steps` passes over the same plans and
+    streams, each started and sampled as the timed loop is (staggered start, synchronised at its end,
+    kernel events on each plan's first and last pass, sample_every) -- the timed loop's condition
+    repeated, so that the overlapped k_prep / scan durations rest on 2 x plans x loops launches instead of
+    2 x plans.  (One long unsynchronised loop drifts between the streams' two phases, and events on every
+    pass put it in the slow one: 0.19-0.26 / 0.275 ms per scan launch, profiles/r06ah, r06ai.)
     Returns (k_prep ms, scan ms, launches sampled)."""
     from sfs2d.engine import Plan
     ns = len(plans)
-    for q in plans:
-        q.set_timing(passes, every=every, kernels=5)
-    Plan.run_streams(plans, cx.streams[:ns], passes)
-    cx.torch.cuda.synchronize()
-    kt = [q.timing_read() for q in plans]
+    every = sample_every(-(-steps // ns))
+    acc = [0, 0.0, 0.0]
+    for _ in range(loops):
+        for q in plans:
+            q.set_timing(steps, every=every, kernels=5)
+        Plan.run_streams(plans, cx.streams[:ns], steps)
+        cx.torch.cuda.synchronize()
+        for q in plans:
+            n, k = q.timing_read()
+            acc[0] += n
+            acc[1] += n * k[0]
+            acc[2] += n * k[2]
     for q in plans:
         q.set_timing(0)
         q.check()
-    nk = sum(n for n, _ in kt)
-    return (sum(n * k[0] for n, k in kt) / max(1, nk), sum(n * k[2] for n, k in kt) / max(1, nk), nk)
+    nk = max(1, acc[0])
+    return (acc[1] / nk, acc[2] / nk, acc[0])
 
 
 def single_pass_ms(cx, plan, runs=10):
@@ -612,7 +620,7 @@ def config3_strong(cx, args):
         total_windows = n_windows(r["gathered"])
     win_rank = n_windows(r["mine"])
     k1, _, k3 = kernel_times(plans[0])
-    dense = dense_kernel_samples(cx, plans, 400, 10) if cx.rank == 0 else None
+    dense = dense_kernel_samples(cx, plans, 10, args.steps) if cx.rank == 0 else None
     # a single scan of the genome as a user runs it: the default plan (no scan grid cap), back to back
     # on one stream
     one = None
@@ -977,8 +985,8 @@ def main():
                                  "stream: rank0.scan_alone_ms); traffic: " + (tsrc or "no PMC pass committed"),
                          "dense_check": ({"ms": r0["scan_dense_ms"], "launches": r0["dense_samples"],
                                           "frac": b3 / (r0["scan_dense_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                                          "note": "the same kernel over 400 untimed passes after the timed loop "
-                                                  "on the same 2 streams, every 10th pass per plan sampled"}
+                                          "note": "the same kernel over 10 more untimed loops of the timed loop's "
+                                                  "passes, plans, streams and sampling (dense_kernel_samples)"}
                                          if r0.get("scan_dense_ms") else None)},
             "roofline_pipeline": {"bound": "hbm", "achieved": bp / step_s / 1e9, "peak": HBM_PEAK_GBS * world,
                                   "unit": "GB/s", "frac": bp / step_s / 1e9 / (HBM_PEAK_GBS * world),
