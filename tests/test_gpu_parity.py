@@ -243,6 +243,43 @@ def test_run_streams_overlapped_plans(fst, nplans):
     dev.close()
 
 
+def test_graph_replay_snp_windows_large_grid():
+    """Config 5's bench shape replayed as HIP graphs (bench.py config5_snpwin): 500-SNP windows at pop
+    100/75 (201 x 151 grid, k_scan_gw), per-chromosome backgrounds, 4 plans on 4 streams -- every
+    replay's records byte-equal to one plan run alone (whose SNP-window records the oracle pins in
+    test_large_grid_kernels / the bySNPs goldens)."""
+    import torch
+    from sfs2d import _lib as L
+    from sfs2d.engine import Engine, Plan, ScanConfig
+    from sfs2d.synth import synth_genome
+    p = synth_genome(2, [40000, 25000], 100, 75, seed=6262)
+    eng = Engine.get(0)
+    dev = eng.upload(p)
+    cfg = ScanConfig(n1p=100, n2p=75, window_mode=L.WINDOW_SNPS, window=500)
+    ref = eng.plan(dev, cfg)
+    ref.run()
+    ref.check()
+    want = ref.read()
+    plans = [eng.plan(dev, cfg) for _ in range(4)]
+    streams = [torch.cuda.Stream(device=0).cuda_stream for _ in range(4)]
+    outs = [torch.zeros((plans[0].nrec, 64), dtype=torch.uint8, device="cuda:0") for _ in range(4)]
+    g = Plan.graph(plans, streams, 16, [o.data_ptr() for o in outs])
+    for rep in range(2):
+        for o in outs:
+            o.zero_()
+        torch.cuda.synchronize()
+        g.launch(rep + 1)
+        torch.cuda.synchronize()
+        for k, q in enumerate(plans):
+            q.check()
+            got = np.frombuffer(outs[k].cpu().numpy().tobytes(), dtype=L.WINDOW_DTYPE)
+            assert got.tobytes() == want.tobytes(), (rep, k)
+    g.close()
+    for q in plans + [ref]:
+        q.close()
+    dev.close()
+
+
 @pytest.mark.parametrize("fst,nplans", [(True, 3), (False, 2), (True, 1)])
 def test_graph_replay(fst, nplans):
     """sfs2d_graph_*: a run_streams sequence captured into a HIP graph and replayed writes the same
