@@ -13,8 +13,9 @@ from sfs2d.engine import Engine, ScanConfig  # noqa: E402
 from sfs2d.synth import synth_genome  # noqa: E402
 
 which = sys.argv[1] if len(sys.argv) > 1 else "config2"
-if which == "config5":   # 201 x 151 grid, 500-SNP windows (large-grid kernels, k_bg_slice with its tail)
-    p = synth_genome(1, 1_000_000, 100, 75, seed=55)
+if which in ("config5", "config5b"):   # 201 x 151 grid, 500-SNP windows (large-grid kernels, k_bg_slice with its tail)
+    # config5b: the bench's shape, 4 chromosomes x 250,000 SNPs (4 backgrounds)
+    p = synth_genome(1, 1_000_000, 100, 75, seed=55) if which == "config5" else synth_genome(4, 250_000, 100, 75, seed=2024)
     cfg = ScanConfig(n1p=100, n2p=75, window_mode=L.WINDOW_SNPS, window=500)
 else:
     nch = int(sys.argv[2]) if len(sys.argv) > 2 else 32   # config3 [chromosomes]: a rank's share
@@ -72,7 +73,7 @@ print(which, f"k_scan_w waves: {live.sum()}  windows/wave min/med/max {w[live,1]
       f"  end min/med/max {en[live].min():.1f}/{np.median(en[live]):.1f}/{en[live].max():.1f} us")
 if which != "config2":
     # workgroups are interleaved over the grid: block b scans chromosome b % 32 (equal chromosomes)
-    nc = 32 if which == "config5" else nch
+    nc = {"config5": 32, "config5b": 4}.get(which) or nch
     chrom = (np.arange(nb * 8) // 8) % nc
     ce = [(en[chrom == c].min(), en[chrom == c].max(), int(w[chrom == c, 1].sum())) for c in range(nc)]
     print(which, "per chromosome end min-max / windows:", " ".join(f"{a:.0f}-{b:.0f}/{n}" for a, b, n in ce))
