@@ -1738,12 +1738,16 @@ int sfs2d_plan_check(sfs2d_plan* pl) {
 // diagnostic: stamps of a -DSFS2D_STAMPS build (returns SFS2D_E_ARG in the shipped build)
 int sfs2d__debug_stamps(unsigned long long* out64) {
 #ifdef SFS2D_STAMPS
-  // 64 phase stamps, then per-block (start, end) of k_prep and k_scan_w (2 x 4096 x 2), then per wave
+  // 64 phase stamps, then per-block (start, end) of k_prep and k_scan_w (2 x 4096 x 2), then per wave,
+  // then k_bg_slice per block
   if (hipMemcpyFromSymbol(out64, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 64) != hipSuccess) return SFS2D_E_HIP;
   if (hipMemcpyFromSymbol(out64 + 64, HIP_SYMBOL(g_blk), sizeof(unsigned long long) * 2 * 4096 * 2) != hipSuccess)
     return SFS2D_E_HIP;
   // then k_scan_w per wavefront (end, windows): 4096 x 8 x 2
   if (hipMemcpyFromSymbol(out64 + 64 + 2 * 4096 * 2, HIP_SYMBOL(g_wv), sizeof(unsigned long long) * 4096 * 8 * 2) != hipSuccess)
+    return SFS2D_E_HIP;
+  // then k_bg_slice per block (start, work done): 1024 x 2
+  if (hipMemcpyFromSymbol(out64 + 64 + 2 * 4096 * 2 + 4096 * 8 * 2, HIP_SYMBOL(g_bgs), sizeof(unsigned long long) * 1024 * 2) != hipSuccess)
     return SFS2D_E_HIP;
   return 0;
 #else

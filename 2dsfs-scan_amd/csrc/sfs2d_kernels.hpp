@@ -218,6 +218,12 @@ __device__ unsigned long long g_blk[2][4096][2];   // per-block start / end (k_p
     if (threadIdx.x == 0) g_stamps[i] = __builtin_amdgcn_s_memrealtime();                        \
   } while (0)
 __device__ unsigned long long g_wv[4096 * 8][2];   // k_scan_w per wavefront: end, windows scanned
+__device__ unsigned long long g_bgs[1024][2];      // k_bg_slice per block (x + y * gridDim.x): start, work done
+#define BGS_STAMP(e)                                                                             \
+  do {                                                                                           \
+    const unsigned bi = blockIdx.x + blockIdx.y * gridDim.x;                                     \
+    if (threadIdx.x == 0 && bi < 1024) g_bgs[bi][e] = __builtin_amdgcn_s_memrealtime();          \
+  } while (0)
 #define WV_STAMP(n)                                                                              \
   do {                                                                                           \
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096) {                                          \
@@ -237,6 +243,9 @@ __device__ unsigned long long g_wv[4096 * 8][2];   // k_scan_w per wavefront: en
   } while (0)
 #define BLK_STAMP(k, e) \
   do {                  \
+  } while (0)
+#define BGS_STAMP(e) \
+  do {               \
   } while (0)
 #endif
 
@@ -1220,6 +1229,7 @@ __global__ __launch_bounds__(KBLOCK) void k_bg_slice(KParams P, uint32_t* __rest
   const int s = blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & (WAVE - 1);
+  BGS_STAMP(0);
   if (s > nslices) {   // the extra workgroups (background 0's row only): Fst per window, using the
                        // GPU while this kernel's table blocks wait on memory
     if (b == 0) {
@@ -1338,6 +1348,7 @@ __global__ __launch_bounds__(KBLOCK) void k_bg_slice(KParams P, uint32_t* __rest
     }
   }
 
+  BGS_STAMP(1);
   if (!tail) return;
   // completion: the last block of this background combines (threadfence-reduction pattern)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");

@@ -27,21 +27,30 @@ pl = eng.plan(dev, cfg)
 for _ in range(3):
     pl.run()
 pl.check()
-buf = (C.c_ulonglong * (64 + 2 * 4096 * 2 + 4096 * 8 * 2))()
+buf = (C.c_ulonglong * (64 + 2 * 4096 * 2 + 4096 * 8 * 2 + 1024 * 2))()
 assert L.lib().sfs2d__debug_stamps(buf) == 0
 t = list(buf[:64])
 blk = list(buf[64:64 + 16384])
-wvs = np.array(buf[64 + 16384:], dtype=np.int64).reshape(4096 * 8, 2)
+wvs = np.array(buf[64 + 16384:64 + 16384 + 65536], dtype=np.int64).reshape(4096 * 8, 2)
+bgs = np.array(buf[64 + 16384 + 65536:], dtype=np.int64).reshape(1024, 2)
 def d(a, b):
     return (t[b] - t[a]) * 0.01 if t[a] and t[b] else float("nan")
 print(which, "K1 blk0: zero %.2f  loop %.2f  flush %.2f us" % (d(20, 21), d(21, 22), d(22, 23)))
-print(which, "K2 slice0: repl+p/lp %.2f  leaves %.2f us; tail block: %.2f us" % (d(0, 1), d(1, 2), d(3, 4)))
+print(which, "K2 slice0: repl+p/lp %.2f  leaves %.2f us; slice0 end -> tail start %.2f us; tail block: %.2f us" % (
+    d(0, 1), d(1, 2), d(2, 3), d(3, 4)))
 print(which, "K3 blk0: prologue %.2f  2D pass(1st) %.2f  1D+clear %.2f  reduce+store %.2f  rest %.2f us" % (
     d(10, 11), d(11, 12), d(12, 13), d(13, 14), d(14, 15)))
 print(which, "K3 fused prologue: replicas %.2f  1D+leaves %.2f  tree %.2f  logs %.2f  zero %.2f us" % (
     d(10, 16), d(16, 17), d(17, 18), d(18, 19), d(19, 11)))
 print(which, "K3 sliced prologue: D/F copy %.2f  lp copy %.2f  leaf tree %.2f  head %.2f  zero %.2f us" % (
     d(10, 24), d(24, 25), d(25, 26), d(26, 27), d(27, 11)))
+nb_s = int((bgs[:, 0] > 0).sum())
+if nb_s:   # k_bg_slice blocks (x + y * gridDim.x): start and work-done times from the earliest start
+    g0 = bgs[:nb_s, 0].min()
+    st_s, en_s = (bgs[:nb_s, 0] - g0) * 0.01, (bgs[:nb_s, 1] - g0) * 0.01
+    slow = np.argsort(en_s)[-6:]
+    print(which, f"k_bg_slice: blocks {nb_s}  start max {st_s.max():.2f}  done p50/max {np.median(en_s):.2f}/{en_s.max():.2f} us;"
+          " latest blocks (index: start-done):", " ".join(f"{i}:{st_s[i]:.1f}-{en_s[i]:.1f}" for i in slow))
 print(which, "gaps: K1end->K2start %.2f  K2end->K3start %.2f us" % (d(23, 0), d(4, 10)))
 
 # per-block spans (us) of the last run: k_prep = 0, k_scan_w = 1
